@@ -1,0 +1,142 @@
+"""ctypes front-end of the CPU oracle (oracle/libptoracle.so) — TEST INFRASTRUCTURE.
+
+Only tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg import this module.
+It maps a recorded uniform stream (tests/golden/*.json, the exact effect.set* calls the reference
+setup scripts make) onto the oracle's frame struct and runs the restated fragment programs.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libptoracle.so")
+
+SCENES = {"cornell": 0, "gltf": 1}
+
+c_f = ctypes.c_float
+c_i = ctypes.c_int32
+F16 = c_f * 16
+
+
+class Frame(ctypes.Structure):
+    _fields_ = [
+        ("scene", c_i), ("width", c_i), ("height", c_i),
+        ("uResolution", c_f * 2), ("uRandomVec2", c_f * 2),
+        ("uULen", c_f), ("uVLen", c_f), ("uTime", c_f),
+        ("uFrameCounter", c_f), ("uSampleCounter", c_f),
+        ("uEPS_intersect", c_f), ("uApertureSize", c_f), ("uFocusDistance", c_f),
+        ("uCameraIsMoving", c_i),
+        ("uCameraMatrix", F16), ("uLeftSphereInvMatrix", F16), ("uRightSphereInvMatrix", F16),
+        ("uGLTF_Model_InvMatrix", F16),
+        ("uQuadLightPlaneSelectionNumber", c_f), ("uQuadLightRadius", c_f),
+        ("uRightSphereMatType", c_i), ("uModelMaterialType", c_i),
+        ("uModelUsesAlbedoTexture", c_i), ("uModelUsesBumpTexture", c_i),
+        ("uModelUsesMetallicTexture", c_i), ("uModelUsesEmissiveTexture", c_i),
+        ("blueNoise", ctypes.c_void_p),
+        ("aabb", ctypes.c_void_p), ("aabbTexels", ctypes.c_int64),
+        ("tri", ctypes.c_void_p), ("triTexels", ctypes.c_int64),
+        ("albedo", ctypes.c_void_p), ("albedoW", c_i), ("albedoH", c_i),
+        ("bump", ctypes.c_void_p), ("bumpW", c_i), ("bumpH", c_i),
+        ("metallic", ctypes.c_void_p), ("metallicW", c_i), ("metallicH", c_i),
+        ("emissive", ctypes.c_void_p), ("emissiveW", c_i), ("emissiveH", c_i),
+    ]
+
+
+class Counters(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in
+                ("paths", "segments", "node_fetches", "leaf_tests", "hit_lookups", "rgba8_taps", "stack_overflow")]
+
+    def as_dict(self):
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.run(["make", "-s", "-C", HERE], check=True)
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.POINTER
+        L.pto_path_trace.argtypes = [P(Frame), ctypes.c_void_p, ctypes.c_void_p, c_i, c_i, c_i, P(Counters)]
+        L.pto_gbuffer.argtypes = [P(Frame), ctypes.c_void_p, c_i, c_i, c_i]
+        L.pto_screen_output.argtypes = [c_i, c_i, ctypes.c_void_p, c_f, c_f, ctypes.c_void_p, c_i]
+        L.pto_math_probe.argtypes = [c_i, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
+        _lib = L
+    return _lib
+
+
+class Scene:
+    """Keeps the sampler arrays alive and builds Frame structs from recorded uniforms."""
+
+    def __init__(self, scene, width, height, bluenoise, bvh=None, tri=None):
+        self.scene = scene
+        self.width, self.height = width, height
+        self.bluenoise = np.ascontiguousarray(bluenoise, dtype=np.uint8)
+        self.bvh = None if bvh is None else np.ascontiguousarray(bvh, dtype=np.float32)
+        self.tri = None if tri is None else np.ascontiguousarray(tri, dtype=np.float32)
+
+    def frame(self, uniforms):
+        f = Frame()
+        f.scene = SCENES[self.scene]
+        f.width, f.height = self.width, self.height
+        for name, (kind, vals) in uniforms.items():
+            if not hasattr(f, name):
+                continue
+            cur = getattr(f, name)
+            if isinstance(cur, ctypes.Array):
+                for i, v in enumerate(vals):
+                    cur[i] = v
+            else:
+                setattr(f, name, int(vals[0]) if kind == "i" else float(vals[0]))
+        f.blueNoise = self.bluenoise.ctypes.data
+        if self.bvh is not None:
+            f.aabb = self.bvh.ctypes.data
+            f.aabbTexels = self.bvh.size // 4
+            f.tri = self.tri.ctypes.data
+            f.triTexels = self.tri.size // 4
+        return f
+
+    def path_trace(self, uniforms, prev, row0=0, row1=None, nthreads=0):
+        row1 = self.height if row1 is None else row1
+        f = self.frame(uniforms)
+        prev = np.ascontiguousarray(prev, dtype=np.float32)
+        out = prev.copy()
+        cnt = Counters()
+        rc = lib().pto_path_trace(ctypes.byref(f), prev.ctypes.data, out.ctypes.data, row0, row1, nthreads, ctypes.byref(cnt))
+        if rc != 0:
+            raise RuntimeError("pto_path_trace failed: %d" % rc)
+        return out, cnt.as_dict()
+
+    def gbuffer(self, uniforms, row0=0, row1=None, nthreads=0):
+        row1 = self.height if row1 is None else row1
+        f = self.frame(uniforms)
+        g = np.zeros((row1 - row0, self.width, 11), dtype=np.float32)
+        rc = lib().pto_gbuffer(ctypes.byref(f), g.ctypes.data, row0, row1, nthreads)
+        if rc != 0:
+            raise RuntimeError("pto_gbuffer failed: %d" % rc)
+        return g
+
+
+def screen_output(acc, one_over_n, exposure=1.0):
+    acc = np.ascontiguousarray(acc, dtype=np.float32)
+    h, w = acc.shape[:2]
+    out = np.zeros((h, w, 4), dtype=np.uint8)
+    rc = lib().pto_screen_output(w, h, acc.ctypes.data, one_over_n, exposure, out.ctypes.data, 0)
+    if rc != 0:
+        raise RuntimeError("pto_screen_output failed")
+    return out
+
+
+def math_probe(op, x, y=None):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = None if y is None else np.ascontiguousarray(y, dtype=np.float32)
+    out = np.zeros_like(x)
+    rc = lib().pto_math_probe(op, x.ctypes.data, None if y is None else y.ctypes.data, out.ctypes.data, x.size)
+    if rc != 0:
+        raise RuntimeError("bad op")
+    return out
