@@ -1,0 +1,94 @@
+// pt_args.h — kernel-argument layouts shared by the C-ABI host code (pt_capi.cpp) and the gfx950
+// kernels (pt_kernels.hip). Passed by value as kernarg segments (scalar-loaded, wave-uniform).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_glsl.h"
+
+namespace pt {
+
+constexpr int kBlock = 256;          // 4 waves; a block shades a 16x16 pixel tile
+constexpr int kTile = 16;            // tile edge == row-band height used for sharding
+constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing_FragmentShader.js:95
+constexpr int kStackLds = 12;        // levels kept in LDS per lane; deeper levels go to scratch
+
+enum Counter { C_PATHS, C_SEGMENTS, C_NODE, C_LEAF, C_HIT, C_RGBA8, C_OVERFLOW, C_NUM };
+enum ErrBits { E_STACK = 1u };
+
+// material enum of js/PathTracingCommon.js:330-350 (the subset the implemented scenes use)
+enum Mat { LIGHT = 0, DIFFUSE = 1, TRANSPARENT = 2, METAL = 3, CLEARCOAT_DIFFUSE = 4, PBR_MATERIAL = 10 };
+
+struct QuadArg {            // struct Quad of the scene shaders (js/GLTFModelPathTracing_FragmentShader.js:39)
+    ptg::f3 normal, v0, v1, v2, v3, color;
+    int type;
+};
+
+// the two triangles of quad i (QuadIntersect = TriangleIntersect(v0,v1,v2) min (v0,v2,v3)) with
+// the edge vectors v1-v0, v2-v0 evaluated once on the host (same IEEE subtraction as the GLSL)
+struct TriArg {
+    ptg::f3 v0, e1, e2;
+};
+
+struct SphereArg {          // UnitSphere + its inverse transform uniform
+    ptg::m4 inv;
+    ptg::f3 color;
+    int type;
+};
+
+struct Tex8 {               // RGBA8 sampler: texels row-major from row 0 (invertY applied at upload)
+    const uchar4* p;
+    int w, h;
+};
+
+// Per-draw kernel arguments. Wave-uniform: read with scalar loads from the kernarg segment; the
+// per-object loops index them dynamically so they are re-read from the scalar cache instead of
+// being hoisted into (vector) registers.
+struct TraceArgs {
+    int width, height;      // render target
+    int num_parts, part;    // row-band sharding (pt_set_row_partition)
+    // common uniforms (js/PathTracingCommon.js:357-368)
+    float res[2], rnd[2];
+    float ulen, vlen, frame, eps, aperture, focus;
+    int moving;
+    ptg::m4 cam, model;
+    // SetupScene() hoisted to the host: identical IEEE ops, evaluated once per frame
+    SphereArg sph[2];
+    TriArg qtri[12];
+    ptg::f3 qnormal[6], qcolor[6];
+    int qtype[6];
+    QuadArg light;          // quads[5], sampled by sampleAxisAlignedQuadLight
+    float light_r2;         // distance(v0,v1)*distance(v0,v3) of quads[5]
+    // glTF material switches (js/GLTFModelPathTracing_FragmentShader.js:21-25)
+    int model_mat, uses_albedo, uses_bump, uses_metal, uses_emissive;
+    // samplers
+    const float4* prev;
+    float4* out;
+    Tex8 bluenoise;
+    const float4* aabb;
+    long long aabb_texels;
+    const float4* tri;
+    long long tri_texels;
+    Tex8 albedo, bump, metal, emissive;
+    // diagnostics
+    unsigned long long* counters;   // C_NUM entries, only with counting builds
+    unsigned* err;                  // ErrBits
+};
+
+struct OutputArgs {
+    int width, height;      // output (canvas or render target) size
+    int acc_w, acc_h;       // accumulation texture size (texelFetch bounds)
+    float one_over_n, exposure;
+    const float4* acc;
+    uchar4* canvas;         // RGBA8 target (NULL when writing float)
+    float4* out_f;          // RGBA32F target (NULL when writing the canvas)
+};
+
+struct CopyArgs {
+    int width, height;
+    int num_parts, part;
+    const float4* src;
+    float4* dst;
+};
+
+} // namespace pt

@@ -1,0 +1,733 @@
+// pt_capi.cpp — the C ABI of libpt.so (include/pt.h): contexts, effects, textures, render
+// targets and draws, mirroring the Babylon effect API the reference's setup scripts call.
+//
+// What happens on pt_render(effect, target), per recognised program:
+//   CORNELL / GLTF  -> uniforms resolved by name, SetupScene() evaluated once on the host with the
+//                      same IEEE ops as the GLSL, one pt_trace launch over the 16-row bands this
+//                      context owns (pt_set_row_partition);
+//   SCREEN_COPY     -> pt_copy over the owned bands;
+//   SCREEN_OUTPUT   -> pt_output into the canvas (RGBA8) or an RGBA32F target.
+// Everything is enqueued on the context's stream; HIP events bracket every draw for timing.
+#include "../../include/pt.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <set>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "pt_args.h"
+
+extern "C" {
+hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s);
+hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
+hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
+hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
+}
+
+namespace {
+
+enum TexKind { TEX_F32 = 0, TEX_U8 = 1, TEX_RT = 2 };
+constexpr int kProgSlots = 8;
+
+struct Uniform {
+    int n = 0;
+    bool is_int = false;
+    bool set = false;
+    float f[16] = {};
+    int i = 0;
+};
+
+}  // namespace
+
+struct pt_texture {
+    pt_ctx* ctx = nullptr;
+    int kind = TEX_F32;
+    int w = 0, h = 0;
+    void* d = nullptr;
+    size_t bytes = 0;
+    int sampling = PT_SAMPLING_NEAREST;
+    int invert_y = 0;
+    bool external = false;   // caller-owned device memory (pt_render_target_wrap)
+};
+
+struct pt_effect {
+    pt_ctx* ctx = nullptr;
+    int prog = PT_PROG_UNKNOWN;
+    std::unordered_map<std::string, Uniform> uniforms;
+    std::unordered_map<std::string, pt_texture*> samplers;
+};
+
+struct pt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    uchar4* canvas = nullptr;
+    int cw = 0, ch = 0;
+    unsigned* d_err = nullptr;
+    unsigned long long* d_counters = nullptr;
+    bool counting = false;
+    int num_parts = 1, part = 0;
+    hipEvent_t ev0[kProgSlots] = {}, ev1[kProgSlots] = {};
+    bool ev_used[kProgSlots] = {};
+    // timing window: per draw event pairs, reused across windows
+    bool window = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+    std::vector<std::pair<int, int>> window_draws;   // (program, pool index)
+    int pending = -1;
+    std::set<pt_texture*> textures;
+    std::set<pt_effect*> effects;
+};
+
+namespace {
+
+int fail(pt_ctx* c, int code, const std::string& msg)
+{
+    if (c) c->err = msg;
+    return code;
+}
+
+int hipfail(pt_ctx* c, hipError_t e, const char* what)
+{
+    return fail(c, PT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(c, call)                                   \
+    do {                                                  \
+        hipError_t e_ = (call);                           \
+        if (e_ != hipSuccess) return hipfail(c, e_, #call); \
+    } while (0)
+
+bool contains(const char* s, const char* pat) { return s && std::strstr(s, pat) != nullptr; }
+
+// Recognise the program from the GLSL registered in Effect.ShadersStore (the reference passes
+// `BABYLON.Effect.ShadersStore["...FragmentShader"]` as `fragmentShader`).
+int classify(const char* src)
+{
+    if (contains(src, "uniform sampler2D pathTracedImageBuffer")) return PT_PROG_SCREEN_COPY;
+    if (contains(src, "uniform sampler2D accumulationBuffer")) return PT_PROG_SCREEN_OUTPUT;
+    if (!contains(src, "pathtracing_default_main")) return PT_PROG_UNKNOWN;
+    if (contains(src, "uniform sampler2D tHDRTexture")) return PT_PROG_HDRI;
+    if (contains(src, "uniform mat4 uTorusInvMatrix")) return PT_PROG_QUADRIC;
+    if (contains(src, "pathtracing_physical_sky_functions")) return PT_PROG_SKY;
+    if (contains(src, "uniform sampler2D tAABBTexture")) return PT_PROG_GLTF;
+    if (contains(src, "uniform int uRightSphereMatType")) return PT_PROG_CORNELL;
+    return PT_PROG_UNKNOWN;
+}
+
+float uf(const pt_effect* fx, const char* name, int k = 0)
+{
+    auto it = fx->uniforms.find(name);
+    if (it == fx->uniforms.end() || !it->second.set) return 0.0f;   // GLSL uniforms default to 0
+    const Uniform& u = it->second;
+    if (u.is_int) return (float)u.i;
+    return k < u.n ? u.f[k] : 0.0f;
+}
+int ui(const pt_effect* fx, const char* name)
+{
+    auto it = fx->uniforms.find(name);
+    if (it == fx->uniforms.end() || !it->second.set) return 0;
+    const Uniform& u = it->second;
+    return u.is_int ? u.i : (int)u.f[0];
+}
+void um4(const pt_effect* fx, const char* name, ptg::m4& m)
+{
+    for (int k = 0; k < 16; k++) m.m[k] = uf(fx, name, k);
+}
+pt_texture* sampler(const pt_effect* fx, const char* name)
+{
+    auto it = fx->samplers.find(name);
+    return it == fx->samplers.end() ? nullptr : it->second;
+}
+
+pt::Tex8 tex8(const pt_texture* t)
+{
+    pt::Tex8 r{ nullptr, 0, 0 };
+    if (t && t->kind == TEX_U8) { r.p = (const uchar4*)t->d; r.w = t->w; r.h = t->h; }
+    return r;
+}
+
+ptg::f3 v3(float x, float y, float z) { return ptg::f3{ x, y, z }; }
+pt::QuadArg quad(ptg::f3 n, ptg::f3 a, ptg::f3 b, ptg::f3 c, ptg::f3 d, ptg::f3 col, int type)
+{
+    pt::QuadArg q;
+    q.normal = n; q.v0 = a; q.v1 = b; q.v2 = c; q.v3 = d; q.color = col; q.type = type;
+    return q;
+}
+float hdist(ptg::f3 a, ptg::f3 b)
+{
+    float x = a.x - b.x, y = a.y - b.y, z = a.z - b.z;
+    return std::sqrt(x * x + y * y + z * z);
+}
+
+// SetupScene() of js/BabylonPathTracing_FragmentShader.js:348-378 and
+// js/GLTFModelPathTracing_FragmentShader.js:613-643, evaluated once per draw.
+void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
+{
+    const float W = 50.0f;
+    const float L = uf(fx, "uQuadLightRadius") * 0.2f;
+    const ptg::f3 E = v3(1.0f * 10.0f, 1.0f * 10.0f, 1.0f * 10.0f);
+    const ptg::f3 white = v3(1.0f, 1.0f, 1.0f);
+    um4(fx, "uLeftSphereInvMatrix", a.sph[0].inv);
+    um4(fx, "uRightSphereInvMatrix", a.sph[1].inv);
+    a.sph[0].color = v3(1.0f, 1.0f, 0.0f);
+    a.sph[0].type = pt::CLEARCOAT_DIFFUSE;
+    a.sph[1].color = v3(1.0f, 1.0f, 1.0f);
+    a.sph[1].type = fx->prog == PT_PROG_CORNELL ? ui(fx, "uRightSphereMatType") : pt::METAL;
+    pt::QuadArg q[6];
+    q[0] = quad(v3(0, 0, 1), v3(-W, W, W), v3(W, W, W), v3(W, -W, W), v3(-W, -W, W), white, pt::DIFFUSE);
+    q[1] = quad(v3(1, 0, 0), v3(-W, -W, W), v3(-W, -W, -W), v3(-W, W, -W), v3(-W, W, W), v3(0.7f, 0.05f, 0.05f), pt::DIFFUSE);
+    q[2] = quad(v3(-1, 0, 0), v3(W, -W, -W), v3(W, -W, W), v3(W, W, W), v3(W, W, -W), v3(0.05f, 0.05f, 0.7f), pt::DIFFUSE);
+    q[3] = quad(v3(0, -1, 0), v3(-W, W, -W), v3(W, W, -W), v3(W, W, W), v3(-W, W, W), white, pt::DIFFUSE);
+    q[4] = quad(v3(0, 1, 0), v3(-W, -W, W), v3(W, -W, W), v3(W, -W, -W), v3(-W, -W, -W), white, pt::DIFFUSE);
+    const float sel = uf(fx, "uQuadLightPlaneSelectionNumber");
+    const float wm = W - 1.0f, wp = -W + 1.0f;
+    std::memset(&q[5], 0, sizeof(q[5]));   // unselected: the GLSL global keeps its zero default
+    if (sel == 1.0f) q[5] = quad(v3(-1, 0, 0), v3(wm, -L, L), v3(wm, L, L), v3(wm, L, -L), v3(wm, -L, -L), E, pt::LIGHT);
+    else if (sel == 2.0f) q[5] = quad(v3(1, 0, 0), v3(wp, -L, -L), v3(wp, L, -L), v3(wp, L, L), v3(wp, -L, L), E, pt::LIGHT);
+    else if (sel == 3.0f) q[5] = quad(v3(0, 0, 1), v3(-L, -L, wp), v3(L, -L, wp), v3(L, L, wp), v3(-L, L, wp), E, pt::LIGHT);
+    else if (sel == 4.0f) q[5] = quad(v3(0, 0, -1), v3(-L, -L, wm), v3(-L, L, wm), v3(L, L, wm), v3(L, -L, wm), E, pt::LIGHT);
+    else if (sel == 5.0f) q[5] = quad(v3(0, 1, 0), v3(-L, wp, -L), v3(-L, wp, L), v3(L, wp, L), v3(L, wp, -L), E, pt::LIGHT);
+    else if (sel == 6.0f) q[5] = quad(v3(0, -1, 0), v3(-L, wm, -L), v3(L, wm, -L), v3(L, wm, L), v3(-L, wm, L), E, pt::LIGHT);
+    auto sub = [](ptg::f3 x, ptg::f3 y) { return v3(x.x - y.x, x.y - y.y, x.z - y.z); };
+    for (int i = 0; i < 6; i++) {
+        a.qtri[2 * i] = pt::TriArg{ q[i].v0, sub(q[i].v1, q[i].v0), sub(q[i].v2, q[i].v0) };
+        a.qtri[2 * i + 1] = pt::TriArg{ q[i].v0, sub(q[i].v2, q[i].v0), sub(q[i].v3, q[i].v0) };
+        a.qnormal[i] = q[i].normal;
+        a.qcolor[i] = q[i].color;
+        a.qtype[i] = q[i].type;
+    }
+    a.light = q[5];
+    a.light_r2 = hdist(q[5].v0, q[5].v1) * hdist(q[5].v0, q[5].v3);
+}
+
+int bands_owned(const pt_ctx* c, int height)
+{
+    int nb = (height + pt::kTile - 1) / pt::kTile;
+    if (c->part >= nb) return 0;
+    return (nb - c->part + c->num_parts - 1) / c->num_parts;
+}
+
+int begin_draw(pt_ctx* c, int prog)
+{
+    if (!c->ev0[prog]) {
+        HIPCHK(c, hipEventCreate(&c->ev0[prog]));
+        HIPCHK(c, hipEventCreate(&c->ev1[prog]));
+    }
+    HIPCHK(c, hipEventRecord(c->ev0[prog], c->stream));
+    if (c->window) {
+        size_t k = c->window_draws.size();
+        if (k == c->pool.size()) {
+            hipEvent_t a, b;
+            HIPCHK(c, hipEventCreate(&a));
+            HIPCHK(c, hipEventCreate(&b));
+            c->pool.emplace_back(a, b);
+        }
+        HIPCHK(c, hipEventRecord(c->pool[k].first, c->stream));
+        c->window_draws.emplace_back(prog, (int)k);
+    }
+    return PT_OK;
+}
+int end_draw(pt_ctx* c, int prog)
+{
+    HIPCHK(c, hipEventRecord(c->ev1[prog], c->stream));
+    c->ev_used[prog] = true;
+    if (c->window && !c->window_draws.empty())
+        HIPCHK(c, hipEventRecord(c->pool[c->window_draws.back().second].second, c->stream));
+    return PT_OK;
+}
+
+int render_trace(pt_effect* fx, pt_texture* target)
+{
+    pt_ctx* c = fx->ctx;
+    if (!target || target->kind != TEX_RT) return fail(c, PT_ERR_ARG, "path tracing draws need a render target");
+    pt_texture* prev = sampler(fx, "previousBuffer");
+    pt_texture* bn = sampler(fx, "blueNoiseTexture");
+    if (!prev || prev->kind == TEX_U8 || prev->w != target->w || prev->h != target->h)
+        return fail(c, PT_ERR_STATE, "previousBuffer must be an RGBA32F texture of the target's size");
+    if (!bn || bn->kind != TEX_U8) return fail(c, PT_ERR_STATE, "blueNoiseTexture must be bound (RGBA8)");
+    pt::TraceArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.width = target->w;
+    a.height = target->h;
+    a.num_parts = c->num_parts;
+    a.part = c->part;
+    a.res[0] = uf(fx, "uResolution", 0); a.res[1] = uf(fx, "uResolution", 1);
+    a.rnd[0] = uf(fx, "uRandomVec2", 0); a.rnd[1] = uf(fx, "uRandomVec2", 1);
+    a.ulen = uf(fx, "uULen"); a.vlen = uf(fx, "uVLen");
+    a.frame = uf(fx, "uFrameCounter");
+    a.eps = uf(fx, "uEPS_intersect");
+    a.aperture = uf(fx, "uApertureSize");
+    a.focus = uf(fx, "uFocusDistance");
+    a.moving = ui(fx, "uCameraIsMoving");
+    um4(fx, "uCameraMatrix", a.cam);
+    setup_scene(fx, a);
+    a.prev = (const float4*)prev->d;
+    a.out = (float4*)target->d;
+    a.bluenoise = tex8(bn);
+    if (fx->prog == PT_PROG_GLTF) {
+        pt_texture* bvh = sampler(fx, "tAABBTexture");
+        pt_texture* tri = sampler(fx, "tTriangleTexture");
+        if (!bvh || !tri || bvh->kind != TEX_F32 || tri->kind != TEX_F32)
+            return fail(c, PT_ERR_STATE, "tAABBTexture / tTriangleTexture must be bound RGBA32F data textures");
+        um4(fx, "uGLTF_Model_InvMatrix", a.model);
+        a.model_mat = ui(fx, "uModelMaterialType");
+        a.uses_albedo = ui(fx, "uModelUsesAlbedoTexture");
+        a.uses_bump = ui(fx, "uModelUsesBumpTexture");
+        a.uses_metal = ui(fx, "uModelUsesMetallicTexture");
+        a.uses_emissive = ui(fx, "uModelUsesEmissiveTexture");
+        a.aabb = (const float4*)bvh->d;
+        a.aabb_texels = (long long)bvh->w * bvh->h;
+        a.tri = (const float4*)tri->d;
+        a.tri_texels = (long long)tri->w * tri->h;
+        a.albedo = tex8(sampler(fx, "tAlbedoTexture"));
+        a.bump = tex8(sampler(fx, "tBumpTexture"));
+        a.metal = tex8(sampler(fx, "tMetallicTexture"));
+        a.emissive = tex8(sampler(fx, "tEmissiveTexture"));
+    }
+    a.counters = c->d_counters;
+    a.err = c->d_err;
+    int gx = (target->w + pt::kTile - 1) / pt::kTile;
+    int gy = bands_owned(c, target->h);
+    int rc = begin_draw(c, fx->prog);
+    if (rc) return rc;
+    if (gy > 0) HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, gy, c->stream));
+    return end_draw(c, fx->prog);
+}
+
+int render_copy(pt_effect* fx, pt_texture* target)
+{
+    pt_ctx* c = fx->ctx;
+    pt_texture* src = sampler(fx, "pathTracedImageBuffer");
+    if (!target || target->kind != TEX_RT) return fail(c, PT_ERR_ARG, "screenCopy needs a render target");
+    if (!src || src->kind == TEX_U8 || src->w != target->w || src->h != target->h)
+        return fail(c, PT_ERR_STATE, "pathTracedImageBuffer must be an RGBA32F texture of the target's size");
+    int rc = begin_draw(c, fx->prog);
+    if (rc) return rc;
+    if (src != target) {
+        pt::CopyArgs a{ target->w, target->h, c->num_parts, c->part, (const float4*)src->d, (float4*)target->d };
+        int gx = (target->w + 255) / 256, gy = bands_owned(c, target->h);
+        if (gy > 0) HIPCHK(c, pt_launch_copy(&a, gx, gy, c->stream));
+    }
+    return end_draw(c, fx->prog);
+}
+
+int render_output(pt_effect* fx, pt_texture* target)
+{
+    pt_ctx* c = fx->ctx;
+    pt_texture* acc = sampler(fx, "accumulationBuffer");
+    if (!acc || acc->kind == TEX_U8) return fail(c, PT_ERR_STATE, "accumulationBuffer must be an RGBA32F texture");
+    pt::OutputArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.acc = (const float4*)acc->d;
+    a.acc_w = acc->w;
+    a.acc_h = acc->h;
+    a.one_over_n = uf(fx, "uOneOverSampleCounter");
+    a.exposure = uf(fx, "uToneMappingExposure");
+    if (target) {
+        if (target->kind != TEX_RT) return fail(c, PT_ERR_ARG, "screenOutput target must be a render target or the canvas");
+        a.width = target->w; a.height = target->h; a.out_f = (float4*)target->d;
+    } else {
+        if (c->cw == 0 && c->ch == 0) {
+            int rc = pt_canvas_resize(c, acc->w, acc->h);
+            if (rc) return rc;
+        }
+        a.width = c->cw; a.height = c->ch; a.canvas = c->canvas;
+    }
+    int rc = begin_draw(c, fx->prog);
+    if (rc) return rc;
+    if (a.width > 0 && a.height > 0) HIPCHK(c, pt_launch_output(&a, c->stream));
+    return end_draw(c, fx->prog);
+}
+
+pt_texture* new_texture(pt_ctx* c, int kind, int w, int h, size_t texel, int* err)
+{
+    auto* t = new pt_texture();
+    t->ctx = c; t->kind = kind; t->w = w; t->h = h;
+    t->bytes = (size_t)w * (size_t)h * texel;
+    if (t->bytes) {
+        hipError_t e = hipMalloc(&t->d, t->bytes);
+        if (e != hipSuccess) {
+            hipfail(c, e, "hipMalloc");
+            delete t;
+            if (err) *err = PT_ERR_OOM;
+            return nullptr;
+        }
+    }
+    c->textures.insert(t);
+    return t;
+}
+
+pt_texture* upload(pt_ctx* c, int kind, int w, int h, const void* data, size_t texel, int sampling, int invert_y, int* err)
+{
+    if (err) *err = PT_OK;
+    if (!c || w <= 0 || h <= 0 || (long long)w * h >= (1ll << 31)) { if (err) *err = PT_ERR_ARG; return nullptr; }
+    hipSetDevice(c->device);
+    pt_texture* t = new_texture(c, kind, w, h, texel, err);
+    if (!t) return nullptr;
+    t->sampling = sampling; t->invert_y = invert_y;
+    hipError_t e = hipSuccess;
+    if (!data) e = hipMemsetAsync(t->d, 0, t->bytes, c->stream);
+    else if (!invert_y) e = hipMemcpyAsync(t->d, data, t->bytes, hipMemcpyHostToDevice, c->stream);
+    else {
+        const size_t row = (size_t)w * texel;   // UNPACK_FLIP_Y: source row r lands on row h-1-r
+        for (int r = 0; r < h && e == hipSuccess; r++)
+            e = hipMemcpyAsync((char*)t->d + (size_t)(h - 1 - r) * row, (const char*)data + (size_t)r * row, row,
+                               hipMemcpyHostToDevice, c->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);   // the caller keeps ownership of data
+    if (e != hipSuccess) {
+        hipfail(c, e, "texture upload");
+        pt_texture_destroy(t);
+        if (err) *err = PT_ERR_HIP;
+        return nullptr;
+    }
+    return t;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pt_version(void) { return "libpt 0.1.0 gfx950"; }
+
+pt_ctx* pt_ctx_create(int device, int* err)
+{
+    if (err) *err = PT_OK;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+        if (err) *err = PT_ERR_DEVICE;
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        if (err) *err = PT_ERR_DEVICE;   // the code objects are gfx950-only
+        return nullptr;
+    }
+    auto* c = new pt_ctx();
+    c->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&c->d_err, 256);
+    if (e == hipSuccess) e = hipMalloc(&c->d_counters, pt::C_NUM * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(c->d_err, 0, 256);
+    if (e == hipSuccess) e = hipMemset(c->d_counters, 0, pt::C_NUM * sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        if (err) *err = PT_ERR_HIP;
+        pt_ctx_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+void pt_ctx_destroy(pt_ctx* c)
+{
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    std::vector<pt_effect*> fx(c->effects.begin(), c->effects.end());
+    for (auto* f : fx) pt_effect_destroy(f);
+    std::vector<pt_texture*> tx(c->textures.begin(), c->textures.end());
+    for (auto* t : tx) pt_texture_destroy(t);
+    for (auto& pr : c->pool) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
+    for (int i = 0; i < kProgSlots; i++) {
+        if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
+        if (c->ev1[i]) hipEventDestroy(c->ev1[i]);
+    }
+    if (c->canvas) hipFree(c->canvas);
+    if (c->d_err) hipFree(c->d_err);
+    if (c->d_counters) hipFree(c->d_counters);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* pt_last_error(pt_ctx* c) { return c ? c->err.c_str() : "no context"; }
+
+int pt_sync(pt_ctx* c)
+{
+    if (!c) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    unsigned flags = 0;
+    HIPCHK(c, hipMemcpy(&flags, c->d_err, sizeof(flags), hipMemcpyDeviceToHost));
+    if (flags) {
+        HIPCHK(c, hipMemset(c->d_err, 0, sizeof(unsigned)));
+        if (flags & pt::E_STACK) return fail(c, PT_ERR_DATA, "BVH traversal needed more than stackLevels[28]");
+    }
+    return PT_OK;
+}
+
+int pt_canvas_resize(pt_ctx* c, int w, int h)
+{
+    if (!c || w < 0 || h < 0) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (w == c->cw && h == c->ch && c->canvas) return PT_OK;
+    if (c->canvas) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->canvas)); c->canvas = nullptr; }
+    c->cw = w; c->ch = h;
+    if (w * (size_t)h) {
+        HIPCHK(c, hipMalloc(&c->canvas, (size_t)w * h * sizeof(uchar4)));
+        HIPCHK(c, hipMemsetAsync(c->canvas, 0, (size_t)w * h * sizeof(uchar4), c->stream));
+    }
+    return PT_OK;
+}
+
+pt_effect* pt_effect_create(pt_ctx* c, const char* src, const char* const* un, int nu, const char* const* sn, int ns, int* err)
+{
+    if (err) *err = PT_OK;
+    if (!c || !src) { if (err) *err = PT_ERR_ARG; return nullptr; }
+    int prog = classify(src);
+    if (prog == PT_PROG_UNKNOWN) {
+        fail(c, PT_ERR_SHADER, "fragment shader not recognised as a reference path-tracing program");
+        if (err) *err = PT_ERR_SHADER;
+        return nullptr;
+    }
+    return pt_effect_create_program(c, prog, un, nu, sn, ns, err);
+}
+
+pt_effect* pt_effect_create_program(pt_ctx* c, int prog, const char* const* un, int nu, const char* const* sn, int ns, int* err)
+{
+    if (err) *err = PT_OK;
+    if (!c || nu < 0 || ns < 0 || prog <= PT_PROG_UNKNOWN || prog > PT_PROG_QUADRIC) { if (err) *err = PT_ERR_ARG; return nullptr; }
+    auto* fx = new pt_effect();
+    fx->ctx = c;
+    fx->prog = prog;
+    for (int i = 0; i < nu; i++) if (un && un[i]) fx->uniforms[un[i]] = Uniform();
+    for (int i = 0; i < ns; i++) if (sn && sn[i]) fx->samplers[sn[i]] = nullptr;
+    c->effects.insert(fx);
+    return fx;
+}
+
+void pt_effect_destroy(pt_effect* fx)
+{
+    if (!fx) return;
+    fx->ctx->effects.erase(fx);
+    delete fx;
+}
+
+int pt_effect_program(const pt_effect* fx) { return fx ? fx->prog : PT_PROG_UNKNOWN; }
+
+int pt_set_float(pt_effect* fx, const char* name, const float* v, int n)
+{
+    if (!fx || !name || !v || n < 1 || n > 16) return PT_ERR_ARG;
+    auto it = fx->uniforms.find(name);
+    if (it == fx->uniforms.end()) return PT_OK;   // undeclared: ignored, as in Babylon
+    Uniform& u = it->second;
+    u.is_int = false; u.n = n; u.set = true;
+    for (int k = 0; k < n; k++) u.f[k] = v[k];
+    return PT_OK;
+}
+
+int pt_set_int(pt_effect* fx, const char* name, int v)
+{
+    if (!fx || !name) return PT_ERR_ARG;
+    auto it = fx->uniforms.find(name);
+    if (it == fx->uniforms.end()) return PT_OK;
+    Uniform& u = it->second;
+    u.is_int = true; u.n = 1; u.i = v; u.set = true;
+    return PT_OK;
+}
+
+int pt_set_texture(pt_effect* fx, const char* name, pt_texture* t)
+{
+    if (!fx || !name) return PT_ERR_ARG;
+    if (t && t->ctx != fx->ctx) return fail(fx->ctx, PT_ERR_ARG, "texture belongs to another context");
+    auto it = fx->samplers.find(name);
+    if (it == fx->samplers.end()) return PT_OK;
+    it->second = t;
+    return PT_OK;
+}
+
+pt_texture* pt_texture_create_rgba32f(pt_ctx* c, int w, int h, const float* data, int sampling, int invert_y, int* err)
+{
+    return upload(c, TEX_F32, w, h, data, 16, sampling, invert_y, err);
+}
+
+pt_texture* pt_texture_create_rgba8(pt_ctx* c, int w, int h, const uint8_t* data, int sampling, int invert_y, int* err)
+{
+    return upload(c, TEX_U8, w, h, data, 4, sampling, invert_y, err);
+}
+
+pt_texture* pt_render_target_create(pt_ctx* c, int w, int h, int* err)
+{
+    return upload(c, TEX_RT, w, h, nullptr, 16, PT_SAMPLING_NEAREST, 0, err);
+}
+
+pt_texture* pt_render_target_wrap(pt_ctx* c, int w, int h, void* dptr, int* err)
+{
+    if (err) *err = PT_OK;
+    if (!c || w <= 0 || h <= 0 || !dptr) { if (err) *err = PT_ERR_ARG; return nullptr; }
+    auto* t = new pt_texture();
+    t->ctx = c; t->kind = TEX_RT; t->w = w; t->h = h;
+    t->bytes = (size_t)w * h * 16;
+    t->d = dptr;
+    t->external = true;
+    c->textures.insert(t);
+    return t;
+}
+
+int pt_render_target_resize(pt_texture* t, int w, int h)
+{
+    if (!t || t->kind != TEX_RT || w <= 0 || h <= 0) return PT_ERR_ARG;
+    if (t->external) return fail(t->ctx, PT_ERR_ARG, "wrapped render targets are not resizable");
+    pt_ctx* c = t->ctx;
+    if (w == t->w && h == t->h) return PT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (t->d) HIPCHK(c, hipFree(t->d));
+    t->d = nullptr;
+    t->w = w; t->h = h; t->bytes = (size_t)w * h * 16;
+    HIPCHK(c, hipMalloc(&t->d, t->bytes));
+    HIPCHK(c, hipMemsetAsync(t->d, 0, t->bytes, c->stream));
+    return PT_OK;
+}
+
+int pt_texture_size(const pt_texture* t, int* w, int* h)
+{
+    if (!t) return PT_ERR_ARG;
+    if (w) *w = t->w;
+    if (h) *h = t->h;
+    return PT_OK;
+}
+
+void pt_texture_destroy(pt_texture* t)
+{
+    if (!t) return;
+    pt_ctx* c = t->ctx;
+    hipSetDevice(c->device);
+    for (auto* fx : c->effects)
+        for (auto& kv : fx->samplers)
+            if (kv.second == t) kv.second = nullptr;
+    if (t->d && !t->external) { hipStreamSynchronize(c->stream); hipFree(t->d); }
+    c->textures.erase(t);
+    delete t;
+}
+
+int pt_render(pt_effect* fx, pt_texture* target)
+{
+    if (!fx) return PT_ERR_ARG;
+    pt_ctx* c = fx->ctx;
+    if (target && target->ctx != c) return fail(c, PT_ERR_ARG, "target belongs to another context");
+    HIPCHK(c, hipSetDevice(c->device));
+    switch (fx->prog) {
+    case PT_PROG_CORNELL:
+    case PT_PROG_GLTF: return render_trace(fx, target);
+    case PT_PROG_SCREEN_COPY: return render_copy(fx, target);
+    case PT_PROG_SCREEN_OUTPUT: return render_output(fx, target);
+    default: return fail(c, PT_ERR_UNSUPPORTED, "program recognised but not implemented in this build");
+    }
+}
+
+int pt_read_pixels(pt_ctx* c, const pt_texture* t, void* dst, size_t bytes)
+{
+    if (!c || !dst) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    const void* src = t ? t->d : (const void*)c->canvas;
+    size_t need = t ? t->bytes : (size_t)c->cw * c->ch * sizeof(uchar4);
+    if (bytes < need) return fail(c, PT_ERR_ARG, "destination too small");
+    HIPCHK(c, hipMemcpyAsync(dst, src, need, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_write_pixels(pt_ctx* c, pt_texture* t, const void* src, size_t bytes)
+{
+    if (!c || !t || !src || bytes != t->bytes) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(t->d, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_set_row_partition(pt_ctx* c, int num_parts, int part)
+{
+    if (!c || num_parts < 1 || part < 0 || part >= num_parts) return PT_ERR_ARG;
+    c->num_parts = num_parts;
+    c->part = part;
+    return PT_OK;
+}
+
+void* pt_texture_device_ptr(pt_texture* t) { return t ? t->d : nullptr; }
+
+int pt_last_render_ms(pt_ctx* c, int prog, float* ms)
+{
+    if (!c || !ms || prog < 0 || prog >= kProgSlots || !c->ev_used[prog]) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipEventElapsedTime(ms, c->ev0[prog], c->ev1[prog]));
+    return PT_OK;
+}
+
+int pt_timing_begin(pt_ctx* c)
+{
+    if (!c) return PT_ERR_ARG;
+    c->window = true;
+    c->window_draws.clear();
+    return PT_OK;
+}
+
+int pt_timing_end(pt_ctx* c, int prog, double* total_ms, int* launches)
+{
+    if (!c || !total_ms || !launches) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    double t = 0.0;
+    int n = 0;
+    for (auto& d : c->window_draws) {
+        if (d.first != prog) continue;
+        float ms = 0.0f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->pool[d.second].first, c->pool[d.second].second));
+        t += ms;
+        n++;
+    }
+    *total_ms = t;
+    *launches = n;
+    return PT_OK;
+}
+
+int pt_set_counting(pt_ctx* c, int enable)
+{
+    if (!c) return PT_ERR_ARG;
+    c->counting = enable != 0;
+    return PT_OK;
+}
+
+int pt_read_counters(pt_ctx* c, uint64_t out[7])
+{
+    if (!c || !out) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out, c->d_counters, pt::C_NUM * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+int pt_reset_counters(pt_ctx* c)
+{
+    if (!c) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemsetAsync(c->d_counters, 0, pt::C_NUM * sizeof(unsigned long long), c->stream));
+    return PT_OK;
+}
+
+int pt_math_probe(pt_ctx* c, int op, const float* x, const float* y, float* out, int n)
+{
+    if (!c || !x || !out || n <= 0) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    float *dx = nullptr, *dy = nullptr, *dout = nullptr;
+    size_t b = (size_t)n * sizeof(float);
+    HIPCHK(c, hipMalloc(&dx, b));
+    HIPCHK(c, hipMalloc(&dout, b));
+    if (y) HIPCHK(c, hipMalloc(&dy, b));
+    HIPCHK(c, hipMemcpy(dx, x, b, hipMemcpyHostToDevice));
+    if (y) HIPCHK(c, hipMemcpy(dy, y, b, hipMemcpyHostToDevice));
+    HIPCHK(c, pt_launch_math_probe(op, dx, dy, dout, n, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(out, dout, b, hipMemcpyDeviceToHost));
+    hipFree(dx); hipFree(dout);
+    if (dy) hipFree(dy);
+    return PT_OK;
+}
+
+}  // extern "C"

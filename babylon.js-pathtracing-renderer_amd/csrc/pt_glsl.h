@@ -1,0 +1,186 @@
+// pt_glsl.h — device-side GLSL ES 3.00 built-ins for gfx950 with the pinned "pt-glsl v1"
+// semantics documented in DESIGN.md §Parity: one IEEE binary32 op per GLSL op, no contraction
+// (the library is built with -ffp-contract=off), correctly rounded '/' and sqrt, GLSL-spec
+// min/max/clamp/mix, and fixed range-reduction + polynomial sequences for exp2/log2/sin/cos/atan
+// built only from IEEE ops, v_floor, v_frexp_* and v_ldexp (all exact on CDNA4).
+// Everything here is __device__ code; nothing is shared with the CPU oracle except the spec.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PT_D __device__ __forceinline__
+
+namespace ptg {
+
+constexpr float kInf = __builtin_inff();
+
+PT_D float gmin(float x, float y) { return y < x ? y : x; }
+PT_D float gmax(float x, float y) { return x < y ? y : x; }
+PT_D float gclamp(float x, float a, float b) { return gmin(gmax(x, a), b); }
+PT_D float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+PT_D float gfract(float x) { return x - floorf(x); }
+PT_D float gmod(float x, float y) { return x - y * floorf(x / y); }
+PT_D float gsmoothstep(float e0, float e1, float x)
+{
+    float t = gclamp((x - e0) / (e1 - e0), 0.0f, 1.0f);
+    return (t * t) * (3.0f - 2.0f * t);
+}
+
+PT_D float gexp2(float x)
+{
+    if (x != x) return x;
+    if (x >= 128.0f) return kInf;
+    if (x < -150.0f) return 0.0f;
+    float n = floorf(x + 0.5f);
+    float f = x - n;
+    float p = 1.5252733804059841e-05f;
+    p = p * f + 1.5403530393381609e-04f;
+    p = p * f + 1.3333558146428443e-03f;
+    p = p * f + 9.6181291076284772e-03f;
+    p = p * f + 5.5504108664821580e-02f;
+    p = p * f + 2.4022650695910071e-01f;
+    p = p * f + 6.9314718055994531e-01f;
+    p = p * f + 1.0f;
+    return ldexpf(p, (int)n);
+}
+
+PT_D float glog2(float x)
+{
+    if (x != x || x < 0.0f) return __builtin_nanf("");
+    if (x == 0.0f) return -kInf;
+    if (x == kInf) return kInf;
+    int e;
+    float m = frexpf(x, &e);
+    if (m < 0.70710678118654752f) { m = m * 2.0f; e = e - 1; }
+    float t = (m - 1.0f) / (m + 1.0f);
+    float t2 = t * t;
+    float p = 0.11111111111111111f;
+    p = p * t2 + 0.14285714285714285f;
+    p = p * t2 + 0.2f;
+    p = p * t2 + 0.33333333333333333f;
+    p = p * t2;
+    float l = (t + t * p) * 2.8853900817779268f;
+    return (float)e + l;
+}
+
+PT_D float gexp(float x) { return gexp2(x * 1.4426950408889634f); }
+PT_D float glog(float x) { return glog2(x) * 0.69314718055994531f; }
+PT_D float gpow(float x, float y) { return gexp2(y * glog2(x)); }
+
+PT_D void gsincos_reduce(float x, float& r, int& q)
+{
+    float k = floorf(x * 0.63661977236758134f + 0.5f);
+    float rr = x - k * 1.5703125f;
+    rr = rr - k * 4.837512969970703125e-4f;
+    rr = rr - k * 7.54978995489188216e-8f;
+    r = rr;
+    q = (int)(k - 4.0f * floorf(k * 0.25f));
+}
+PT_D float gsin_poly(float r)
+{
+    float r2 = r * r;
+    float p = -1.9515295891e-4f;
+    p = p * r2 + 8.3321608736e-3f;
+    p = p * r2 - 1.6666654611e-1f;
+    return r + r * (r2 * p);
+}
+PT_D float gcos_poly(float r)
+{
+    float r2 = r * r;
+    float p = 2.443315711809948e-5f;
+    p = p * r2 - 1.388731625493765e-3f;
+    p = p * r2 + 4.166664568298827e-2f;
+    return (1.0f - 0.5f * r2) + (r2 * r2) * p;
+}
+// sin and cos of the same angle share one reduction (the path tracer always needs both)
+PT_D void gsincos(float x, float& s, float& c)
+{
+    if (!(x - x == 0.0f)) { s = c = __builtin_nanf(""); return; }
+    float r; int q;
+    gsincos_reduce(x, r, q);
+    float sp = gsin_poly(r), cp = gcos_poly(r);
+    s = q == 0 ? sp : q == 1 ? cp : q == 2 ? -sp : -cp;
+    c = q == 0 ? cp : q == 1 ? -sp : q == 2 ? -cp : sp;
+}
+PT_D float gsin(float x) { float s, c; gsincos(x, s, c); return s; }
+PT_D float gcos(float x) { float s, c; gsincos(x, s, c); return c; }
+
+PT_D float gatan(float x)
+{
+    if (x != x) return x;
+    float sgn = x < 0.0f ? -1.0f : 1.0f;
+    float a = x < 0.0f ? -x : x;
+    float y = 0.0f;
+    if (a > 2.414213562373095f) { y = 1.5707963267948966f; a = -1.0f / a; }
+    else if (a > 0.4142135623730950f) { y = 0.7853981633974483f; a = (a - 1.0f) / (a + 1.0f); }
+    float z = a * a;
+    float p = 8.05374449538e-2f;
+    p = p * z - 1.38776856032e-1f;
+    p = p * z + 1.99777106478e-1f;
+    p = p * z - 3.33329491539e-1f;
+    y = y + (p * z * a + a);
+    return sgn * y;
+}
+PT_D float gatan2(float y, float x)
+{
+    if (x != x || y != y) return x + y;
+    if (x == 0.0f) {
+        if (y > 0.0f) return 1.5707963267948966f;
+        if (y < 0.0f) return -1.5707963267948966f;
+        return 0.0f;
+    }
+    float t = gatan(y / x);
+    if (x > 0.0f) return t;
+    return y < 0.0f ? t - 3.14159265358979323f : t + 3.14159265358979323f;
+}
+PT_D float gacos(float x)
+{
+    if (!(x >= -1.0f && x <= 1.0f)) return __builtin_nanf("");
+    if (x == -1.0f) return 3.14159265358979323f;
+    return 2.0f * gatan(sqrtf((1.0f - x) / (1.0f + x)));
+}
+
+// ------------------------------------------------------------------------------------- vec3
+struct f3 { float x, y, z; };
+PT_D f3 mk(float x, float y, float z) { return f3{ x, y, z }; }
+PT_D f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+PT_D f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+PT_D f3 operator*(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+PT_D f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+PT_D f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
+PT_D float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PT_D f3 cross(f3 a, f3 b) { return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y); }
+PT_D float length(f3 a) { return sqrtf(dot(a, a)); }
+PT_D f3 normalize(f3 a) { float inv = 1.0f / sqrtf(dot(a, a)); return a * inv; }
+PT_D float distance(f3 a, f3 b) { return length(a - b); }
+PT_D f3 reflect(f3 I, f3 N) { return I - N * (2.0f * dot(N, I)); }
+PT_D f3 refract(f3 I, f3 N, float eta)
+{
+    float d = dot(N, I);
+    float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
+    return I * eta - N * (eta * d + sqrtf(k));
+}
+PT_D f3 mix3(f3 a, f3 b, float t) { return mk(gmix(a.x, b.x, t), gmix(a.y, b.y, t), gmix(a.z, b.z, t)); }
+PT_D f3 clamp3(f3 a, float lo, float hi) { return mk(gclamp(a.x, lo, hi), gclamp(a.y, lo, hi), gclamp(a.z, lo, hi)); }
+PT_D f3 max3s(f3 a, float s) { return mk(gmax(a.x, s), gmax(a.y, s), gmax(a.z, s)); }
+
+// GLSL mat4 from Babylon Matrix.m (column-major): M * vec4(v, w)
+struct m4 { float m[16]; };
+PT_D f3 mul(const m4& M, f3 v, float w)
+{
+    const float* m = M.m;
+    return mk(m[0] * v.x + m[4] * v.y + m[8] * v.z + m[12] * w,
+              m[1] * v.x + m[5] * v.y + m[9] * v.z + m[13] * w,
+              m[2] * v.x + m[6] * v.y + m[10] * v.z + m[14] * w);
+}
+// transpose(mat3(M)) * n
+PT_D f3 mul3t(const m4& M, f3 n)
+{
+    const float* m = M.m;
+    return mk(m[0] * n.x + m[1] * n.y + m[2] * n.z,
+              m[4] * n.x + m[5] * n.y + m[6] * n.z,
+              m[8] * n.x + m[9] * n.y + m[10] * n.z);
+}
+
+} // namespace ptg

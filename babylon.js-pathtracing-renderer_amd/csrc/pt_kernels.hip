@@ -1,0 +1,737 @@
+// pt_kernels.hip — gfx950 kernels behind libpt.so.
+//
+//   pt_trace<PROG,COUNT>  the per-pixel path-tracing program (js/PathTracingCommon.js:1251-1358
+//                         with the Cornell / glTF scene shaders' SetupScene, SceneIntersect and
+//                         CalculateRadiance). One lane = one pixel = one path of <= 6 segments.
+//   pt_copy               screenCopy (js/PathTracingCommon.js:1-16), band-aware.
+//   pt_output             screenOutput (js/PathTracingCommon.js:19-309): 5x5 / 3x3 edge-aware
+//                         filter, 1/N, Reinhard, gamma 0.4545, unorm8.
+//   pt_math_probe_kernel  device self-test of the pinned built-ins.
+//
+// Mapping onto CDNA4:
+//  * a 256-lane block shades a 16x16 tile as four 8x8 wave tiles; lane bits (x0,y0,x1,x2,y1,y2)
+//    put every GL 2x2 fragment quad inside 4 consecutive lanes, so dFdx/dFdy/fwidth are two
+//    DPP/ds_swizzle exchanges (__shfl_xor 1 and 2) instead of a G-buffer round trip through HBM;
+//  * the scene constants (SetupScene) live in the kernarg segment -> SGPRs;
+//  * the BVH short stack (stackLevels[28] of (node, tNear)) keeps its first kStackLds levels per
+//    lane in LDS at [level][lane] (conflict-free); deeper levels (never reached by the reference
+//    meshes' rays, but legal for depth <= 28 trees) go to a private array = scratch, which the
+//    runtime backs only for resident waves;
+//  * BVH nodes are read as the reference's 32-byte texel pairs (two dwordx4 loads per node) and
+//    leaf triangles as three dwordx4 loads: the AoS texture layout is already the right one for
+//    incoherent per-lane gathers (one 32/48-B segment per lane, vs 8-9 lines for SoA).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_args.h"
+#include "pt_glsl.h"
+
+using namespace ptg;
+
+namespace pt {
+
+constexpr float kINF = 1000000.0f;   // #define INFINITY 1000000.0 (js/PathTracingCommon.js:329)
+constexpr float kTwoPi = 6.28318530717958648f;
+
+enum { PROG_CORNELL = 3, PROG_GLTF = 4 };
+// PROG_GLTF_TEX: the glTF program instantiated with its PBR / normal-map code (models with an
+// albedo or bump texture); PROG_GLTF is the same program with those branches compiled out.
+enum { PROG_GLTF_TEX = 104 };
+template <int P> constexpr bool kIsGltf = P == PROG_GLTF || P == PROG_GLTF_TEX;
+template <int P> constexpr bool kHasTex = P == PROG_GLTF_TEX;
+// waves per SIMD the register allocator must leave room for (128 VGPRs -> 4; the textured
+// variant keeps 2 rather than spill)
+template <int P> constexpr int kMinWaves = kHasTex<P> ? 2 : 4;
+
+// ------------------------------------------------------------------------------ per-lane state
+struct Path {
+    uint32_t s0, s1;       // uvec2 seed (js/PathTracingCommon.js:500)
+    float counter;         // blueNoise_rand() counter
+    float bn0, bn1;        // randVec4.r / .g (channel = mod(counter, 2) only reaches r, g)
+    f3 ro, rd;             // rayOrigin, rayDirection
+};
+
+PT_D float rng(Path& p)
+{
+    p.s0 += 1u; p.s1 += 1u;
+    uint32_t qx = 1103515245u * ((p.s0 >> 1u) ^ p.s1);
+    uint32_t qy = 1103515245u * ((p.s1 >> 1u) ^ p.s0);
+    uint32_t n = 1103515245u * (qx ^ (qy >> 3u));
+    return (float)n * (1.0f / 4294967296.0f);
+}
+PT_D float blueNoise_rand(Path& p)
+{
+    p.counter = p.counter + 1.0f;
+    int channel = (int)gmod(p.counter, 2.0f);
+    return gfract(channel == 0 ? p.bn0 : p.bn1);
+}
+PT_D float tentFilter(float x) { return (x < 0.5f) ? sqrtf(2.0f * x) - 1.0f : 1.0f - sqrtf(2.0f - (2.0f * x)); }
+PT_D f3 onb_u(f3 nl)
+{
+    f3 a = (fabsf(nl.y) < 0.9f) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+    return normalize(cross(a, nl));
+}
+PT_D f3 cosWeightedDir(Path& p, f3 nl)
+{
+    float r = sqrtf(rng(p));
+    float phi = rng(p) * kTwoPi;
+    float sn, cs;
+    gsincos(phi, sn, cs);
+    float x = r * cs, y = r * sn;
+    float z = sqrtf(1.0f - x * x - y * y);
+    f3 U = onb_u(nl);
+    f3 V = cross(nl, U);
+    return normalize(U * x + V * y + nl * z);
+}
+PT_D f3 specularLobeDir(Path& p, f3 rdir, float roughness)
+{
+    roughness = gclamp(roughness, 0.0f, 1.0f);
+    float exponent = gmix(7.0f, 0.0f, sqrtf(roughness));
+    float cosTheta = gpow(rng(p), 1.0f / (gexp(exponent) + 1.0f));
+    float sinTheta = sqrtf(gmax(0.0f, 1.0f - cosTheta * cosTheta));
+    float phi = rng(p) * kTwoPi;
+    float sn, cs;
+    gsincos(phi, sn, cs);
+    f3 U = onb_u(rdir);
+    f3 V = cross(rdir, U);
+    f3 lobe = (U * cs) * sinTheta + (V * sn) * sinTheta + rdir * cosTheta;
+    return normalize(mix3(rdir, lobe, roughness));
+}
+PT_D float fresnel(f3 rdir, f3 n, float etai, float etat, float& ratioIoR)
+{
+    float temp = etai;
+    float cosi = gclamp(dot(rdir, n), -1.0f, 1.0f);
+    if (cosi > 0.0f) { etai = etat; etat = temp; }
+    ratioIoR = etai / etat;
+    float sint = ratioIoR * sqrtf(1.0f - (cosi * cosi));
+    if (sint >= 1.0f) return 1.0f;
+    float cost = sqrtf(1.0f - (sint * sint));
+    cosi = fabsf(cosi);
+    float Rs = ((etat * cosi) - (etai * cost)) / ((etat * cosi) + (etai * cost));
+    float Rp = ((etai * cosi) - (etat * cost)) / ((etai * cosi) + (etat * cost));
+    return gclamp(((Rs * Rs) + (Rp * Rp)) * 0.5f, 0.0f, 1.0f);
+}
+PT_D f3 sampleQuadLight(Path& p, const TraceArgs& a, f3 x, f3 nl, float& weight)
+{
+    const QuadArg& L = a.light;
+    f3 q;
+    q.x = gmix(L.v0.x, L.v2.x, gclamp(rng(p), 0.1f, 0.9f));
+    q.y = gmix(L.v0.y, L.v2.y, gclamp(rng(p), 0.1f, 0.9f));
+    q.z = gmix(L.v0.z, L.v2.z, gclamp(rng(p), 0.1f, 0.9f));
+    f3 d = q - x;
+    float d2 = dot(d, d);
+    float cos_a_max = sqrtf(1.0f - gclamp(a.light_r2 / d2, 0.0f, 1.0f));
+    d = normalize(d);
+    float dotNl = gmax(0.0f, dot(nl, d));
+    float w = 2.0f * (1.0f - cos_a_max) * gmax(0.0f, -dot(d, L.normal)) * dotNl;
+    weight = gclamp(w, 0.0f, 1.0f);
+    return d;
+}
+
+// ------------------------------------------------------------------------------ intersectors
+PT_D float unitSphere(f3 ro, f3 rd, f3& n)
+{
+    float a = dot(rd, rd);
+    float b = 2.0f * dot(rd, ro);
+    float c = dot(ro, ro) - 1.0f;
+    float invA = 1.0f / a;          // solveQuadratic, js/PathTracingCommon.js:631-641
+    b *= invA;
+    c *= invA;
+    float nh = -b * 0.5f;
+    float u2 = nh * nh - c;
+    float u;
+    if (u2 < 0.0f) { nh = 0.0f; u = 0.0f; } else u = sqrtf(u2);
+    float t0 = nh - u, t1 = nh + u;
+    float t = t0 > 0.0f ? t0 : t1 > 0.0f ? t1 : kINF;
+    if (t != kINF) { f3 h = ro + rd * t; n = mk(2.0f * h.x, 2.0f * h.y, 2.0f * h.z); }
+    return t;
+}
+// TriangleIntersect, single-sided (QuadIntersect passes isDoubleSided = false), edges precomputed
+PT_D float quadTriangle(const TriArg& T, f3 ro, f3 rd)
+{
+    f3 pv = cross(rd, T.e2);
+    float det = 1.0f / dot(T.e1, pv);
+    if (det < 0.0f) return kINF;
+    f3 tv = ro - T.v0;
+    float u = dot(tv, pv) * det;
+    f3 qv = cross(tv, T.e1);
+    float v = dot(rd, qv) * det;
+    float t = dot(T.e2, qv) * det;
+    return (u < 0.0f || u > 1.0f || v < 0.0f || u + v > 1.0f || t <= 0.0f) ? kINF : t;
+}
+PT_D float box(f3 mn, f3 mx, f3 ro, f3 inv)
+{
+    f3 nr = (mn - ro) * inv;
+    f3 fr = (mx - ro) * inv;
+    float t0 = gmax(gmax(gmin(nr.x, fr.x), gmin(nr.y, fr.y)), gmin(nr.z, fr.z));
+    float t1 = gmin(gmin(gmax(nr.x, fr.x), gmax(nr.y, fr.y)), gmax(nr.z, fr.z));
+    return gmax(t0, 0.0f) > t1 ? kINF : t0;
+}
+PT_D float bvhTriangle(f3 v0, f3 v1, f3 v2, f3 ro, f3 rd, float& u, float& v, bool dbl)
+{
+    f3 e1 = v1 - v0, e2 = v2 - v0;
+    f3 pv = cross(rd, e2);
+    float det = 1.0f / dot(e1, pv);
+    f3 tv = ro - v0;
+    u = dot(tv, pv) * det;
+    f3 qv = cross(tv, e1);
+    v = dot(rd, qv) * det;
+    float t = dot(e2, qv) * det;
+    bool miss = u < 0.0f || u > 1.0f || v < 0.0f || u + v > 1.0f || t <= 0.0f;
+    if (!dbl) miss = miss || det < 0.0f;
+    return miss ? kINF : t;
+}
+
+// texelFetch on a RGBA32F data texture by linear texel index (== ivec2(mod(i,2048), i/2048) for
+// the reference's 2048-wide textures); outside the texture -> 0 (pinned)
+PT_D float4 fetch32(const float4* base, long long n, float idx)
+{
+    if (!(idx >= 0.0f) || !(idx < (float)n)) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    return base[(unsigned)idx];   // data textures hold < 2^31 texels (checked at upload)
+}
+PT_D float unorm8(unsigned b) { return (float)b / 255.0f; }
+// REPEAT wrap of an integer-valued texel coordinate: fmod is exact, so any finite coordinate wraps
+// exactly; NaN/inf (degenerate uv) wrap to texel 0 (pinned, as the oracle)
+PT_D int wrapTexel(float f, int n)
+{
+    float r = fmodf(f, (float)n);
+    if (!(r == r)) r = 0.0f;
+    int i = (int)r;
+    return i < 0 ? i + n : i;
+}
+PT_D void texBilinear(const Tex8& t, float u, float v, float out[4])
+{
+    if (!t.p || t.w <= 0 || t.h <= 0) { out[0] = out[1] = out[2] = out[3] = 0.0f; return; }
+    float x = u * (float)t.w - 0.5f, y = v * (float)t.h - 0.5f;
+    float fx = floorf(x), fy = floorf(y);
+    float ax = x - fx, by = y - fy;
+    int x0 = wrapTexel(fx, t.w), y0 = wrapTexel(fy, t.h);
+    int x1 = x0 + 1 == t.w ? 0 : x0 + 1, y1 = y0 + 1 == t.h ? 0 : y0 + 1;
+    uchar4 t00 = t.p[y0 * t.w + x0], t10 = t.p[y0 * t.w + x1], t01 = t.p[y1 * t.w + x0], t11 = t.p[y1 * t.w + x1];
+    out[0] = gmix(gmix(unorm8(t00.x), unorm8(t10.x), ax), gmix(unorm8(t01.x), unorm8(t11.x), ax), by);
+    out[1] = gmix(gmix(unorm8(t00.y), unorm8(t10.y), ax), gmix(unorm8(t01.y), unorm8(t11.y), ax), by);
+    out[2] = gmix(gmix(unorm8(t00.z), unorm8(t10.z), ax), gmix(unorm8(t01.z), unorm8(t11.z), ax), by);
+    out[3] = gmix(gmix(unorm8(t00.w), unorm8(t10.w), ax), gmix(unorm8(t01.w), unorm8(t11.w), ax), by);
+}
+
+struct Hit {
+    float t;
+    f3 normal, color;
+    float u, v;
+    int type;
+    int id;
+};
+
+struct Cnt {
+    unsigned seg, node, leaf, hit, tap, ovf;
+};
+
+// SceneIntersect: js/BabylonPathTracing_FragmentShader.js:47-112 (Cornell) and
+// js/GLTFModelPathTracing_FragmentShader.js:116-346 (glTF, with the BVH walk). The object loops
+// stay rolled (#pragma unroll 1): each iteration re-reads its sphere / triangle from the kernarg
+// segment through the scalar cache, which keeps ~130 wave-uniform floats out of VGPRs and the
+// code small enough for the instruction cache.
+template <int PROG, bool COUNT>
+PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* lds, unsigned lane_slot,
+                         float2* deep, Cnt& cnt)
+{
+    if (COUNT) cnt.seg++;
+    h.t = kINF;
+    h.type = -100;
+    h.id = -1;
+    f3 sn = mk(0, 0, 0);
+#pragma unroll 1
+    for (int s = 0; s < 2; s++) {
+        const SphereArg& S = a.sph[s];
+        f3 n;
+        float d = unitSphere(mul(S.inv, rayO, 1.0f), mul(S.inv, rayD, 0.0f), n);
+        if (d < h.t) { h.t = d; h.id = s; sn = n; }
+    }
+#pragma unroll 1
+    for (int i = 0; i < 6; i++) {
+        float d = gmin(quadTriangle(a.qtri[2 * i], rayO, rayD), quadTriangle(a.qtri[2 * i + 1], rayO, rayD));
+        if (d < h.t) { h.t = d; h.id = 2 + i; }
+    }
+    // resolve the closest analytic hit's attributes once (the GLSL writes them at every closer hit;
+    // only the last write survives)
+    if (h.id >= 0 && h.id < 2) {
+        const SphereArg& S = a.sph[h.id];
+        h.normal = normalize(mul3t(S.inv, normalize(sn)));
+        h.color = S.color; h.type = S.type;
+    } else if (h.id >= 2) {
+        h.normal = normalize(a.qnormal[h.id - 2]);
+        h.color = a.qcolor[h.id - 2]; h.type = a.qtype[h.id - 2];
+    }
+    if (!kIsGltf<PROG>) return;
+
+    // ---- BVH walk over the BVH_Fast_Builder texture layout (js/GLTFModelPathTracing_FragmentShader.js:201-298)
+    f3 O = mul(a.model, rayO, 1.0f), D = mul(a.model, rayD, 0.0f);
+    f3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+    const bool dbl = (!a.uses_albedo && a.model_mat == TRANSPARENT);
+    float stackptr = 0.0f;
+    float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
+    if (COUNT) cnt.node++;
+    float curId = 0.0f;
+    float curT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
+    lds[lane_slot] = make_float2(curId, curT);   // stackLevels[0] = root
+    bool skip = curT < h.t;
+    float triID = 0.0f, triU = 0.0f, triV = 0.0f;
+    bool lookup = false;
+    for (;;) {
+        if (!skip) {
+            stackptr = stackptr - 1.0f;
+            if (stackptr < 0.0f) break;
+            int si = (int)stackptr;
+            float2 e = si < kStackLds ? lds[si * kBlock + lane_slot] : deep[si - kStackLds];
+            curId = e.x; curT = e.y;
+            if (curT >= h.t) continue;
+            c0 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f);
+            c1 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f + 1.0f);
+            if (COUNT) cnt.node++;
+        }
+        skip = false;
+        if (c0.x < 0.0f) {   // inner node: both children, near first
+            float idA = curId + 1.0f, idB = c1.x;
+            float4 a0 = fetch32(a.aabb, a.aabb_texels, idA * 2.0f), a1 = fetch32(a.aabb, a.aabb_texels, idA * 2.0f + 1.0f);
+            float4 b0 = fetch32(a.aabb, a.aabb_texels, idB * 2.0f), b1 = fetch32(a.aabb, a.aabb_texels, idB * 2.0f + 1.0f);
+            if (COUNT) cnt.node += 2;
+            float tA = box(mk(a0.y, a0.z, a0.w), mk(a1.y, a1.z, a1.w), O, inv);
+            float tB = box(mk(b0.y, b0.z, b0.w), mk(b1.y, b1.z, b1.w), O, inv);
+            if (tB < tA) {
+                float ti = idB; idB = idA; idA = ti;
+                float tt = tB; tB = tA; tA = tt;
+                float4 x0 = b0; b0 = a0; a0 = x0;
+                float4 x1 = b1; b1 = a1; a1 = x1;
+            }
+            if (tB < h.t) { curId = idB; curT = tB; c0 = b0; c1 = b1; skip = true; }
+            if (tA < h.t) {
+                if (skip) {
+                    int si = (int)stackptr;
+                    if (si < kStackLds) lds[si * kBlock + lane_slot] = make_float2(idB, tB);
+                    else if (si < kStackLevels) deep[si - kStackLds] = make_float2(idB, tB);
+                    else { if (COUNT) cnt.ovf++; atomicOr(a.err, (unsigned)E_STACK); }
+                    stackptr = stackptr + 1.0f;
+                }
+                curId = idA; curT = tA; c0 = a0; c1 = a1; skip = true;
+            }
+            continue;
+        }
+        // leaf: one triangle per leaf
+        float id = 8.0f * c0.x;
+        float4 t0 = fetch32(a.tri, a.tri_texels, id), t1 = fetch32(a.tri, a.tri_texels, id + 1.0f),
+               t2 = fetch32(a.tri, a.tri_texels, id + 2.0f);
+        if (COUNT) cnt.leaf++;
+        float tu, tv;
+        float d = bvhTriangle(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
+        if (d < h.t) { h.t = d; triID = id; triU = tu; triV = tv; lookup = true; }
+    }
+    if (lookup) {
+        float4 v2 = fetch32(a.tri, a.tri_texels, triID + 2.0f), v3 = fetch32(a.tri, a.tri_texels, triID + 3.0f),
+               v4 = fetch32(a.tri, a.tri_texels, triID + 4.0f), v5 = fetch32(a.tri, a.tri_texels, triID + 5.0f);
+        if (COUNT) cnt.hit++;
+        float triW = 1.0f - triU - triV;
+        f3 nn = normalize(mk(v2.y, v2.z, v2.w) * triW + mk(v3.x, v3.y, v3.z) * triU + mk(v3.w, v4.x, v4.y) * triV);
+        h.u = triW * v4.z + triU * v5.x + triV * v5.z;
+        h.v = triW * v4.w + triU * v5.y + triV * v5.w;
+        if (kHasTex<PROG> && a.uses_bump) {   // perturbNormal(n, vec2(1), uv), js/GLTFModelPathTracing_FragmentShader.js:72-92
+            f3 S = onb_u(nn);
+            f3 T = cross(nn, S);
+            f3 N = normalize(nn);
+            if (dot(cross(S, T), N) < 0.0f) { S = S * -1.0f; T = T * -1.0f; }
+            float tx[4];
+            texBilinear(a.bump, h.u, h.v, tx);
+            if (COUNT) cnt.tap += 4;
+            f3 mN = normalize(mk(tx[0] * 2.0f - 1.0f, tx[1] * 2.0f - 1.0f, tx[2] * 2.0f - 1.0f));
+            mN.x *= 1.0f; mN.y *= 1.0f;
+            nn = normalize(S * mN.x + T * mN.y + N * mN.z);
+        }
+        h.normal = normalize(mul3t(a.model, nn));
+        h.type = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
+        h.color = mk(1.0f, 1.0f, 1.0f);
+        h.id = 8;
+    }
+}
+
+struct GOut {
+    f3 nrm, col;
+    float id, sharp;
+};
+
+PT_D f3 pow22(f3 c) { return mk(gpow(c.x, 2.2f), gpow(c.y, 2.2f), gpow(c.z, 2.2f)); }
+
+// CalculateRadiance: js/GLTFModelPathTracing_FragmentShader.js:351-609 and
+// js/BabylonPathTracing_FragmentShader.js:117-344 (METAL is a mirror there).
+// The reference's per-material branches are folded so that each sampling routine has ONE call
+// site (TRANSPARENT and CLEARCOAT_DIFFUSE share the Fresnel split; CLEARCOAT's transmitted branch
+// joins DIFFUSE's "cosine bounce or light sample" tail). The sequence of rng()/blueNoise_rand()
+// draws and every IEEE op per path are exactly the GLSL's.
+template <int PROG, bool COUNT>
+PT_D f3 radiance(const TraceArgs& a, Path& p, GOut& g, float2* lds, unsigned lane_slot, float2* deep, Cnt& cnt)
+{
+    constexpr bool gltf = kIsGltf<PROG>;
+    Hit h;
+    f3 accum = mk(0, 0, 0), mask = mk(1, 1, 1);
+    float roughness = 0.0f;   // metallicRoughness.g persists across bounces (:368, :496)
+    int diffuseCount = 0, hitType = -100;
+    bool coat = false, specular = true, sampleLight = false;
+
+#pragma unroll 1
+    for (int bounces = 0; bounces < 6; bounces++) {
+        const int prevType = hitType;
+        sceneIntersect<PROG, COUNT>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt);
+        hitType = h.type;
+        if (h.t == kINF) break;
+        f3 n = normalize(h.normal);
+        f3 nl = dot(n, p.rd) < 0.0f ? normalize(n) : normalize(-n);
+        f3 x = p.ro + p.rd * h.t;
+        if (bounces == 0) { g.nrm = nl; g.col = h.color; g.id = (float)h.id; }
+        if (bounces == 1 && prevType == METAL) { g.nrm = nl; g.id = (float)h.id; }
+
+        if (hitType == LIGHT) {
+            if (diffuseCount == 0) g.sharp = 1.01f;
+            if (specular || sampleLight) accum = mask * h.color;
+            break;
+        }
+        if (sampleLight) break;
+
+        if (kHasTex<PROG> && hitType == PBR_MATERIAL) {
+            float tx[4];
+            texBilinear(a.albedo, h.u, h.v, tx);
+            if (COUNT) cnt.tap += 4;
+            h.color = pow22(mk(tx[0], tx[1], tx[2]));
+            f3 emission = mk(0, 0, 0);
+            if (a.uses_emissive) { texBilinear(a.emissive, h.u, h.v, tx); if (COUNT) cnt.tap += 4; emission = mk(tx[0], tx[1], tx[2]); }
+            emission = pow22(emission);
+            float maxE = gmax(emission.x, gmax(emission.y, emission.z));
+            if (specular && maxE > 0.01f) { g.sharp = 1.01f; accum = mask * emission; break; }
+            hitType = DIFFUSE;
+            f3 mr = mk(0, 0, 0);
+            if (a.uses_metal) { texBilinear(a.metal, h.u, h.v, tx); if (COUNT) cnt.tap += 4; mr = mk(tx[0], tx[1], tx[2]); }
+            mr = pow22(mr);
+            roughness = mr.y;
+            if (mr.y > 0.01f) hitType = CLEARCOAT_DIFFUSE;
+            if (mr.z > 0.01f) hitType = METAL;
+        }
+
+        bool diffuseTail = hitType == DIFFUSE;
+        if (hitType == TRANSPARENT || hitType == CLEARCOAT_DIFFUSE) {
+            const bool glass = hitType == TRANSPARENT;
+            if (glass) {
+                if (diffuseCount == 0 && !coat && !a.moving) g.sharp = 1.01f;
+                else if (diffuseCount > 0) g.sharp = 0.0f;
+                else g.sharp = -1.0f;
+            } else {
+                coat = true;
+                g.sharp = 0.0f;
+            }
+            float ratio;
+            float Re = fresnel(p.rd, glass ? n : nl, 1.0f, glass ? 1.5f : 1.4f, ratio);
+            float Tr = 1.0f - Re;
+            float P = 0.25f + (0.5f * Re);
+            float RP = Re / P, TP = Tr / (1.0f - P);
+            if (blueNoise_rand(p) < P) {            // specular reflection off the interface
+                if (!glass && diffuseCount == 0) g.sharp = a.frame > 500.0f ? 1.01f : -1.0f;
+                mask = mask * RP;
+                p.rd = reflect(p.rd, nl);
+                p.ro = x + nl * a.eps;
+                continue;
+            }
+            if (glass) {                             // refraction through the dielectric
+                if (distance(n, nl) > 0.1f) {
+                    const float thickness = 0.01f;
+                    f3 cc = clamp3(h.color, 0.01f, 0.99f);
+                    mask = mask * mk(gexp(glog(cc.x) * thickness * h.t), gexp(glog(cc.y) * thickness * h.t),
+                                     gexp(glog(cc.z) * thickness * h.t));
+                }
+                mask = mask * TP;
+                p.rd = refract(p.rd, nl, ratio);
+                p.ro = x - nl * a.eps;
+                if (diffuseCount == 1) specular = true;
+                continue;
+            }
+            mask = mask * TP;                        // clear coat transmits into its diffuse base
+            diffuseTail = true;
+        }
+        if (diffuseTail) {
+            diffuseCount++;
+            mask = mask * h.color;
+            specular = false;
+            if (diffuseCount == 1 && blueNoise_rand(p) < 0.5f) {
+                p.rd = cosWeightedDir(p, nl);
+            } else {
+                float w;
+                f3 dl = sampleQuadLight(p, a, x, nl, w);
+                mask = mask * w;
+                p.rd = dl;
+                if (hitType == DIFFUSE || bounces < 3) sampleLight = true;
+            }
+            p.ro = x + nl * a.eps;
+            continue;
+        }
+        if (hitType == METAL) {
+            mask = mask * h.color;
+            if (gltf) p.rd = specularLobeDir(p, reflect(p.rd, nl), roughness);
+            else p.rd = reflect(p.rd, nl);
+            p.ro = x + nl * a.eps;
+            continue;
+        }
+    }
+    return max3s(accum, 0.0f);
+}
+
+PT_D float xorq(float v, int m) { return __shfl_xor(v, m, 64); }
+
+template <int PROG, bool COUNT>
+__global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
+{
+    __shared__ float2 lds_stack[kStackLds * kBlock];
+    const unsigned tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int lx = (lane & 1) | ((lane >> 1) & 6);
+    const int ly = ((lane >> 1) & 1) | ((lane >> 3) & 6);
+    const int band = blockIdx.y * a.num_parts + a.part;         // global 16-row band of this block
+    const int px = blockIdx.x * kTile + (wave & 1) * 8 + lx;
+    const int py = band * kTile + (wave >> 1) * 8 + ly;
+    float2 deep[kStackLevels - kStackLds];
+
+    // lanes whose whole 2x2 quad lies beyond the (even-rounded) target do no work; quad helpers
+    // that only complete a quad at an odd edge are shaded like GL helper invocations
+    const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1);
+    Cnt cnt = { 0, 0, 0, 0, 0, 0 };
+    GOut g;   // pinned: the `out` parameters of CalculateRadiance start at 0
+    g.nrm = mk(0, 0, 0); g.col = mk(0, 0, 0); g.id = 0.0f; g.sharp = 0.0f;
+    f3 r = mk(0, 0, 0);
+    if (active) {
+        // ---- main(): camera ray (js/PathTracingCommon.js:1259-1292)
+        const float* m = a.cam.m;
+        f3 camRight = mk(m[0], m[1], m[2]), camUp = mk(m[4], m[5], m[6]), camFwd = mk(m[8], m[9], m[10]);
+        f3 camPos = mk(m[12], m[13], m[14]);
+        float fcx = (float)px + 0.5f, fcy = (float)py + 0.5f;
+        Path p;
+        p.s0 = (uint32_t)a.frame * (uint32_t)fcx;
+        p.s1 = (uint32_t)(a.frame + 1.0f) * (uint32_t)fcy;
+        p.counter = -1.0f;
+        int bx = (int)gmod(fcx + floorf(a.rnd[0] * 256.0f), 256.0f);
+        int by = (int)gmod(fcy + floorf(a.rnd[1] * 256.0f), 256.0f);
+        p.bn0 = 0.0f; p.bn1 = 0.0f;
+        if (bx < a.bluenoise.w && by < a.bluenoise.h) {
+            uchar4 b = a.bluenoise.p[by * a.bluenoise.w + bx];
+            p.bn0 = unorm8(b.x); p.bn1 = unorm8(b.y);
+        }
+        float ox = tentFilter(rng(p));
+        float oy = tentFilter(rng(p));
+        float ppx = ((fcx + ox) / a.res[0]) * 2.0f - 1.0f;
+        float ppy = ((fcy + oy) / a.res[1]) * 2.0f - 1.0f;
+        f3 rayDir = normalize((camRight * ppx) * a.ulen + (camUp * ppy) * a.vlen + camFwd);
+        f3 focal = rayDir * a.focus;
+        float ang = rng(p) * kTwoPi;
+        float rad = rng(p) * a.aperture;
+        float sn, cs;
+        gsincos(ang, sn, cs);
+        f3 apert = (camRight * cs + camUp * sn) * sqrtf(rad);
+        p.rd = normalize(focal - apert);
+        p.ro = camPos + apert;
+        r = radiance<PROG, COUNT>(a, p, g, lds_stack, tid, deep, cnt);
+    }
+
+    // ---- 2x2 fine derivatives (js/PathTracingCommon.js:1306-1320): partner lanes ^1 (x) and ^2 (y)
+    const bool xodd = lane & 1, yodd = lane & 2;
+    auto ddx = [&](float v) { float o = xorq(v, 1); return xodd ? v - o : o - v; };
+    auto ddy = [&](float v) { float o = xorq(v, 2); return yodd ? v - o : o - v; };
+    float dNx = fabsf(ddx(g.nrm.x)) + fabsf(ddy(g.nrm.x));
+    float dNy = fabsf(ddx(g.nrm.y)) + fabsf(ddy(g.nrm.y));
+    float dNz = fabsf(ddx(g.nrm.z)) + fabsf(ddy(g.nrm.z));
+    float normalDiff = gsmoothstep(0.2f, 0.6f, dNx) + gsmoothstep(0.2f, 0.6f, dNy) + gsmoothstep(0.2f, 0.6f, dNz);
+    float dObj = fabsf(ddx(g.id)) > 0.0f ? 1.0f : 0.0f;
+    dObj += fabsf(ddy(g.id)) > 0.0f ? 1.0f : 0.0f;
+    float objectDiff = gsmoothstep(0.0f, 0.5f, dObj);
+    f3 dcx = mk(ddx(g.col.x), ddx(g.col.y), ddx(g.col.z));
+    f3 dcy = mk(ddy(g.col.x), ddy(g.col.y), ddy(g.col.z));
+    float dCol = length(dcx) > 0.0f ? 1.0f : 0.0f;
+    dCol += length(dcy) > 0.0f ? 1.0f : 0.0f;
+    float colorDiff = gsmoothstep(0.0f, 0.5f, dCol);
+
+    if (COUNT && active) {
+        unsigned long long* C = a.counters;
+        atomicAdd(&C[C_PATHS], 1ull);
+        atomicAdd(&C[C_SEGMENTS], (unsigned long long)cnt.seg);
+        atomicAdd(&C[C_NODE], (unsigned long long)cnt.node);
+        atomicAdd(&C[C_LEAF], (unsigned long long)cnt.leaf);
+        atomicAdd(&C[C_HIT], (unsigned long long)cnt.hit);
+        atomicAdd(&C[C_RGBA8], (unsigned long long)(cnt.tap + 1));
+        atomicAdd(&C[C_OVERFLOW], (unsigned long long)cnt.ovf);
+    }
+    if (px >= a.width || py >= a.height) return;   // quad helper outside the target
+
+    // ---- progressive accumulation (js/PathTracingCommon.js:1326-1357)
+    const long long pi = (long long)py * a.width + px;
+    float4 prev = a.prev[pi];
+    float cr = r.x, cg = r.y, cb = r.z, ca;
+    if (a.frame == 1.0f) prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    else if (a.moving) {
+        prev.x *= 0.5f; prev.y *= 0.5f; prev.z *= 0.5f;
+        cr *= 0.5f; cg *= 0.5f; cb *= 0.5f;
+        prev.w = 0.0f;
+    }
+    ca = 0.0f;
+    float sharp = g.sharp;
+    if (colorDiff >= 1.0f || normalDiff >= 1.0f || objectDiff >= 1.0f) sharp = 1.01f;
+    if (sharp == 1.01f) ca = 1.01f;
+    if (sharp == -1.0f) ca = -1.0f;
+    if (prev.w == 1.01f) ca = 1.01f;
+    if (prev.w == -1.0f) ca = 0.0f;
+    a.out[pi] = make_float4(prev.x + cr, prev.y + cg, prev.z + cb, ca);
+}
+
+template __global__ void pt_trace<PROG_CORNELL, false>(TraceArgs);
+template __global__ void pt_trace<PROG_CORNELL, true>(TraceArgs);
+template __global__ void pt_trace<PROG_GLTF, false>(TraceArgs);
+template __global__ void pt_trace<PROG_GLTF, true>(TraceArgs);
+template __global__ void pt_trace<PROG_GLTF_TEX, false>(TraceArgs);
+template __global__ void pt_trace<PROG_GLTF_TEX, true>(TraceArgs);
+
+// ------------------------------------------------------------------------------ screenCopy
+__global__ __launch_bounds__(256) void pt_copy(CopyArgs a)
+{
+    // one block per (16-row band, 256-texel column chunk); shards copy only their own bands
+    const int band = blockIdx.y * a.num_parts + a.part;
+    const int x = blockIdx.x * 256 + threadIdx.x;
+    if (x >= a.width) return;
+    for (int r = 0; r < kTile; r++) {
+        int y = band * kTile + r;
+        if (y >= a.height) return;
+        long long i = (long long)y * a.width + x;
+        a.dst[i] = a.src[i];
+    }
+}
+
+// ------------------------------------------------------------------------------ screenOutput
+PT_D float4 accAt(const OutputArgs& a, int x, int y)
+{
+    if (x < 0 || y < 0 || x >= a.acc_w || y >= a.acc_h) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    return a.acc[(long long)y * a.acc_w + x];
+}
+
+__global__ __launch_bounds__(256) void pt_output(OutputArgs a)
+{
+    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
+    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    if (x >= a.width || y >= a.height) return;
+    float4 m25[25];
+#pragma unroll
+    for (int k = 0; k < 25; k++) m25[k] = accAt(a, x + (k % 5) - 2, y + 2 - (k / 5));
+    const float th = 1.0f;
+    float4 cp = m25[12];
+    float fr = cp.x, fg = cp.y, fb = cp.z;
+    int count = 1;
+    // first-ring tap, then its two outer taps, in the reference's order (js/PathTracingCommon.js:82-209)
+    constexpr int T5[8][3] = { { 11, 10, 5 }, { 13, 14, 19 }, { 7, 2, 3 }, { 17, 22, 21 },
+                               { 6, 0, 1 }, { 8, 4, 9 }, { 16, 15, 20 }, { 18, 23, 24 } };
+#pragma unroll
+    for (int r = 0; r < 8; r++) {
+        if (m25[T5[r][0]].w < th) {
+            fr += m25[T5[r][0]].x; fg += m25[T5[r][0]].y; fb += m25[T5[r][0]].z; count++;
+            if (m25[T5[r][1]].w < th) { fr += m25[T5[r][1]].x; fg += m25[T5[r][1]].y; fb += m25[T5[r][1]].z; count++; }
+            if (m25[T5[r][2]].w < th) { fr += m25[T5[r][2]].x; fg += m25[T5[r][2]].y; fb += m25[T5[r][2]].z; count++; }
+        }
+    }
+    fr /= (float)count; fg /= (float)count; fb /= (float)count;
+    if (cp.w > 0.0f || cp.w == -1.0f) {
+        constexpr int R3[8] = { 11, 13, 7, 17, 6, 8, 16, 18 };
+        count = 1;
+        fr = cp.x; fg = cp.y; fb = cp.z;
+#pragma unroll
+        for (int r = 0; r < 8; r++)
+            if (m25[R3[r]].w < th) { fr += m25[R3[r]].x; fg += m25[R3[r]].y; fb += m25[R3[r]].z; count++; }
+        fr /= (float)count; fg /= (float)count; fb /= (float)count;
+        fr = gmix(fr, cp.x, 0.5f); fg = gmix(fg, cp.y, 0.5f); fb = gmix(fb, cp.z, 0.5f);
+    }
+    if ((cp.w == 1.01f && a.one_over_n < 0.005f) || a.one_over_n < 0.0002f) { fr = cp.x; fg = cp.y; fb = cp.z; }
+    fr *= a.one_over_n; fg *= a.one_over_n; fb *= a.one_over_n;
+    float c[3] = { fr * a.exposure, fg * a.exposure, fb * a.exposure };
+    float o[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        float v = gclamp(c[k] / (1.0f + c[k]), 0.0f, 1.0f);
+        o[k] = gclamp(gpow(v, 0.4545f), 0.0f, 1.0f);
+    }
+    const long long i = (long long)y * a.width + x;
+    if (a.canvas)
+        a.canvas[i] = make_uchar4((unsigned char)floorf(o[0] * 255.0f + 0.5f), (unsigned char)floorf(o[1] * 255.0f + 0.5f),
+                                  (unsigned char)floorf(o[2] * 255.0f + 0.5f), 255);
+    else
+        a.out_f[i] = make_float4(o[0], o[1], o[2], 1.0f);
+}
+
+// ------------------------------------------------------------------------------ self-test
+__global__ void pt_math_probe_kernel(int op, const float* x, const float* y, float* out, int n)
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float a = x[i], b = y ? y[i] : 0.0f;
+    float r = 0.0f;
+    switch (op) {
+    case 0: r = gexp2(a); break;
+    case 1: r = glog2(a); break;
+    case 2: r = gsin(a); break;
+    case 3: r = gcos(a); break;
+    case 4: r = gatan(a); break;
+    case 5: r = gatan2(a, b); break;
+    case 6: r = gacos(a); break;
+    case 7: r = gpow(a, b); break;
+    case 8: r = gexp(a); break;
+    case 9: r = glog(a); break;
+    case 10: r = sqrtf(a); break;
+    case 11: { Path p; p.s0 = (uint32_t)a; p.s1 = (uint32_t)b; r = rng(p); break; }
+    case 12: r = a / b; break;
+    case 13: r = 1.0f / sqrtf(a); break;
+    default: r = 0.0f;
+    }
+    out[i] = r;
+}
+
+} // namespace pt
+
+// ------------------------------------------------------------------------------ launchers
+extern "C" {
+
+hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s)
+{
+    dim3 grid(grid_x, grid_y), block(pt::kBlock);
+    // texture-free glTF models (the bench's StanfordBunny) take the variant without PBR code
+    if (prog == pt::PROG_GLTF && (a->uses_albedo || a->uses_bump)) prog = pt::PROG_GLTF_TEX;
+#define PT_LAUNCH(P)                                                                              \
+    do {                                                                                          \
+        if (count) hipLaunchKernelGGL((pt::pt_trace<P, true>), grid, block, 0, s, *a);             \
+        else hipLaunchKernelGGL((pt::pt_trace<P, false>), grid, block, 0, s, *a);                  \
+    } while (0)
+    switch (prog) {
+    case pt::PROG_CORNELL: PT_LAUNCH(pt::PROG_CORNELL); break;
+    case pt::PROG_GLTF: PT_LAUNCH(pt::PROG_GLTF); break;
+    case pt::PROG_GLTF_TEX: PT_LAUNCH(pt::PROG_GLTF_TEX); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef PT_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s)
+{
+    hipLaunchKernelGGL(pt::pt_copy, dim3(grid_x, grid_y), dim3(256), 0, s, *a);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s)
+{
+    dim3 grid((a->width + 15) / 16, (a->height + 15) / 16);
+    hipLaunchKernelGGL(pt::pt_output, grid, dim3(256), 0, s, *a);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s)
+{
+    hipLaunchKernelGGL(pt::pt_math_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, s, op, x, y, out, n);
+    return hipGetLastError();
+}
+
+}

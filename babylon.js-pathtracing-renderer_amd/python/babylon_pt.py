@@ -1,0 +1,433 @@
+"""Python binding of libpt.so (include/pt.h), shaped like the Babylon effect API the reference's
+setup scripts use, plus a replayer for recorded per-frame render-call streams.
+
+The reference host is JavaScript; its drop-in binding is the Node N-API addon + JS shim in
+../napi and ../js. This module is the same boundary seen from Python, for the parity tests and
+bench.py: the classes mirror
+
+  new BABYLON.Engine(canvas)                       -> Engine(device)
+  BABYLON.RawTexture.CreateRGBATexture(...)        -> RawTexture.CreateRGBATexture(...)
+  new BABYLON.Texture(url, ...) (decoded RGBA8)    -> Texture(engine, rgba8, ...)
+  new BABYLON.RenderTargetTexture(name, {w,h}, ..) -> RenderTargetTexture(name, (w, h), engine)
+  new BABYLON.EffectWrapper({...})                 -> EffectWrapper(engine, program, uniformNames, samplerNames)
+  wrapper.effect.setFloat/setFloat2/.../setTexture -> the same method names
+  new BABYLON.EffectRenderer(engine).render(w, t)  -> EffectRenderer(engine).render(w, t)
+
+(js/GLTF_Model_Path_Tracing.js:189, 466-487, 749-768, 770-848, 1230-1235). There is no CPU
+fallback: if libpt.so or a gfx950 device is missing, construction raises.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("PT_LIBPT", os.path.join(PKG, "libpt.so"))
+
+PROG = {"screenCopy": 1, "screenOutput": 2, "cornell": 3, "gltf": 4, "hdri": 5, "sky": 6, "quadric": 7}
+ERRORS = {0: "PT_OK", -1: "PT_ERR_ARG", -2: "PT_ERR_HIP", -3: "PT_ERR_SHADER", -4: "PT_ERR_STATE",
+          -5: "PT_ERR_OOM", -6: "PT_ERR_DEVICE", -7: "PT_ERR_UNSUPPORTED", -8: "PT_ERR_DATA"}
+NEAREST, BILINEAR, TRILINEAR = 1, 2, 3
+
+# every symbol include/pt.h declares (checked by tests/test_capi_symbols.py)
+SYMBOLS = [
+    "pt_ctx_create", "pt_ctx_destroy", "pt_last_error", "pt_sync", "pt_canvas_resize",
+    "pt_effect_create", "pt_effect_create_program", "pt_effect_destroy", "pt_effect_program",
+    "pt_set_float", "pt_set_int", "pt_set_texture",
+    "pt_texture_create_rgba32f", "pt_texture_create_rgba8", "pt_render_target_create", "pt_render_target_wrap",
+    "pt_render_target_resize", "pt_texture_size", "pt_texture_destroy",
+    "pt_render", "pt_read_pixels", "pt_write_pixels",
+    "pt_set_row_partition", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
+    "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_math_probe", "pt_version",
+]
+
+_lib = None
+
+
+def lib():
+    """Load libpt.so and declare the C signatures (no device call happens here)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libpt.so not built: run __graft_entry__.build() (%s)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, ip, i32, f32p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_float)
+    cpp = ctypes.POINTER(ctypes.c_char_p)
+    sig = {
+        "pt_ctx_create": ([i32, ip], vp), "pt_ctx_destroy": ([vp], None), "pt_last_error": ([vp], ctypes.c_char_p),
+        "pt_sync": ([vp], i32), "pt_canvas_resize": ([vp, i32, i32], i32),
+        "pt_effect_create": ([vp, ctypes.c_char_p, cpp, i32, cpp, i32, ip], vp),
+        "pt_effect_create_program": ([vp, i32, cpp, i32, cpp, i32, ip], vp),
+        "pt_effect_destroy": ([vp], None), "pt_effect_program": ([vp], i32),
+        "pt_set_float": ([vp, ctypes.c_char_p, f32p, i32], i32), "pt_set_int": ([vp, ctypes.c_char_p, i32], i32),
+        "pt_set_texture": ([vp, ctypes.c_char_p, vp], i32),
+        "pt_texture_create_rgba32f": ([vp, i32, i32, vp, i32, i32, ip], vp),
+        "pt_texture_create_rgba8": ([vp, i32, i32, vp, i32, i32, ip], vp),
+        "pt_render_target_create": ([vp, i32, i32, ip], vp),
+        "pt_render_target_wrap": ([vp, i32, i32, vp, ip], vp),
+        "pt_render_target_resize": ([vp, i32, i32], i32),
+        "pt_texture_size": ([vp, ip, ip], i32), "pt_texture_destroy": ([vp], None),
+        "pt_render": ([vp, vp], i32), "pt_read_pixels": ([vp, vp, vp, ctypes.c_size_t], i32),
+        "pt_write_pixels": ([vp, vp, vp, ctypes.c_size_t], i32),
+        "pt_set_row_partition": ([vp, i32, i32], i32), "pt_texture_device_ptr": ([vp], vp),
+        "pt_last_render_ms": ([vp, i32, f32p], i32), "pt_set_counting": ([vp, i32], i32),
+        "pt_timing_begin": ([vp], i32),
+        "pt_timing_end": ([vp, i32, ctypes.POINTER(ctypes.c_double), ip], i32),
+        "pt_read_counters": ([vp, ctypes.POINTER(ctypes.c_uint64)], i32), "pt_reset_counters": ([vp], i32),
+        "pt_math_probe": ([vp, i32, vp, vp, vp, i32], i32), "pt_version": ([], ctypes.c_char_p),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _lib = L
+    return L
+
+
+class PtError(RuntimeError):
+    pass
+
+
+def _names(seq):
+    arr = (ctypes.c_char_p * max(1, len(seq)))()
+    for i, s in enumerate(seq):
+        arr[i] = s.encode()
+    return arr
+
+
+class Engine:
+    """`new BABYLON.Engine(canvas)` -> one pt context (one HIP stream) on one gfx950 device."""
+
+    def __init__(self, device=0):
+        err = ctypes.c_int(0)
+        self.ctx = lib().pt_ctx_create(device, ctypes.byref(err))
+        if not self.ctx:
+            raise PtError("pt_ctx_create(device=%d) failed: %s" % (device, ERRORS.get(err.value, err.value)))
+        self.device = device
+        self._objs = []
+
+    def check(self, rc, what=""):
+        if rc != 0:
+            raise PtError("%s: %s (%s)" % (what, ERRORS.get(rc, rc), lib().pt_last_error(self.ctx).decode()))
+        return rc
+
+    def sync(self):
+        self.check(lib().pt_sync(self.ctx), "pt_sync")
+
+    def resize_canvas(self, w, h):
+        self.check(lib().pt_canvas_resize(self.ctx, w, h), "pt_canvas_resize")
+
+    def read_canvas(self, w, h):
+        out = np.zeros((h, w, 4), dtype=np.uint8)
+        self.check(lib().pt_read_pixels(self.ctx, None, out.ctypes.data, out.nbytes), "pt_read_pixels")
+        return out
+
+    def set_row_partition(self, parts, part):
+        self.check(lib().pt_set_row_partition(self.ctx, parts, part), "pt_set_row_partition")
+
+    def last_render_ms(self, program):
+        ms = ctypes.c_float(0)
+        self.check(lib().pt_last_render_ms(self.ctx, PROG.get(program, program), ctypes.byref(ms)), "pt_last_render_ms")
+        return ms.value
+
+    def timing_begin(self):
+        self.check(lib().pt_timing_begin(self.ctx), "pt_timing_begin")
+
+    def timing_end(self, program):
+        """(total device ms, launches) of `program` draws since timing_begin (synchronises)."""
+        t, n = ctypes.c_double(0), ctypes.c_int(0)
+        self.check(lib().pt_timing_end(self.ctx, PROG.get(program, program), ctypes.byref(t), ctypes.byref(n)), "pt_timing_end")
+        return t.value, n.value
+
+    def set_counting(self, on):
+        self.check(lib().pt_set_counting(self.ctx, 1 if on else 0))
+
+    def reset_counters(self):
+        self.check(lib().pt_reset_counters(self.ctx))
+
+    def counters(self):
+        buf = (ctypes.c_uint64 * 7)()
+        self.check(lib().pt_read_counters(self.ctx, buf), "pt_read_counters")
+        keys = ("paths", "segments", "node_fetches", "leaf_tests", "hit_lookups", "rgba8_taps", "stack_overflow")
+        return {k: int(v) for k, v in zip(keys, buf)}
+
+    def math_probe(self, op, x, y=None):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        y = None if y is None else np.ascontiguousarray(y, dtype=np.float32)
+        out = np.zeros_like(x)
+        self.check(lib().pt_math_probe(self.ctx, op, x.ctypes.data, None if y is None else y.ctypes.data,
+                                       out.ctypes.data, x.size), "pt_math_probe")
+        return out
+
+    def dispose(self):
+        if self.ctx:
+            lib().pt_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.dispose()
+        except Exception:
+            pass
+
+
+class _Tex:
+    def __init__(self, engine, handle, name):
+        self.engine, self.handle, self.name = engine, handle, name
+
+    def getSize(self):
+        w, h = ctypes.c_int(0), ctypes.c_int(0)
+        lib().pt_texture_size(self.handle, ctypes.byref(w), ctypes.byref(h))
+        return {"width": w.value, "height": h.value}
+
+    def dispose(self):
+        if self.handle and self.engine.ctx:
+            lib().pt_texture_destroy(self.handle)
+        self.handle = None
+
+
+class RenderTargetTexture(_Tex):
+    """RGBA32F render target, zero-filled (js/GLTF_Model_Path_Tracing.js:762-768)."""
+
+    def __init__(self, name, size, engine, device_ptr=None):
+        w, h = (size["width"], size["height"]) if isinstance(size, dict) else size
+        err = ctypes.c_int(0)
+        if device_ptr is None:
+            hnd = lib().pt_render_target_create(engine.ctx, w, h, ctypes.byref(err))
+        else:   # caller-owned device memory (e.g. a torch tensor shared with RCCL)
+            hnd = lib().pt_render_target_wrap(engine.ctx, w, h, ctypes.c_void_p(device_ptr), ctypes.byref(err))
+        if not hnd:
+            raise PtError("pt_render_target_create: %s" % ERRORS.get(err.value, err.value))
+        super().__init__(engine, hnd, name)
+
+    def resize(self, size):
+        w, h = (size["width"], size["height"]) if isinstance(size, dict) else size
+        self.engine.check(lib().pt_render_target_resize(self.handle, w, h), "resize")
+
+    def read(self):
+        s = self.getSize()
+        out = np.zeros((s["height"], s["width"], 4), dtype=np.float32)
+        self.engine.check(lib().pt_read_pixels(self.engine.ctx, self.handle, out.ctypes.data, out.nbytes), "read")
+        return out
+
+    def write(self, arr):
+        arr = np.ascontiguousarray(arr, dtype=np.float32)
+        self.engine.check(lib().pt_write_pixels(self.engine.ctx, self.handle, arr.ctypes.data, arr.nbytes), "write")
+
+    def device_ptr(self):
+        return lib().pt_texture_device_ptr(self.handle)
+
+
+class RawTexture(_Tex):
+    @staticmethod
+    def CreateRGBATexture(data, w, h, engine, generateMipMaps=False, invertY=False, samplingMode=NEAREST, name=None):
+        """RGBA32F data texture (js/GLTF_Model_Path_Tracing.js:466-487); data is copied."""
+        arr = np.ascontiguousarray(np.asarray(data, dtype=np.float32).reshape(-1))
+        if arr.size < 4 * w * h:
+            arr = np.concatenate([arr, np.zeros(4 * w * h - arr.size, np.float32)])
+        err = ctypes.c_int(0)
+        hnd = lib().pt_texture_create_rgba32f(engine.ctx, w, h, arr.ctypes.data, samplingMode, 1 if invertY else 0, ctypes.byref(err))
+        if not hnd:
+            raise PtError("pt_texture_create_rgba32f: %s" % ERRORS.get(err.value, err.value))
+        return RawTexture(engine, hnd, name or "raw")
+
+
+class Texture(_Tex):
+    """An 8-bit image texture (the blue-noise PNG, PBR maps), decoded by the host to RGBA8."""
+
+    def __init__(self, engine, rgba8, invertY=False, samplingMode=NEAREST, name="texture"):
+        arr = np.ascontiguousarray(rgba8, dtype=np.uint8)
+        h, w = arr.shape[:2]
+        err = ctypes.c_int(0)
+        hnd = lib().pt_texture_create_rgba8(engine.ctx, w, h, arr.ctypes.data, samplingMode, 1 if invertY else 0, ctypes.byref(err))
+        if not hnd:
+            raise PtError("pt_texture_create_rgba8: %s" % ERRORS.get(err.value, err.value))
+        super().__init__(engine, hnd, name)
+
+
+class Effect:
+    """wrapper.effect: the uniform/sampler setters of js/GLTF_Model_Path_Tracing.js:818-847."""
+
+    def __init__(self, engine, handle):
+        self.engine, self.handle = engine, handle
+
+    def _f(self, name, vals):
+        arr = (ctypes.c_float * len(vals))(*vals)
+        self.engine.check(lib().pt_set_float(self.handle, name.encode(), arr, len(vals)), "setFloat " + name)
+
+    def setFloat(self, name, v):
+        self._f(name, [v])
+
+    def setFloat2(self, name, a, b):
+        self._f(name, [a, b])
+
+    def setFloat3(self, name, a, b, c):
+        self._f(name, [a, b, c])
+
+    def setMatrix(self, name, m):
+        self._f(name, list(m))
+
+    def setInt(self, name, v):
+        self.engine.check(lib().pt_set_int(self.handle, name.encode(), int(v)), "setInt " + name)
+
+    def setBool(self, name, v):
+        self.setInt(name, 1 if v else 0)
+
+    def setTexture(self, name, tex):
+        self.engine.check(lib().pt_set_texture(self.handle, name.encode(), tex.handle if tex is not None else None), "setTexture")
+
+
+class EffectWrapper:
+    """EffectWrapper({engine, fragmentShader, uniformNames, samplerNames, name}).
+
+    `program` is either the GLSL text registered in Effect.ShadersStore (as the JS shim passes it)
+    or a program key from PROG (hosts that do not carry the reference's shader text)."""
+
+    def __init__(self, engine, program, uniformNames=(), samplerNames=(), name="effect"):
+        err = ctypes.c_int(0)
+        un, sn = _names(list(uniformNames)), _names(list(samplerNames))
+        if isinstance(program, str) and program in PROG:
+            hnd = lib().pt_effect_create_program(engine.ctx, PROG[program], un, len(uniformNames), sn, len(samplerNames), ctypes.byref(err))
+        else:
+            src = program.encode() if isinstance(program, str) else program
+            hnd = lib().pt_effect_create(engine.ctx, src, un, len(uniformNames), sn, len(samplerNames), ctypes.byref(err))
+        if not hnd:
+            raise PtError("EffectWrapper(%s): %s (%s)" % (name, ERRORS.get(err.value, err.value), lib().pt_last_error(engine.ctx).decode()))
+        self.engine, self.name = engine, name
+        self.effect = Effect(engine, hnd)
+        self._observers = []
+        self.onApplyObservable = self
+
+    def add(self, fn):                      # onApplyObservable.add(cb)
+        self._observers.append(fn)
+
+    def program(self):
+        return lib().pt_effect_program(self.effect.handle)
+
+
+class EffectRenderer:
+    """eRenderer.render(wrapper, target): fire onApply observers, then draw (target None = canvas)."""
+
+    def __init__(self, engine):
+        self.engine = engine
+
+    def render(self, wrapper, target=None):
+        for fn in wrapper._observers:
+            fn()
+        rc = lib().pt_render(wrapper.effect.handle, target.handle if target is not None else None)
+        self.engine.check(rc, "render(%s)" % wrapper.name)
+
+
+# ------------------------------------------------------------------------------------------------
+# Replaying recorded render-call streams (tests/golden/*.json): the same effect.set* calls, sampler
+# bindings and draw order the reference's setup scripts issued, through this boundary.
+
+SHADER_PROG = {"pathTracingFragmentShader": None, "screenCopyFragmentShader": "screenCopy",
+               "screenOutputFragmentShader": "screenOutput"}
+
+
+def splitmix64_uniforms(seed, n):
+    """n floats in [0,1) with 24-bit resolution (exact in fp32): the Math.random stand-in the
+    fixture generator installs (tests/golden/gen/make_fixtures.js)."""
+    M = (1 << 64) - 1
+    st, out = seed & M, []
+    for _ in range(n):
+        st = (st + 0x9E3779B97F4A7C15) & M
+        z = st
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        z ^= z >> 31
+        out.append((z >> 40) / 16777216.0)
+    return out
+
+
+class StreamPlayer:
+    """Drives the boundary with a recorded per-frame call stream, the way the setup script's
+    render loop does (js/GLTF_Model_Path_Tracing.js:1087-1235): per frame set uniforms + samplers
+    on each wrapper and render pathTracing -> screenCopy -> screenOutput."""
+
+    def __init__(self, engine, meta, bluenoise, mesh=None, width=None, height=None, rt_ptrs=None):
+        self.engine = engine
+        self.meta = meta
+        w = width or meta["width"]
+        h = height or meta["height"]
+        self.width, self.height = w, h
+        scene = meta["scene"]
+        rt_ptrs = rt_ptrs or {}
+        self.textures = {
+            n: RenderTargetTexture(n, (w, h), engine, rt_ptrs.get(n))
+            for n in ("pathTracingRenderTarget", "screenCopyRenderTarget")
+        }
+        self.textures["file:BlueNoise_RGBA256.png"] = Texture(engine, bluenoise, name="blueNoise")
+        if mesh is not None:
+            for raw, kind in meta["textures"].items():
+                self.textures[raw] = RawTexture.CreateRGBATexture(mesh[kind], 2048, 2048, engine, name=kind)
+        self.renderer = EffectRenderer(engine)
+        self.wrappers = {}
+        for call in meta["frames"][0]:
+            key = SHADER_PROG[call["shader"]] or scene
+            self.wrappers[call["effect"]] = EffectWrapper(engine, key, list(call["uniforms"].keys()),
+                                                          list(call["samplers"].keys()), call["effect"])
+        self.override = {}
+        if w != meta["width"] or h != meta["height"]:
+            # what handleWindowResize() + onApply recompute for a new canvas size (:521-537, :815-816)
+            vlen = path_uniform(meta["frames"][0], "uVLen")
+            self.override = {"uResolution": ["f", [float(w), float(h)]], "uULen": ["f", [vlen * (w / h)]]}
+
+    def play_call(self, call, uniform_override=None):
+        wr = self.wrappers[call["effect"]]
+        fx = wr.effect
+        uniforms = dict(call["uniforms"])
+        uniforms.update({k: v for k, v in self.override.items() if k in uniforms})
+        if uniform_override:
+            uniforms.update({k: v for k, v in uniform_override.items() if k in uniforms})
+        for name, (kind, vals) in uniforms.items():
+            if kind == "i":
+                fx.setInt(name, vals[0])
+            else:
+                fx._f(name, vals)
+        for name, tex in call["samplers"].items():
+            fx.setTexture(name, self.textures.get(tex) if tex else None)
+        target = self.textures[call["target"]] if call["target"] else None
+        self.renderer.render(wr, target)
+
+    def play_frame(self, i, uniform_override=None):
+        for call in self.meta["frames"][i]:
+            self.play_call(call, uniform_override)
+
+    def synth_frame(self, k, seed=12345):
+        """Frame k after the recording ends, camera still: what the render loop pushes next
+        (uFrameCounter/uSampleCounter += 1, uCameraIsMoving false, a fresh uRandomVec2)."""
+        last = self.meta["frames"][-1]
+        fc = path_uniform(last, "uFrameCounter") + 1 + k
+        sc = path_uniform(last, "uSampleCounter") + 1 + k
+        r = splitmix64_uniforms(seed * 1000003 + k, 2)
+        frame = []
+        for call in last:
+            c = dict(call)
+            u = dict(call["uniforms"])
+            if "uFrameCounter" in u:
+                u["uFrameCounter"] = ["f", [float(fc)]]
+                u["uSampleCounter"] = ["f", [float(sc)]]
+                u["uCameraIsMoving"] = ["i", [0]]
+                u["uRandomVec2"] = ["f", r]
+                u["uTime"] = ["f", [u["uTime"][1][0] + (k + 1) / 60.0]]
+            if "uOneOverSampleCounter" in u:
+                u["uOneOverSampleCounter"] = ["f", [1.0 / sc]]
+            c["uniforms"] = u
+            frame.append(c)
+        return frame
+
+
+def path_uniform(frame, name):
+    for c in frame:
+        if c["shader"] == "pathTracingFragmentShader":
+            return c["uniforms"][name][1][0]
+    raise KeyError(name)
+
+
+def load_stream(path):
+    with open(path) as f:
+        return json.load(f)

@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""bench.py — Mpaths/s of the reference's per-pixel path-tracing frame on MI355X.
+
+Workload (BASELINE.json configs[1]): the StanfordBunny glTF scene (BVH + triangle textures exactly
+as the reference's BVH_Fast_Builder / Prepare_Model_For_PathTracing produce them, tests/golden),
+1920x1080, 1 sample per pixel per frame, driven through the Babylon-effect-shaped C ABI with the
+uniform stream the reference setup script pushes (recorded, then continued with fresh
+uRandomVec2 per frame). One step = one displayed frame = pathTracing + screenCopy +
+screenOutput, as in the reference's render loop (js/GLTF_Model_Path_Tracing.js:1228-1235).
+
+Multi-GPU (one process per GPU, launched by torch.distributed.run): weak scaling over the
+framebuffer. N GPUs render a frame of N x 2.07 MP (1920x1080, 3840x1080, 3840x2160, 7680x2160 for
+N = 1, 2, 4, 8), split into 16-row bands dealt round-robin (pt_set_row_partition); each frame
+the ranks' accumulation bands are gathered to rank 0 over RCCL and rank 0 runs screenOutput.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "babylon.js-pathtracing-renderer_amd")
+sys.path.insert(0, os.path.join(PKG, "python"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+FRAME_SIZES = {1: (1920, 1080), 2: (3840, 1080), 4: (3840, 2160), 8: (7680, 2160)}
+PEAK_HBM_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# algorithmic bytes per counted event
+BYTES = {"node_fetches": 32, "leaf_tests": 48, "hit_lookups": 64, "rgba8_taps": 4}
+PIXEL_IO = 32                  # previousBuffer texel read + accumulation texel write
+
+
+def frame_size(n):
+    if n in FRAME_SIZES:
+        return FRAME_SIZES[n]
+    return 1920, 1080 * n
+
+
+def algorithmic_bytes(cnt):
+    return sum(cnt[k] * b for k, b in BYTES.items()) + PIXEL_IO * cnt["paths"]
+
+
+def cpu_baseline(meta, width, height, budget_s):
+    """The CPU oracle (C restatement of the reference GLSL, OpenMP over rows) on this host,
+    timing whole 1920x1080 frames of the same stream until ~budget_s of wall time is spent."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import helpers as H
+    cores = min(16, os.cpu_count() or 1)
+    sc = H.oracle_scene(meta, width, height)
+    acc = np.zeros((height, width, 4), np.float32)
+    frames, t0 = 0, time.perf_counter()
+    while True:
+        f = meta["frames"][frames % len(meta["frames"])]
+        u = H.with_resolution(H.path_call(f)["uniforms"], width, height)
+        acc, _ = sc.path_trace(u, acc, nthreads=cores)
+        frames += 1
+        dt = time.perf_counter() - t0
+        if dt > budget_s or frames >= 200:
+            break
+    return {"value": round(frames * width * height / dt / 1e6, 3), "unit": "Mpaths/s", "cores": cores,
+            "kind": "port",
+            "sample": "%d full %dx%d frames of the bunny stream, CPU oracle (C restatement, OpenMP %d threads), %.1f s"
+                      % (frames, width, height, cores, dt)}
+
+
+def load_pmc(workload):
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f)
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-oracle baseline (0 = skip)")
+    ap.add_argument("--no-output", action="store_true", help="time pathTracing+copy only (no screenOutput/gather)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = tdist
+
+    import babylon_pt as bp
+    import helpers as H
+
+    meta = H.stream("gltf_bunny_1080p")
+    W, Hh = frame_size(world)
+    engine = bp.Engine(local)
+    mesh = H.texture_payloads(meta, H.mesh(meta))
+
+    rt_ptrs, acc_t, full_t = None, None, None
+    nb = (Hh + 15) // 16
+    pad_bands = ((nb + world - 1) // world) * world
+    if dist is not None:
+        import torch
+        # the accumulation target is the first H rows of a band-padded torch buffer, so a rank's
+        # bands are a strided view of it (no repacking of the whole frame)
+        acc_t = torch.zeros((pad_bands * 16, W, 4), dtype=torch.float32, device="cuda")
+        copy_t = torch.zeros((Hh, W, 4), dtype=torch.float32, device="cuda")
+        rt_ptrs = {"pathTracingRenderTarget": acc_t.data_ptr(), "screenCopyRenderTarget": copy_t.data_ptr()}
+        torch.cuda.synchronize()
+    player = bp.StreamPlayer(engine, meta, H.bluenoise(), mesh, W, Hh, rt_ptrs)
+    engine.resize_canvas(W, Hh)
+    engine.set_row_partition(world, rank)
+
+    # band bookkeeping for the gather: rows of 16-row bands b with b % world == rank
+    if dist is not None:
+        import torch
+        full_t = torch.zeros((pad_bands * 16, W, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
+        send_t = torch.zeros((pad_bands // world, 16, W, 4), dtype=torch.float32, device="cuda")
+        gather_list = [torch.empty_like(send_t) for _ in range(world)] if rank == 0 else None
+        out_rt = None
+        if rank == 0:
+            out_rt = bp.RenderTargetTexture("gathered", (W, Hh), engine, full_t.data_ptr())
+        out_wrapper = player.wrappers["screenOutputEffectWrapper"]
+
+    def step(k):
+        frame = player.synth_frame(k)
+        pt_call, cp_call, out_call = frame
+        player.play_call(pt_call)
+        player.play_call(cp_call)
+        if args.no_output:
+            return
+        if dist is None:
+            player.play_call(out_call)
+            return
+        # RCCL gather of the accumulation bands to rank 0, then screenOutput there
+        engine.sync()
+        send_t.copy_(acc_t.view(pad_bands // world, world, 16, W, 4)[:, rank])
+        dist.gather(send_t, gather_list, dst=0)
+        if rank == 0:
+            fv = full_t.view(pad_bands // world, world, 16, W, 4)
+            for r in range(world):
+                fv[:, r].copy_(gather_list[r])
+            torch.cuda.current_stream().synchronize()
+            fx = out_wrapper.effect
+            fx.setTexture("accumulationBuffer", out_rt)
+            u = out_call["uniforms"]
+            fx.setFloat("uOneOverSampleCounter", u["uOneOverSampleCounter"][1][0])
+            fx.setFloat("uToneMappingExposure", u["uToneMappingExposure"][1][0])
+            player.renderer.render(out_wrapper, None)
+
+    def barrier_sync():
+        engine.sync()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for k in range(args.warmup):
+        step(k)
+    barrier_sync()
+    engine.timing_begin()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, args.warmup + args.steps):
+        step(k)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    pt_ms, pt_n = engine.timing_end("gltf")
+    cp_ms, _ = engine.timing_end("screenCopy")
+    out_ms, _ = engine.timing_end("screenOutput")
+
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # algorithmic bytes of the measured launches: a counted (untimed) replay of the same frames
+    engine.set_counting(True)
+    engine.reset_counters()
+    nc = min(args.steps, 5)
+    for k in range(args.warmup, args.warmup + nc):
+        player.play_call(player.synth_frame(k)[0])
+    cnt = engine.counters()
+    engine.set_counting(False)
+    bytes_per_launch = algorithmic_bytes(cnt) / nc
+    if dist is not None:
+        import torch
+        t = torch.tensor([bytes_per_launch, cnt["paths"] / nc], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        bytes_total_launch = float(t[0].item())
+    else:
+        bytes_total_launch = bytes_per_launch
+
+    if rank != 0:
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+
+    paths = W * Hh * args.steps
+    value = paths / elapsed / 1e6
+    avg_launch_ms = pt_ms / max(1, pt_n)
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    workload = "gltf_bunny_%dx%d" % (W, Hh)
+    pmc = load_pmc(workload)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    line = {
+        "metric": "Mpaths/s (StanfordBunny glTF scene, 1 spp per frame, full pathTracing+screenCopy+screenOutput frame)",
+        "value": round(value, 2),
+        "unit": "Mpaths/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: the reference setup script's recorded StanfordBunny uniform stream, continued with fresh uRandomVec2 per frame; mesh textures = the reference BVH_Fast_Builder output",
+        "config": {"workload": workload, "width": W, "height": Hh, "spp_per_frame": 1, "max_bounces": 6,
+                   "triangles": int(meta.get("triangles", 0)), "parallelism": "row-bands x%d" % world,
+                   "gather": "rccl gather of RGBA32F bands to rank 0 per frame" if world > 1 else None},
+        "pathtrace_mpaths_per_s": round(W * Hh / world / (avg_launch_ms * 1e-3) / 1e6 * world, 2),
+        "kernel_ms": {"pathtrace": round(avg_launch_ms, 4), "screen_copy": round(cp_ms / max(1, pt_n), 4),
+                      "screen_output": round(out_ms / max(1, pt_n), 4)},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                     "kernel": "pt_trace<GLTF>", "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                     "counts_per_launch": {k: v / nc for k, v in cnt.items()}},
+    }
+    if args.cpu_budget > 0:
+        line["cpu_baseline"] = cpu_baseline(meta, 1920, 1080, args.cpu_budget) if world == 1 else None
+    print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

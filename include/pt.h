@@ -1,0 +1,150 @@
+/* include/pt.h — C ABI of libpt.so, the MI355X (gfx950) backend behind the Babylon.js effect API.
+ *
+ * The reference drives its hot path only through Babylon's effect API (js/babylon.js, vendored
+ * 5.0.0-alpha.43). Each entry point below is what a binding of that API needs; the comment on
+ * each names the reference call it replaces (file:line in the reference repository). A Node
+ * N-API addon (babylon.js-pathtracing-renderer_amd/napi/pt_napi.c) binds these for the
+ * unmodified setup scripts; ctypes binds them for tests and bench.py.
+ *
+ * Conventions: plain pointers and sizes; every call returns PT_OK (0) or a negative pt_status
+ * and never throws. Device memory is owned by the context. Host arrays are copied at the call.
+ * All work of a context goes onto one HIP stream; pt_render is asynchronous and
+ * pt_read_pixels / pt_sync synchronise. Not re-entrant (single JS thread, like the reference).
+ * Image rows are stored bottom-up (row 0 = gl_FragCoord.y 0.5), as GL render targets are.
+ */
+#ifndef PT_H
+#define PT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pt_ctx pt_ctx;
+typedef struct pt_effect pt_effect;
+typedef struct pt_texture pt_texture;
+
+enum pt_status {
+    PT_OK = 0,
+    PT_ERR_ARG = -1,         /* bad handle, size or name */
+    PT_ERR_HIP = -2,         /* HIP runtime error (message in pt_last_error) */
+    PT_ERR_SHADER = -3,      /* fragment source not recognised as a supported program */
+    PT_ERR_STATE = -4,       /* e.g. render with a required sampler unbound */
+    PT_ERR_OOM = -5,
+    PT_ERR_DEVICE = -6,      /* no usable gfx950 device */
+    PT_ERR_UNSUPPORTED = -7, /* recognised program that this build does not implement yet */
+    PT_ERR_DATA = -8         /* scene data outside the reference's limits (e.g. BVH deeper than stackLevels[28]) */
+};
+
+/* Programs recognised from the fragment source registered in Effect.ShadersStore. */
+enum pt_program {
+    PT_PROG_UNKNOWN = 0,
+    PT_PROG_SCREEN_COPY = 1,    /* js/PathTracingCommon.js:1-16 */
+    PT_PROG_SCREEN_OUTPUT = 2,  /* js/PathTracingCommon.js:19-309 */
+    PT_PROG_CORNELL = 3,        /* js/BabylonPathTracing_FragmentShader.js */
+    PT_PROG_GLTF = 4,           /* js/GLTFModelPathTracing_FragmentShader.js */
+    PT_PROG_HDRI = 5,           /* js/HDRIEnvironmentPathTracing_FragmentShader.js */
+    PT_PROG_SKY = 6,            /* js/PhysicalSkyModel_FragmentShader.js */
+    PT_PROG_QUADRIC = 7         /* js/TransformedQuadricGeometry_FragmentShader.js */
+};
+
+/* Babylon sampling-mode constants (BABYLON.Constants.TEXTURE_*_SAMPLINGMODE) */
+enum pt_sampling { PT_SAMPLING_NEAREST = 1, PT_SAMPLING_BILINEAR = 2, PT_SAMPLING_TRILINEAR = 3 };
+
+/* ---- context: replaces `new BABYLON.Engine(canvas, true)` (js/GLTF_Model_Path_Tracing.js:189) */
+pt_ctx* pt_ctx_create(int device, int* err);
+void pt_ctx_destroy(pt_ctx* ctx);
+const char* pt_last_error(pt_ctx* ctx);
+int pt_sync(pt_ctx* ctx);
+/* the default framebuffer ("canvas", RGBA8) that pt_render(effect, NULL) draws into;
+ * replaces engine.resize()/getRenderWidth() (js/GLTF_Model_Path_Tracing.js:521-537) */
+int pt_canvas_resize(pt_ctx* ctx, int width, int height);
+
+/* ---- effects: replaces `new BABYLON.EffectWrapper({engine, fragmentShader, uniformNames,
+ * samplerNames, name})` (js/GLTF_Model_Path_Tracing.js:773-811). The program is recognised from
+ * the GLSL text; unknown text -> NULL with *err = PT_ERR_SHADER. Uniform/sampler names not in the
+ * lists are ignored by the setters, as Babylon ignores undeclared uniforms. */
+pt_effect* pt_effect_create(pt_ctx* ctx, const char* fragment_source,
+                            const char* const* uniform_names, int n_uniforms,
+                            const char* const* sampler_names, int n_samplers, int* err);
+/* Same, with the program named directly (hosts that do not carry the reference's GLSL text,
+ * e.g. the Python binding replaying a recorded uniform stream on the GPU box). */
+pt_effect* pt_effect_create_program(pt_ctx* ctx, int program,
+                                    const char* const* uniform_names, int n_uniforms,
+                                    const char* const* sampler_names, int n_samplers, int* err);
+void pt_effect_destroy(pt_effect* fx);
+int pt_effect_program(const pt_effect* fx);
+
+/* ---- uniforms: replaces effect.setFloat / setFloat2 / setFloat3 / setVector3 / setMatrix /
+ * setInt / setBool (js/GLTF_Model_Path_Tracing.js:826-847). n = component count (1,2,3,4,16).
+ * setBool is setInt(0|1), as in Babylon. Returns PT_OK also for ignored (undeclared) names. */
+int pt_set_float(pt_effect* fx, const char* name, const float* v, int n);
+int pt_set_int(pt_effect* fx, const char* name, int v);
+/* effect.setTexture(sampler, texture) (js/GLTF_Model_Path_Tracing.js:818-825); tex NULL binds
+ * nothing (an unloaded Babylon texture) */
+int pt_set_texture(pt_effect* fx, const char* sampler, pt_texture* tex);
+
+/* ---- textures -------------------------------------------------------------------------------
+ * BABYLON.RawTexture.CreateRGBATexture(data, w, h, scene, mips, invertY, sampling, FLOAT)
+ * (js/GLTF_Model_Path_Tracing.js:466-487): RGBA32F, data copied. */
+pt_texture* pt_texture_create_rgba32f(pt_ctx* ctx, int width, int height, const float* data,
+                                      int sampling, int invert_y, int* err);
+/* new BABYLON.Texture(url, scene, noMipmap, invertY, sampling) of 8-bit images, decoded by the
+ * host (js/GLTF_Model_Path_Tracing.js:749-758): RGBA8, data copied. */
+pt_texture* pt_texture_create_rgba8(pt_ctx* ctx, int width, int height, const uint8_t* data,
+                                    int sampling, int invert_y, int* err);
+/* new BABYLON.RenderTargetTexture(name, {width,height}, scene, false, false, TEXTURETYPE_FLOAT,
+ * false, NEAREST, ...) (js/GLTF_Model_Path_Tracing.js:762-768): RGBA32F, zero-filled. */
+pt_texture* pt_render_target_create(pt_ctx* ctx, int width, int height, int* err);
+/* MI355X extension: an RGBA32F render target over caller-owned device memory (w*h*16 bytes on
+ * this context's device, e.g. a torch tensor that RCCL collectives also use). Not freed by
+ * pt_texture_destroy; not resizable. */
+pt_texture* pt_render_target_wrap(pt_ctx* ctx, int width, int height, void* device_ptr, int* err);
+/* renderTarget.resize({width,height}) (js/GLTF_Model_Path_Tracing.js:529-530) */
+int pt_render_target_resize(pt_texture* tex, int width, int height);
+/* renderTarget.getSize() (js/GLTF_Model_Path_Tracing.js:826) */
+int pt_texture_size(const pt_texture* tex, int* width, int* height);
+void pt_texture_destroy(pt_texture* tex);
+
+/* ---- draw: replaces eRenderer.render(effectWrapper, renderTargetOrNull)
+ * (js/GLTF_Model_Path_Tracing.js:1230-1235). target NULL = the canvas. */
+int pt_render(pt_effect* fx, pt_texture* target);
+
+/* readPixels of a render target (RGBA32F, 16 B/texel) or of the canvas (tex NULL, RGBA8),
+ * rows bottom-up; synchronises. */
+int pt_read_pixels(pt_ctx* ctx, const pt_texture* tex, void* dst, size_t bytes);
+/* Upload rows of a render target (RGBA32F), used to seed the history buffer in tests and to
+ * land gathered bands on the root in multi-GPU runs. */
+int pt_write_pixels(pt_ctx* ctx, pt_texture* tex, const void* src, size_t bytes);
+
+/* ---- MI355X extensions (no reference counterpart) -------------------------------------------
+ * Row-band sharding for multi-GPU rendering: this context's path-tracing passes shade only the
+ * 16-row bands b with b % num_parts == part (bands are whole 2x2 quads, so derivatives are
+ * unchanged). screenOutput/copy stay full-frame. num_parts = 1 restores full frames. */
+int pt_set_row_partition(pt_ctx* ctx, int num_parts, int part);
+/* Device pointer of a render target's RGBA32F storage (for RCCL collectives from the host). */
+void* pt_texture_device_ptr(pt_texture* tex);
+/* Device time of the last pt_render of each program kind, in ms (HIP events on the context
+ * stream; requires pt_sync first). */
+int pt_last_render_ms(pt_ctx* ctx, int program, float* ms);
+/* Timing window: between pt_timing_begin and pt_timing_end every draw is bracketed by its own
+ * HIP event pair (no host sync inside the window); pt_timing_end synchronises and returns the
+ * summed device time and launch count of one program kind. */
+int pt_timing_begin(pt_ctx* ctx);
+int pt_timing_end(pt_ctx* ctx, int program, double* total_ms, int* launches);
+/* Algorithmic-byte counters: when enabled, path-tracing passes also accumulate
+ * {paths, segments, node_fetches, leaf_tests, hit_lookups, rgba8_taps, stack_overflow}. */
+int pt_set_counting(pt_ctx* ctx, int enable);
+int pt_read_counters(pt_ctx* ctx, uint64_t out[7]);
+int pt_reset_counters(pt_ctx* ctx);
+/* Device self-test of the pinned GLSL built-ins (ops as the oracle's pto_math_probe). */
+int pt_math_probe(pt_ctx* ctx, int op, const float* x, const float* y, float* out, int n);
+/* Library identity: "libpt <version> gfx950" */
+const char* pt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -198,22 +198,27 @@ static float BVH_TriangleIntersect(v3 v0, v3 v1, v3 v2, v3 ro, v3 rd, float* u, 
 static const float* texel32(const float* base, int64_t n, float idx)
 {
     /* the GLSL computes ivec2(mod(i, 2048.0), i * (1/2048)); for i < 2^24 that is texel i */
-    int64_t i = (int64_t)idx;
     static const float zero4[4] = { 0, 0, 0, 0 };
-    if (i < 0 || i >= n) return zero4;
-    return base + 4 * i;
+    if (!(idx >= 0.0f) || !(idx < (float)n)) return zero4;
+    return base + 4 * (int64_t)idx;
 }
 static float unorm8(uint8_t b) { return (float)b / 255.0f; }
 /* texture(sampler, uv) on an RGBA8 map: LOD 0 bilinear, REPEAT wrap, unorm8 texels */
+static int wrap_texel(float f, int n)
+{
+    float r = fmodf(f, (float)n);   /* exact */
+    if (!(r == r)) r = 0.0f;         /* NaN / inf coordinates wrap to texel 0 (pinned) */
+    int i = (int)r;
+    return i < 0 ? i + n : i;
+}
 static void tex_bilinear(const uint8_t* t, int w, int h, float u, float v, float out[4])
 {
     if (!t || w <= 0 || h <= 0) { out[0] = out[1] = out[2] = out[3] = 0.0f; return; }
     float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
     float fx = floorf(x), fy = floorf(y);
     float a = x - fx, b = y - fy;
-    int64_t ix = (int64_t)fx, iy = (int64_t)fy;
-    int64_t x0 = ((ix % w) + w) % w, x1 = (((ix + 1) % w) + w) % w;
-    int64_t y0 = ((iy % h) + h) % h, y1 = (((iy + 1) % h) + h) % h;
+    int64_t x0 = wrap_texel(fx, w), y0 = wrap_texel(fy, h);
+    int64_t x1 = (x0 + 1) % w, y1 = (y0 + 1) % h;
     for (int c = 0; c < 4; c++) {
         float t00 = unorm8(t[4 * (y0 * w + x0) + c]), t10 = unorm8(t[4 * (y0 * w + x1) + c]);
         float t01 = unorm8(t[4 * (y1 * w + x0) + c]), t11 = unorm8(t[4 * (y1 * w + x1) + c]);
