@@ -1,0 +1,237 @@
+// babylon_pt.js — the drop-in: Babylon's effect API (EffectWrapper / EffectRenderer /
+// RenderTargetTexture / RawTexture / Texture / Engine render loop) implemented over libpt.so through
+// the N-API addon, so the reference's unmodified js/*_Path_Tracing.js setup scripts render on an
+// MI355X. Everything else those scripts use (Vector3, Matrix, TransformNode, UniversalCamera,
+// SceneLoader, Mesh.MergeMeshes, the glTF loader) stays the real Babylon running on NullEngine:
+// the scene graph is host-side bookkeeping, the pixels are produced by the gfx950 kernels.
+//
+//   const BABYLON = require('babylonjs');              // the vendored build the page loads
+//   require('.../js/babylon_pt.js').install(BABYLON, { width: 1920, height: 1080 });
+//   // ...then load js/PathTracingCommon.js, the scene shader and the setup script unchanged.
+//
+// Boundary map (reference call -> C ABI, include/pt.h):
+//   new BABYLON.Engine(canvas)                    -> pt_ctx_create           (js/GLTF_Model_Path_Tracing.js:189)
+//   new BABYLON.RenderTargetTexture(n,{w,h},...)  -> pt_render_target_create (:762-768), .resize -> pt_render_target_resize
+//   BABYLON.RawTexture.CreateRGBATexture(...)     -> pt_texture_create_rgba32f / _rgba8 (:466-487)
+//   new BABYLON.Texture(url, ...)                 -> host PNG decode + pt_texture_create_rgba8 (:749-758)
+//   new BABYLON.EffectWrapper({...})              -> pt_effect_create (GLSL text -> program) (:773-811)
+//   effect.setFloat/.../setMatrix/setTexture      -> pt_set_float / pt_set_int / pt_set_texture (:813-848)
+//   new BABYLON.EffectRenderer(engine).render()   -> pt_render (:1230-1235)
+'use strict';
+const fs = require('fs');
+const path = require('path');
+const zlib = require('zlib');
+
+const ERR = { 0: 'PT_OK', '-1': 'PT_ERR_ARG', '-2': 'PT_ERR_HIP', '-3': 'PT_ERR_SHADER', '-4': 'PT_ERR_STATE',
+  '-5': 'PT_ERR_OOM', '-6': 'PT_ERR_DEVICE', '-7': 'PT_ERR_UNSUPPORTED', '-8': 'PT_ERR_DATA' };
+const TEXTURETYPE_UNSIGNED_BYTE = 0;
+
+function loadAddon() {
+  return require(path.join(__dirname, '..', 'napi', 'pt_napi.node'));
+}
+
+// ---------------------------------------------------------------------------------- PNG (RGBA8/16)
+// The blue-noise texture is a 16-bit RGBA PNG; WebGL samples it as 8-bit. Pinned: high byte.
+function decodePNG(buf) {
+  if (buf.readUInt32BE(0) !== 0x89504e47) throw new Error('not a PNG');
+  let pos = 8, w = 0, h = 0, bd = 0, ct = 0;
+  const idat = [];
+  while (pos < buf.length) {
+    const len = buf.readUInt32BE(pos), type = buf.toString('ascii', pos + 4, pos + 8);
+    const body = buf.slice(pos + 8, pos + 8 + len);
+    if (type === 'IHDR') { w = body.readUInt32BE(0); h = body.readUInt32BE(4); bd = body[8]; ct = body[9]; if (body[12]) throw new Error('interlaced PNG'); }
+    else if (type === 'IDAT') idat.push(body);
+    pos += 12 + len;
+  }
+  const ch = { 6: 4, 2: 3, 0: 1, 4: 2 }[ct];
+  if (!ch || (bd !== 8 && bd !== 16)) throw new Error('unsupported PNG format');
+  const bpp = ch * bd / 8, stride = w * bpp;
+  const raw = zlib.inflateSync(Buffer.concat(idat));
+  const cur = Buffer.alloc(stride), prev = Buffer.alloc(stride);
+  const out = new Uint8Array(w * h * 4);
+  for (let y = 0, p = 0; y < h; y++) {
+    const ft = raw[p++];
+    for (let x = 0; x < stride; x++) {
+      const a = x >= bpp ? cur[x - bpp] : 0, b = prev[x], c = x >= bpp ? prev[x - bpp] : 0;
+      let v = raw[p++];
+      if (ft === 1) v += a; else if (ft === 2) v += b; else if (ft === 3) v += (a + b) >> 1;
+      else if (ft === 4) { const pa = Math.abs(b - c), pb = Math.abs(a - c), pc = Math.abs(a + b - 2 * c); v += (pa <= pb && pa <= pc) ? a : (pb <= pc ? b : c); }
+      cur[x] = v & 255;
+    }
+    for (let x = 0; x < w; x++) {
+      const px = [0, 0, 0, 255];
+      for (let k = 0; k < ch; k++) px[k] = cur[x * bpp + k * (bd / 8)];   // 16-bit: high byte
+      if (ch === 1) { px[1] = px[2] = px[0]; }
+      if (ch === 2) { px[3] = px[1]; px[1] = px[2] = px[0]; }
+      out.set(px, 4 * (y * w + x));
+    }
+    cur.copy(prev);
+  }
+  return { width: w, height: h, data: out };
+}
+
+function install(BABYLON, opts) {
+  opts = Object.assign({ device: 0, width: 1920, height: 1080, baseDir: process.cwd(), addon: null, onError: null,
+                        label: null }, opts || {});
+  const addon = opts.addon || loadAddon();
+  // opts.label(handle, name): optional debug hook naming each native handle (tracing tools)
+  const label = (h, name) => { if (opts.label && h && typeof h !== 'number') opts.label(h, name); return h; };
+  const report = opts.onError || ((msg) => console.error('[babylon_pt] ' + msg));
+  // with the real Babylon loaded, the scene graph runs on its NullEngine; without it (e.g. a replay
+  // host on the GPU box) a minimal base keeps the render-size bookkeeping
+  const RealNull = BABYLON.NullEngine || class {
+    constructor(o) { this._options = o; }
+    getRenderWidth() { return this._options.renderWidth; }
+    getRenderHeight() { return this._options.renderHeight; }
+    dispose() {}
+  };
+  const set = (k, v) => { try { BABYLON[k] = v; } catch (e) { Object.defineProperty(BABYLON, k, { value: v, writable: true, configurable: true }); } };
+  let current = null;   // the engine whose context owns textures created without an engine argument
+
+  function check(ctx, rc, what) {
+    if (typeof rc === 'number' && rc !== 0) report(what + ': ' + (ERR[rc] || rc) + ' ' + addon.pt_last_error(ctx));
+    return rc;
+  }
+  function ctxOf(sceneOrEngine) {
+    if (sceneOrEngine && sceneOrEngine._pt) return sceneOrEngine._pt;
+    if (sceneOrEngine && sceneOrEngine.getEngine && sceneOrEngine.getEngine()._pt) return sceneOrEngine.getEngine()._pt;
+    return current._pt;
+  }
+
+  class Engine extends RealNull {
+    constructor(canvas, antialias, options) {
+      const w = (canvas && canvas.width) || opts.width, h = (canvas && canvas.height) || opts.height;
+      super({ renderWidth: w, renderHeight: h, textureSize: 512, deterministicLockstep: false, lockstepMaxSteps: 1 });
+      const c = addon.pt_ctx_create(opts.device);
+      if (typeof c === 'number') throw new Error('pt_ctx_create: ' + (ERR[c] || c));
+      this._pt = c;
+      this._renderLoop = null;
+      this.isPointerLock = false;
+      addon.pt_canvas_resize(c, w, h);
+      current = this;
+    }
+    runRenderLoop(fn) { this._renderLoop = fn; }
+    // the browser calls the loop from requestAnimationFrame; a Node host steps it explicitly
+    stepFrame() { if (this._renderLoop) this._renderLoop(); }
+    enterPointerlock() {}
+    exitPointerlock() {}
+    setHardwareScalingLevel(l) { this._scaling = l; }
+    getDeltaTime() { return opts.deltaTimeMs || 1000 / 60; }
+    resize() { addon.pt_canvas_resize(this._pt, this.getRenderWidth(), this.getRenderHeight()); }
+    readCanvas() {
+      const out = new Uint8Array(this.getRenderWidth() * this.getRenderHeight() * 4);
+      check(this._pt, addon.pt_read_pixels(this._pt, null, out), 'readPixels');
+      return out;
+    }
+    dispose() { if (this._pt) { addon.pt_ctx_destroy(this._pt); this._pt = null; } super.dispose(); }
+  }
+
+  class RenderTargetTexture {
+    constructor(name, size, scene) {
+      this.name = name;
+      this._ctx = ctxOf(scene);
+      const h = addon.pt_render_target_create(this._ctx, size.width, size.height);
+      if (typeof h === 'number') throw new Error('RenderTargetTexture: ' + (ERR[h] || h));
+      this._pt = label(h, name);
+    }
+    getSize() { const s = addon.pt_texture_size(this._pt); return { width: s[0], height: s[1] }; }
+    resize(size) { check(this._ctx, addon.pt_render_target_resize(this._pt, size.width, size.height), 'resize'); }
+    readPixels() {
+      const s = this.getSize(), out = new Float32Array(s.width * s.height * 4);
+      check(this._ctx, addon.pt_read_pixels(this._ctx, this._pt, out), 'readPixels');
+      return out;
+    }
+    dispose() { if (this._pt) addon.pt_texture_destroy(this._pt); this._pt = null; }
+  }
+
+  const RawTexture = {
+    CreateRGBATexture(data, w, h, scene, generateMipMaps, invertY, samplingMode, type) {
+      const ctx = ctxOf(scene);
+      const t = { name: 'RawTexture', _ctx: ctx };
+      const sampling = samplingMode === undefined ? 3 : samplingMode;
+      const handle = type === TEXTURETYPE_UNSIGNED_BYTE || data instanceof Uint8Array
+        ? addon.pt_texture_create_rgba8(ctx, w, h, data, sampling, invertY ? 1 : 0)
+        : addon.pt_texture_create_rgba32f(ctx, w, h, data, sampling, invertY ? 1 : 0);
+      if (typeof handle === 'number') { report('CreateRGBATexture: ' + (ERR[handle] || handle)); return null; }
+      t._pt = label(handle, 'RawTexture');
+      t.dispose = () => { if (t._pt) addon.pt_texture_destroy(t._pt); t._pt = null; };
+      return t;
+    },
+  };
+
+  class Texture {
+    constructor(url, scene, noMipmap, invertY, samplingMode) {
+      this.name = url;
+      this._ctx = ctxOf(scene);
+      this._pt = null;
+      const file = path.isAbsolute(url) ? url : path.join(opts.baseDir, url);
+      try {
+        const img = decodePNG(fs.readFileSync(file));
+        const h = addon.pt_texture_create_rgba8(this._ctx, img.width, img.height, img.data, samplingMode === undefined ? 3 : samplingMode, invertY ? 1 : 0);
+        if (typeof h !== 'number') this._pt = label(h, url);
+      } catch (e) {
+        report('Texture(' + url + '): ' + e.message + ' (left unbound)');
+      }
+    }
+    readPixels() { return Promise.resolve(null); }
+    dispose() { if (this._pt) addon.pt_texture_destroy(this._pt); this._pt = null; }
+  }
+
+  class Effect {
+    constructor(ctx, handle) { this._ctx = ctx; this._pt = handle; }
+    isReady() { return this._pt !== null; }
+    _f(name, arr) { if (this._pt) check(this._ctx, addon.pt_set_float(this._pt, name, arr), 'set ' + name); return this; }
+    setFloat(n, v) { return this._f(n, [v]); }
+    setFloat2(n, a, b) { return this._f(n, [a, b]); }
+    setFloat3(n, a, b, c) { return this._f(n, [a, b, c]); }
+    setFloat4(n, a, b, c, d) { return this._f(n, [a, b, c, d]); }
+    setVector2(n, v) { return this._f(n, [v.x, v.y]); }
+    setVector3(n, v) { return this._f(n, [v.x, v.y, v.z]); }
+    setMatrix(n, m) { return this._f(n, Array.from(m.m !== undefined ? m.m : m.toArray())); }
+    setInt(n, v) { if (this._pt) check(this._ctx, addon.pt_set_int(this._pt, n, v | 0), 'setInt ' + n); return this; }
+    setBool(n, v) { return this.setInt(n, v ? 1 : 0); }
+    setTexture(n, t) {
+      // an unloaded Babylon texture (null / undefined, e.g. a model without albedo map) binds nothing
+      if (this._pt) check(this._ctx, addon.pt_set_texture(this._pt, n, t && t._pt ? t._pt : null), 'setTexture ' + n);
+      return this;
+    }
+  }
+
+  class EffectWrapper {
+    constructor(o) {
+      this.name = o.name;
+      const ctx = ctxOf(o.engine);
+      // o.ptProgram (extension): name the program directly when the GLSL text is not at hand
+      const h = o.ptProgram
+        ? addon.pt_effect_create_program(ctx, o.ptProgram, o.uniformNames || [], o.samplerNames || [])
+        : addon.pt_effect_create(ctx, o.fragmentShader || '', o.uniformNames || [], o.samplerNames || []);
+      label(h, o.name);
+      if (typeof h === 'number') report('EffectWrapper(' + o.name + '): ' + (ERR[h] || h) + ' ' + addon.pt_last_error(ctx));
+      this.effect = new Effect(ctx, typeof h === 'number' ? null : h);
+      this._observers = [];
+      this.onApplyObservable = { add: (f) => { this._observers.push(f); return f; }, clear: () => { this._observers = []; } };
+    }
+    dispose() { if (this.effect._pt) addon.pt_effect_destroy(this.effect._pt); this.effect._pt = null; }
+  }
+
+  class EffectRenderer {
+    constructor(engine) { this.engine = engine; }
+    // Babylon skips a non-ready effect silently; so does this
+    render(wrapper, target) {
+      if (!wrapper.effect.isReady()) return;
+      wrapper._observers.forEach((f) => f());
+      check(wrapper.effect._ctx, addon.pt_render(wrapper.effect._pt, target ? target._pt : null), 'render ' + wrapper.name);
+    }
+    dispose() {}
+  }
+
+  set('Engine', Engine);
+  set('RenderTargetTexture', RenderTargetTexture);
+  set('RawTexture', RawTexture);
+  set('Texture', Texture);
+  set('EffectWrapper', EffectWrapper);
+  set('EffectRenderer', EffectRenderer);
+  return { addon, Engine, decodePNG };
+}
+
+module.exports = { install, decodePNG, loadAddon };

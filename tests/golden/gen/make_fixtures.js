@@ -15,7 +15,6 @@
 const fs = require('fs');
 const path = require('path');
 const vm = require('vm');
-const Module = require('module');
 
 const REF = process.env.PT_REFERENCE || '/root/reference';
 const [scene, outdir, W_, H_, F_, SEED_, MODEL_] = process.argv.slice(2);
@@ -25,86 +24,7 @@ const SEED = BigInt(SEED_ || '1');
 const MODEL = MODEL_ || 'Stanford Bunny';
 fs.mkdirSync(outdir, { recursive: true });
 
-// ---------------------------------------------------------------- deterministic Math.random
-// splitmix64 -> top 24 bits / 2^24 (exactly representable in fp32, so the uniform is lossless)
-let smState = SEED;
-function splitmix64() {
-  smState = (smState + 0x9E3779B97F4A7C15n) & 0xFFFFFFFFFFFFFFFFn;
-  let z = smState;
-  z = ((z ^ (z >> 30n)) * 0xBF58476D1CE4E5B9n) & 0xFFFFFFFFFFFFFFFFn;
-  z = ((z ^ (z >> 27n)) * 0x94D049BB133111EBn) & 0xFFFFFFFFFFFFFFFFn;
-  return z ^ (z >> 31n);
-}
-Math.random = () => Number(splitmix64() >> 40n) / 16777216;
-
-// ---------------------------------------------------------------- browser-ish globals
-global.window = global; global.self = global;
-global.navigator = { userAgent: 'node', maxTouchPoints: 0 };
-global.atob = (s) => Buffer.from(s, 'base64').toString('binary');
-global.btoa = (s) => Buffer.from(s, 'binary').toString('base64');
-function fakeElement() {
-  return { style: {}, innerHTML: '', addEventListener() {}, removeEventListener() {}, appendChild() {},
-           getBoundingClientRect() { return { left: 0, top: 0, width: W, height: H }; },
-           focus() {}, setAttribute() {}, getContext() { return null; }, width: W, height: H };
-}
-global.document = { getElementById: () => fakeElement(), addEventListener() {}, removeEventListener() {},
-                    createElement: () => fakeElement(), body: fakeElement() };
-global.addEventListener = () => {};
-global.removeEventListener = () => {};
-global.Stats = function () { this.domElement = fakeElement(); this.update = () => {}; };
-function Controller(obj, prop) { this.object = obj; this.property = prop; this.__onChange = null; }
-Controller.prototype.onChange = function (f) { this.__onChange = f; return this; };
-Controller.prototype.onFinishChange = function () { return this; };
-Controller.prototype.getValue = function () { return this.object[this.property]; };
-Controller.prototype.setValue = function (v) { this.object[this.property] = v; if (this.__onChange) this.__onChange.call(this, v); return this; };
-Controller.prototype.name = function () { return this; };
-Controller.prototype.step = function () { return this; };
-function GUI() {}
-GUI.prototype.add = function (obj, prop) { return new Controller(obj, prop); };
-GUI.prototype.addColor = GUI.prototype.add;
-GUI.prototype.addFolder = function () { return new GUI(); };
-GUI.prototype.open = GUI.prototype.close = function () {};
-global.dat = { GUI };
-
-// local-file XMLHttpRequest (the glTF loader fetches through it)
-class LocalXHR {
-  constructor() { this.readyState = 0; this.status = 0; this._l = {}; this.responseType = ''; this.onreadystatechange = null; }
-  open(m, url) { this._url = url; this.readyState = 1; }
-  setRequestHeader() {} getResponseHeader() { return null; } getAllResponseHeaders() { return ''; } abort() {}
-  addEventListener(e, f) { (this._l[e] = this._l[e] || []).push(f); }
-  removeEventListener(e, f) { if (this._l[e]) this._l[e] = this._l[e].filter((g) => g !== f); }
-  send() {
-    const p = decodeURIComponent(this._url.replace(/^file:\/\//, '').split('?')[0]);
-    setImmediate(() => {
-      try {
-        const b = fs.readFileSync(p);
-        this.status = 200;
-        if (this.responseType === 'arraybuffer') this.response = b.buffer.slice(b.byteOffset, b.byteOffset + b.byteLength);
-        else { this.response = b.toString('utf8'); this.responseText = this.response; }
-      } catch (e) { this.status = 404; this.response = null; }
-      this.readyState = 4;
-      if (this.onreadystatechange) this.onreadystatechange();
-      for (const ev of ['readystatechange', 'load', 'loadend']) (this._l[ev] || []).forEach((f) => f.call(this));
-    });
-  }
-}
-global.XMLHttpRequest = LocalXHR;
-
-const origResolve = Module._resolveFilename;
-Module._resolveFilename = function (req, ...rest) {
-  if (req === 'babylonjs') return path.join(REF, 'js/babylon.js');
-  return origResolve.call(this, req, ...rest);
-};
-const REAL = require(path.join(REF, 'js/babylon.js'));
-// a writable facade over the module namespace (its exports are getter-only)
-const BABYLON = {};
-for (const k of Object.keys(REAL)) {
-  Object.defineProperty(BABYLON, k, { configurable: true, enumerable: true, get: () => REAL[k],
-    set: (v) => Object.defineProperty(BABYLON, k, { value: v, writable: true, configurable: true, enumerable: true }) });
-}
-global.BABYLON = BABYLON;
-require(path.join(REF, 'js/babylon.glTFFileLoader.min.js'));
-BABYLON.Logger.LogLevels = BABYLON.Logger.ErrorLogLevel;
+const { REAL, BABYLON } = require('./browser_env.js').setup(REF, W, H, SEED);
 
 // ---------------------------------------------------------------- recording boundary
 let renderLoop = null;

@@ -1,0 +1,31 @@
+"""The JavaScript host path on the GPU: recorded reference streams replayed through the Babylon
+effect-API shim (js/babylon_pt.js) and the N-API addon onto libpt.so, bit-exact vs the oracle."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not shutil.which("node"), reason="node not installed")]
+REPLAY = os.path.join(H.ROOT, "babylon.js-pathtracing-renderer_amd", "js", "replay_stream.js")
+
+
+@pytest.mark.parametrize("name", ["cornell_256", "gltf_teapot_320x180"])
+def test_node_replay_bitexact(tmp_path, name):
+    meta = H.stream(name)
+    H.bluenoise().tofile(tmp_path / "bluenoise.u8")
+    if meta["scene"] == "gltf":
+        for k, v in H.texture_payloads(meta, H.mesh(meta)).items():
+            v.tofile(tmp_path / (k + ".f32"))
+    out = str(tmp_path / "out")
+    subprocess.run(["node", REPLAY, os.path.join(H.GOLD, name + ".json"), str(tmp_path), out],
+                   check=True, timeout=300)
+    w, h = meta["width"], meta["height"]
+    acc = np.fromfile(out + ".acc.f32", np.float32).reshape(h, w, 4)
+    can = np.fromfile(out + ".canvas.u8", np.uint8).reshape(h, w, 4)
+    ref_acc, ref_can, _ = H.oracle_replay(meta, with_output=True)
+    assert np.array_equal(acc.view(np.uint32), ref_acc[-1].view(np.uint32))
+    assert np.array_equal(can, ref_can[-1])
