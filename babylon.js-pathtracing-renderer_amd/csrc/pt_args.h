@@ -75,6 +75,23 @@ struct TraceArgs {
     unsigned* err;                  // ErrBits
 };
 
+// wavefront buffers (pt_wavefront.hip): path state travels with the queue as 4 x 16-byte SoA
+// records, double-buffered between bounces; per-pixel outputs are indexed py * wq + px
+struct WfBufs {
+    float4* qA[2];          // ro.xyz, pixel index (bits)
+    float4* qB[2];          // rd.xyz, blueNoise counter
+    float4* qC[2];          // mask.xyz, metallicRoughness.g
+    float4* qD[2];          // seed.xy (bits), flags (bits), blue-noise bytes (bits)
+    float4* hit0;           // per slot of the current bounce: t, object id (bits), u, v
+    float4* hit1;           // hitNormal.xyz
+    unsigned* bvhq;         // slots whose ray enters the model's root box this bounce
+    float4* gb0;            // per pixel: objectNormal.xyz, objectID
+    float4* gb1;            // per pixel: objectColor.xyz, pixelSharpness
+    float4* rad;            // per pixel: CalculateRadiance() result
+    unsigned* cnt;          // [b] = live paths entering bounce b (0..6); [8 + b] = BVH queue of bounce b
+    int wq, hq;             // quad-rounded frame size
+};
+
 struct OutputArgs {
     int width, height;      // output (canvas or render target) size
     int acc_w, acc_h;       // accumulation texture size (texelFetch bounds)

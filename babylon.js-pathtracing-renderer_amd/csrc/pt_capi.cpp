@@ -27,6 +27,8 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
+hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x, int bands,
+                               int persist_blocks, hipStream_t s);
 }
 
 namespace {
@@ -72,6 +74,11 @@ struct pt_ctx {
     unsigned long long* d_counters = nullptr;
     bool counting = false;
     int num_parts = 1, part = 0;
+    int backend = PT_BACKEND_WAVEFRONT;
+    int cu_count = 256;
+    pt::WfBufs wf = {};
+    void* wf_mem = nullptr;
+    size_t wf_pixels = 0;
     hipEvent_t ev0[kProgSlots] = {}, ev1[kProgSlots] = {};
     bool ev_used[kProgSlots] = {};
     // timing window: per draw event pairs, reused across windows
@@ -241,6 +248,33 @@ int end_draw(pt_ctx* c, int prog)
     return PT_OK;
 }
 
+// (re)allocate the wavefront buffers for a wq x hq quad-rounded frame: one slab, carved
+int wf_reserve(pt_ctx* c, int wq, int hq)
+{
+    const size_t P = (size_t)wq * hq;
+    if (P <= c->wf_pixels && c->wf_mem) {
+        c->wf.wq = wq; c->wf.hq = hq;
+        return PT_OK;
+    }
+    if (c->wf_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->wf_mem)); c->wf_mem = nullptr; }
+    const size_t f4 = P * sizeof(float4);
+    const size_t bytes = 8 * f4 + 2 * f4 + 3 * f4 + P * sizeof(unsigned) + 256;
+    HIPCHK(c, hipMalloc(&c->wf_mem, bytes));
+    char* m = (char*)c->wf_mem;
+    auto take = [&](size_t n) { char* r = m; m += (n + 255) & ~(size_t)255; return r; };
+    c->wf.cnt = (unsigned*)take(256);
+    for (int k = 0; k < 2; k++) {
+        c->wf.qA[k] = (float4*)take(f4); c->wf.qB[k] = (float4*)take(f4);
+        c->wf.qC[k] = (float4*)take(f4); c->wf.qD[k] = (float4*)take(f4);
+    }
+    c->wf.hit0 = (float4*)take(f4); c->wf.hit1 = (float4*)take(f4);
+    c->wf.gb0 = (float4*)take(f4); c->wf.gb1 = (float4*)take(f4); c->wf.rad = (float4*)take(f4);
+    c->wf.bvhq = (unsigned*)take(P * sizeof(unsigned));
+    c->wf_pixels = P;
+    c->wf.wq = wq; c->wf.hq = hq;
+    return PT_OK;
+}
+
 int render_trace(pt_effect* fx, pt_texture* target)
 {
     pt_ctx* c = fx->ctx;
@@ -293,9 +327,22 @@ int render_trace(pt_effect* fx, pt_texture* target)
     a.err = c->d_err;
     int gx = (target->w + pt::kTile - 1) / pt::kTile;
     int gy = bands_owned(c, target->h);
+    if (c->backend == PT_BACKEND_WAVEFRONT) {
+        int rc = wf_reserve(c, gx * pt::kTile, ((target->h + pt::kTile - 1) / pt::kTile) * pt::kTile);
+        if (rc) return rc;
+        c->wf.wq = (target->w + 1) & ~1;   // quad-rounded frame: the pixels that are shaded
+        c->wf.hq = (target->h + 1) & ~1;
+    }
     int rc = begin_draw(c, fx->prog);
     if (rc) return rc;
-    if (gy > 0) HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, gy, c->stream));
+    if (gy > 0) {
+        if (c->backend == PT_BACKEND_WAVEFRONT) {
+            HIPCHK(c, hipMemsetAsync(c->wf.cnt, 0, 64, c->stream));
+            HIPCHK(c, pt_launch_wavefront(fx->prog, c->counting ? 1 : 0, &a, &c->wf, gx, gy, c->cu_count * 8, c->stream));
+        } else {
+            HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, gy, c->stream));
+        }
+    }
     return end_draw(c, fx->prog);
 }
 
@@ -410,6 +457,7 @@ pt_ctx* pt_ctx_create(int device, int* err)
     }
     auto* c = new pt_ctx();
     c->device = device;
+    c->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&c->d_err, 256);
@@ -439,6 +487,7 @@ void pt_ctx_destroy(pt_ctx* c)
         if (c->ev1[i]) hipEventDestroy(c->ev1[i]);
     }
     if (c->canvas) hipFree(c->canvas);
+    if (c->wf_mem) hipFree(c->wf_mem);
     if (c->d_err) hipFree(c->d_err);
     if (c->d_counters) hipFree(c->d_counters);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -639,6 +688,13 @@ int pt_write_pixels(pt_ctx* c, pt_texture* t, const void* src, size_t bytes)
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(t->d, src, bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_set_backend(pt_ctx* c, int backend)
+{
+    if (!c || (backend != PT_BACKEND_MEGAKERNEL && backend != PT_BACKEND_WAVEFRONT)) return PT_ERR_ARG;
+    c->backend = backend;
     return PT_OK;
 }
 

@@ -1,0 +1,200 @@
+// pt_device.h — device routines shared by the megakernel (pt_kernels.hip) and the wavefront
+// kernels (pt_wavefront.hip): the reference's random / sampling / material / intersection helpers
+// with the pinned GLSL semantics (pt_glsl.h). Each cites the GLSL it restates.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_args.h"
+#include "pt_glsl.h"
+
+namespace pt {
+using namespace ptg;
+
+constexpr float kINF = 1000000.0f;   // #define INFINITY 1000000.0 (js/PathTracingCommon.js:329)
+constexpr float kTwoPi = 6.28318530717958648f;
+
+enum { PROG_CORNELL = 3, PROG_GLTF = 4 };
+// PROG_GLTF_TEX: the glTF program instantiated with its PBR / normal-map code (models with an
+// albedo or bump texture); PROG_GLTF is the same program with those branches compiled out.
+enum { PROG_GLTF_TEX = 104 };
+template <int P> constexpr bool kIsGltf = P == PROG_GLTF || P == PROG_GLTF_TEX;
+template <int P> constexpr bool kHasTex = P == PROG_GLTF_TEX;
+// waves per SIMD the register allocator must leave room for (128 VGPRs -> 4; the textured
+// variant keeps 2 rather than spill)
+template <int P> constexpr int kMinWaves = kHasTex<P> ? 2 : 4;
+
+// ------------------------------------------------------------------------------ per-lane state
+struct Path {
+    uint32_t s0, s1;       // uvec2 seed (js/PathTracingCommon.js:500)
+    float counter;         // blueNoise_rand() counter
+    float bn0, bn1;        // randVec4.r / .g (channel = mod(counter, 2) only reaches r, g)
+    f3 ro, rd;             // rayOrigin, rayDirection
+};
+
+PT_D float rng(Path& p)
+{
+    p.s0 += 1u; p.s1 += 1u;
+    uint32_t qx = 1103515245u * ((p.s0 >> 1u) ^ p.s1);
+    uint32_t qy = 1103515245u * ((p.s1 >> 1u) ^ p.s0);
+    uint32_t n = 1103515245u * (qx ^ (qy >> 3u));
+    return (float)n * (1.0f / 4294967296.0f);
+}
+PT_D float blueNoise_rand(Path& p)
+{
+    p.counter = p.counter + 1.0f;
+    int channel = (int)gmod(p.counter, 2.0f);
+    return gfract(channel == 0 ? p.bn0 : p.bn1);
+}
+PT_D float tentFilter(float x) { return (x < 0.5f) ? sqrtf(2.0f * x) - 1.0f : 1.0f - sqrtf(2.0f - (2.0f * x)); }
+PT_D f3 onb_u(f3 nl)
+{
+    f3 a = (fabsf(nl.y) < 0.9f) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+    return normalize(cross(a, nl));
+}
+PT_D f3 cosWeightedDir(Path& p, f3 nl)
+{
+    float r = sqrtf(rng(p));
+    float phi = rng(p) * kTwoPi;
+    float sn, cs;
+    gsincos(phi, sn, cs);
+    float x = r * cs, y = r * sn;
+    float z = sqrtf(1.0f - x * x - y * y);
+    f3 U = onb_u(nl);
+    f3 V = cross(nl, U);
+    return normalize(U * x + V * y + nl * z);
+}
+PT_D f3 specularLobeDir(Path& p, f3 rdir, float roughness)
+{
+    roughness = gclamp(roughness, 0.0f, 1.0f);
+    float exponent = gmix(7.0f, 0.0f, sqrtf(roughness));
+    float cosTheta = gpow(rng(p), 1.0f / (gexp(exponent) + 1.0f));
+    float sinTheta = sqrtf(gmax(0.0f, 1.0f - cosTheta * cosTheta));
+    float phi = rng(p) * kTwoPi;
+    float sn, cs;
+    gsincos(phi, sn, cs);
+    f3 U = onb_u(rdir);
+    f3 V = cross(rdir, U);
+    f3 lobe = (U * cs) * sinTheta + (V * sn) * sinTheta + rdir * cosTheta;
+    return normalize(mix3(rdir, lobe, roughness));
+}
+PT_D float fresnel(f3 rdir, f3 n, float etai, float etat, float& ratioIoR)
+{
+    float temp = etai;
+    float cosi = gclamp(dot(rdir, n), -1.0f, 1.0f);
+    if (cosi > 0.0f) { etai = etat; etat = temp; }
+    ratioIoR = etai / etat;
+    float sint = ratioIoR * sqrtf(1.0f - (cosi * cosi));
+    if (sint >= 1.0f) return 1.0f;
+    float cost = sqrtf(1.0f - (sint * sint));
+    cosi = fabsf(cosi);
+    float Rs = ((etat * cosi) - (etai * cost)) / ((etat * cosi) + (etai * cost));
+    float Rp = ((etai * cosi) - (etat * cost)) / ((etai * cosi) + (etat * cost));
+    return gclamp(((Rs * Rs) + (Rp * Rp)) * 0.5f, 0.0f, 1.0f);
+}
+PT_D f3 sampleQuadLight(Path& p, const TraceArgs& a, f3 x, f3 nl, float& weight)
+{
+    const QuadArg& L = a.light;
+    f3 q;
+    q.x = gmix(L.v0.x, L.v2.x, gclamp(rng(p), 0.1f, 0.9f));
+    q.y = gmix(L.v0.y, L.v2.y, gclamp(rng(p), 0.1f, 0.9f));
+    q.z = gmix(L.v0.z, L.v2.z, gclamp(rng(p), 0.1f, 0.9f));
+    f3 d = q - x;
+    float d2 = dot(d, d);
+    float cos_a_max = sqrtf(1.0f - gclamp(a.light_r2 / d2, 0.0f, 1.0f));
+    d = normalize(d);
+    float dotNl = gmax(0.0f, dot(nl, d));
+    float w = 2.0f * (1.0f - cos_a_max) * gmax(0.0f, -dot(d, L.normal)) * dotNl;
+    weight = gclamp(w, 0.0f, 1.0f);
+    return d;
+}
+
+// ------------------------------------------------------------------------------ intersectors
+PT_D float unitSphere(f3 ro, f3 rd, f3& n)
+{
+    float a = dot(rd, rd);
+    float b = 2.0f * dot(rd, ro);
+    float c = dot(ro, ro) - 1.0f;
+    float invA = 1.0f / a;          // solveQuadratic, js/PathTracingCommon.js:631-641
+    b *= invA;
+    c *= invA;
+    float nh = -b * 0.5f;
+    float u2 = nh * nh - c;
+    float u;
+    if (u2 < 0.0f) { nh = 0.0f; u = 0.0f; } else u = sqrtf(u2);
+    float t0 = nh - u, t1 = nh + u;
+    float t = t0 > 0.0f ? t0 : t1 > 0.0f ? t1 : kINF;
+    if (t != kINF) { f3 h = ro + rd * t; n = mk(2.0f * h.x, 2.0f * h.y, 2.0f * h.z); }
+    return t;
+}
+// TriangleIntersect, single-sided (QuadIntersect passes isDoubleSided = false), edges precomputed
+PT_D float quadTriangle(const TriArg& T, f3 ro, f3 rd)
+{
+    f3 pv = cross(rd, T.e2);
+    float det = 1.0f / dot(T.e1, pv);
+    if (det < 0.0f) return kINF;
+    f3 tv = ro - T.v0;
+    float u = dot(tv, pv) * det;
+    f3 qv = cross(tv, T.e1);
+    float v = dot(rd, qv) * det;
+    float t = dot(T.e2, qv) * det;
+    return (u < 0.0f || u > 1.0f || v < 0.0f || u + v > 1.0f || t <= 0.0f) ? kINF : t;
+}
+PT_D float box(f3 mn, f3 mx, f3 ro, f3 inv)
+{
+    f3 nr = (mn - ro) * inv;
+    f3 fr = (mx - ro) * inv;
+    float t0 = gmax(gmax(gmin(nr.x, fr.x), gmin(nr.y, fr.y)), gmin(nr.z, fr.z));
+    float t1 = gmin(gmin(gmax(nr.x, fr.x), gmax(nr.y, fr.y)), gmax(nr.z, fr.z));
+    return gmax(t0, 0.0f) > t1 ? kINF : t0;
+}
+PT_D float bvhTriangle(f3 v0, f3 v1, f3 v2, f3 ro, f3 rd, float& u, float& v, bool dbl)
+{
+    f3 e1 = v1 - v0, e2 = v2 - v0;
+    f3 pv = cross(rd, e2);
+    float det = 1.0f / dot(e1, pv);
+    f3 tv = ro - v0;
+    u = dot(tv, pv) * det;
+    f3 qv = cross(tv, e1);
+    v = dot(rd, qv) * det;
+    float t = dot(e2, qv) * det;
+    bool miss = u < 0.0f || u > 1.0f || v < 0.0f || u + v > 1.0f || t <= 0.0f;
+    if (!dbl) miss = miss || det < 0.0f;
+    return miss ? kINF : t;
+}
+
+// texelFetch on a RGBA32F data texture by linear texel index (== ivec2(mod(i,2048), i/2048) for
+// the reference's 2048-wide textures); outside the texture -> 0 (pinned)
+PT_D float4 fetch32(const float4* base, long long n, float idx)
+{
+    if (!(idx >= 0.0f) || !(idx < (float)n)) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    return base[(unsigned)idx];   // data textures hold < 2^31 texels (checked at upload)
+}
+PT_D float unorm8(unsigned b) { return (float)b / 255.0f; }
+// REPEAT wrap of an integer-valued texel coordinate: fmod is exact, so any finite coordinate wraps
+// exactly; NaN/inf (degenerate uv) wrap to texel 0 (pinned, as the oracle)
+PT_D int wrapTexel(float f, int n)
+{
+    float r = fmodf(f, (float)n);
+    if (!(r == r)) r = 0.0f;
+    int i = (int)r;
+    return i < 0 ? i + n : i;
+}
+PT_D void texBilinear(const Tex8& t, float u, float v, float out[4])
+{
+    if (!t.p || t.w <= 0 || t.h <= 0) { out[0] = out[1] = out[2] = out[3] = 0.0f; return; }
+    float x = u * (float)t.w - 0.5f, y = v * (float)t.h - 0.5f;
+    float fx = floorf(x), fy = floorf(y);
+    float ax = x - fx, by = y - fy;
+    int x0 = wrapTexel(fx, t.w), y0 = wrapTexel(fy, t.h);
+    int x1 = x0 + 1 == t.w ? 0 : x0 + 1, y1 = y0 + 1 == t.h ? 0 : y0 + 1;
+    uchar4 t00 = t.p[y0 * t.w + x0], t10 = t.p[y0 * t.w + x1], t01 = t.p[y1 * t.w + x0], t11 = t.p[y1 * t.w + x1];
+    out[0] = gmix(gmix(unorm8(t00.x), unorm8(t10.x), ax), gmix(unorm8(t01.x), unorm8(t11.x), ax), by);
+    out[1] = gmix(gmix(unorm8(t00.y), unorm8(t10.y), ax), gmix(unorm8(t01.y), unorm8(t11.y), ax), by);
+    out[2] = gmix(gmix(unorm8(t00.z), unorm8(t10.z), ax), gmix(unorm8(t01.z), unorm8(t11.z), ax), by);
+    out[3] = gmix(gmix(unorm8(t00.w), unorm8(t10.w), ax), gmix(unorm8(t01.w), unorm8(t11.w), ax), by);
+}
+
+PT_D f3 pow22(f3 c) { return mk(gpow(c.x, 2.2f), gpow(c.y, 2.2f), gpow(c.z, 2.2f)); }
+
+} // namespace pt

@@ -1,0 +1,552 @@
+// pt_wavefront.hip — the wavefront form of the path-tracing program (the default backend).
+//
+// The GLSL runs one fragment = one whole path (<= 6 segments); on a 64-lane wave that leaves most
+// lanes idle: paths end at different bounces, branch into different materials, and a few lanes
+// descend the BVH while the rest wait (megakernel PMC: ~28% VALU lane utilisation). Here the path
+// is cut at its segment boundaries and every segment stage runs as its own kernel over a compacted
+// queue of live paths:
+//
+//   wf_raygen            main() up to SetupScene (js/PathTracingCommon.js:1259-1292): camera ray,
+//                        seeds, blue-noise texel; every pixel of the owned bands -> queue 0
+//   per bounce b = 0..5:
+//     wf_extend   <P>    SceneIntersect's analytic part (2 spheres, 6 quads) + the BVH root-box test;
+//                        rays that enter the model's root box are appended to the BVH queue
+//     wf_bvh      <P>    the BVH walk (js/GLTFModelPathTracing_FragmentShader.js:201-344) only for
+//                        those rays: every lane of a wave traverses
+//     wf_shade    <P>    one iteration of CalculateRadiance's loop body; surviving paths are appended
+//                        to queue b+1 (wave ballot + prefix + one atomic per wave)
+//   wf_finish            main() after CalculateRadiance: 2x2-quad derivatives + accumulation
+//
+// Path state travels with the queue as four 16-byte SoA records (coalesced dwordx4 loads/stores);
+// per-pixel outputs (G-buffer for the derivatives, radiance) are pixel-indexed. Every path performs
+// exactly the GLSL's sequence of IEEE ops and random draws, only the schedule differs, so the
+// result is bit-identical to the oracle and to the megakernel (tests/test_gpu_parity.py).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_args.h"
+#include "pt_device.h"
+#include "pt_glsl.h"
+
+namespace pt {
+
+enum Flag : unsigned {
+    F_DIFFUSE_MASK = 7u,     // diffuseCount (0..6)
+    F_COAT = 1u << 3,        // coatTypeIntersected
+    F_SPECULAR = 1u << 4,    // bounceIsSpecular
+    F_SAMPLE_LIGHT = 1u << 5,
+    F_PREV_METAL = 1u << 6,  // previousIntersecType == METAL (after the PBR remap)
+};
+
+// hit record of the current bounce, per queue slot
+struct HitRec {
+    float t;
+    int id;          // 0,1 spheres; 2..7 quads; 8 model; -1 none
+    float u, v;      // model hit uv
+    f3 n;            // hitNormal as SceneIntersect returns it
+};
+
+PT_D float u2f(unsigned u) { return __uint_as_float(u); }
+PT_D unsigned f2u(float f) { return __float_as_uint(f); }
+
+// wave-level stream compaction: returns this lane's slot in `queue` (valid only when `alive`)
+PT_D unsigned wave_append(unsigned* counter, bool alive)
+{
+    const unsigned long long m = __ballot(alive);
+    const unsigned total = (unsigned)__popcll(m);
+    unsigned base = 0;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    if (total && lane == leader) base = atomicAdd(counter, total);
+    base = __shfl(base, leader < 0 ? 0 : leader, 64);
+    const unsigned long long below = m & ((1ull << lane) - 1ull);
+    return base + (unsigned)__popcll(below);
+}
+
+template <bool COUNT>
+PT_D void count_add(const TraceArgs& a, int which, unsigned v)
+{
+    if (COUNT && v) atomicAdd(&a.counters[which], (unsigned long long)v);
+}
+
+// ============================================================================ raygen
+template <bool COUNT>
+__global__ __launch_bounds__(kBlock) void wf_raygen(TraceArgs a, WfBufs w)
+{
+    const unsigned tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int lx = (lane & 1) | ((lane >> 1) & 6);
+    const int ly = ((lane >> 1) & 1) | ((lane >> 3) & 6);
+    const int band = blockIdx.y * a.num_parts + a.part;
+    const int px = blockIdx.x * kTile + (wave & 1) * 8 + lx;
+    const int py = band * kTile + (wave >> 1) * 8 + ly;
+    const bool active = px < w.wq && py < w.hq;
+    Path p;
+    p.s0 = p.s1 = 0;
+    p.ro = p.rd = mk(0, 0, 0);
+    unsigned bnb = 0, pix = 0;
+    if (active) {
+        pix = (unsigned)py * (unsigned)w.wq + (unsigned)px;
+        const float* m = a.cam.m;
+        f3 camRight = mk(m[0], m[1], m[2]), camUp = mk(m[4], m[5], m[6]), camFwd = mk(m[8], m[9], m[10]);
+        f3 camPos = mk(m[12], m[13], m[14]);
+        float fcx = (float)px + 0.5f, fcy = (float)py + 0.5f;
+        p.s0 = (uint32_t)a.frame * (uint32_t)fcx;
+        p.s1 = (uint32_t)(a.frame + 1.0f) * (uint32_t)fcy;
+        int bx = (int)gmod(fcx + floorf(a.rnd[0] * 256.0f), 256.0f);
+        int by = (int)gmod(fcy + floorf(a.rnd[1] * 256.0f), 256.0f);
+        if (bx < a.bluenoise.w && by < a.bluenoise.h) {
+            uchar4 b = a.bluenoise.p[by * a.bluenoise.w + bx];
+            bnb = (unsigned)b.x | ((unsigned)b.y << 8);
+        }
+        float ox = tentFilter(rng(p));
+        float oy = tentFilter(rng(p));
+        float ppx = ((fcx + ox) / a.res[0]) * 2.0f - 1.0f;
+        float ppy = ((fcy + oy) / a.res[1]) * 2.0f - 1.0f;
+        f3 rayDir = normalize((camRight * ppx) * a.ulen + (camUp * ppy) * a.vlen + camFwd);
+        f3 focal = rayDir * a.focus;
+        float ang = rng(p) * kTwoPi;
+        float rad = rng(p) * a.aperture;
+        float sn, cs;
+        gsincos(ang, sn, cs);
+        f3 apert = (camRight * cs + camUp * sn) * sqrtf(rad);
+        p.rd = normalize(focal - apert);
+        p.ro = camPos + apert;
+        // per-pixel outputs start at the `out` parameters' pinned zero
+        w.gb0[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        w.gb1[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        w.rad[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    const unsigned slot = wave_append(&w.cnt[0], active);
+    if (active) {
+        w.qA[0][slot] = make_float4(p.ro.x, p.ro.y, p.ro.z, u2f(pix));
+        w.qB[0][slot] = make_float4(p.rd.x, p.rd.y, p.rd.z, -1.0f);   // blueNoise counter starts at -1
+        w.qC[0][slot] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);           // mask, roughness
+        w.qD[0][slot] = make_float4(u2f(p.s0), u2f(p.s1), u2f(F_SPECULAR), u2f(bnb));
+    }
+    if (COUNT && active) { count_add<true>(a, C_PATHS, 1); count_add<true>(a, C_RGBA8, 1); }
+}
+
+// ============================================================================ extend (analytic part)
+template <int PROG, bool COUNT>
+__global__ __launch_bounds__(kBlock) void wf_extend(TraceArgs a, WfBufs w, int b)
+{
+    const unsigned n = w.cnt[b];
+    const unsigned stride = gridDim.x * kBlock;
+    const int q = b & 1;
+    for (unsigned base = blockIdx.x * kBlock; base < n; base += stride) {
+        const unsigned i = base + threadIdx.x;
+        const bool live = i < n;
+        bool toBvh = false;
+        if (live) {
+            float4 A = w.qA[q][i], B = w.qB[q][i];
+            f3 ro = mk(A.x, A.y, A.z), rd = mk(B.x, B.y, B.z);
+            float t = kINF;
+            int id = -1;
+            f3 sn = mk(0, 0, 0);
+#pragma unroll 1
+            for (int s = 0; s < 2; s++) {
+                const SphereArg& S = a.sph[s];
+                f3 nn;
+                float d = unitSphere(mul(S.inv, ro, 1.0f), mul(S.inv, rd, 0.0f), nn);
+                if (d < t) { t = d; id = s; sn = nn; }
+            }
+#pragma unroll 1
+            for (int k = 0; k < 6; k++) {
+                float d = gmin(quadTriangle(a.qtri[2 * k], ro, rd), quadTriangle(a.qtri[2 * k + 1], ro, rd));
+                if (d < t) { t = d; id = 2 + k; }
+            }
+            f3 hn = mk(0, 0, 0);
+            if (id >= 0 && id < 2) hn = normalize(mul3t(a.sph[id].inv, normalize(sn)));
+            else if (id >= 2) hn = normalize(a.qnormal[id - 2]);
+            if (COUNT) count_add<true>(a, C_SEGMENTS, 1);
+            if (kIsGltf<PROG>) {
+                f3 O = mul(a.model, ro, 1.0f), D = mul(a.model, rd, 0.0f);
+                f3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+                float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
+                if (COUNT) count_add<true>(a, C_NODE, 1);
+                float tRoot = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
+                toBvh = tRoot < t;
+            }
+            w.hit0[i] = make_float4(t, u2f((unsigned)id), 0.0f, 0.0f);
+            w.hit1[i] = make_float4(hn.x, hn.y, hn.z, 0.0f);
+        }
+        if (kIsGltf<PROG>) {
+            const unsigned slot = wave_append(&w.cnt[8 + b], toBvh);
+            if (toBvh) w.bvhq[slot] = i;
+        }
+    }
+}
+
+// ============================================================================ BVH walk
+template <int PROG, bool COUNT>
+__global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b)
+{
+    __shared__ float2 lds[kStackLds * kBlock];
+    const unsigned n = w.cnt[8 + b];
+    const unsigned stride = gridDim.x * kBlock;
+    const int q = b & 1;
+    const unsigned tid = threadIdx.x;
+    float2 deep[kStackLevels - kStackLds];
+    for (unsigned base = blockIdx.x * kBlock; base < n; base += stride) {
+        const unsigned j = base + tid;
+        if (j >= n) continue;
+        const unsigned i = w.bvhq[j];
+        float4 A = w.qA[q][i], B = w.qB[q][i];
+        float hitT = w.hit0[i].x;
+        f3 ro = mk(A.x, A.y, A.z), rd = mk(B.x, B.y, B.z);
+        f3 O = mul(a.model, ro, 1.0f), D = mul(a.model, rd, 0.0f);
+        f3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+        const bool dbl = (!a.uses_albedo && a.model_mat == TRANSPARENT);
+        unsigned nodes = 0, leaves = 0, ovf = 0;
+        // the root was fetched and tested by wf_extend (and counted there); its box is hit
+        float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
+        float curId = 0.0f;
+        float curT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
+        lds[tid] = make_float2(curId, curT);
+        float stackptr = 0.0f;
+        bool skip = curT < hitT;
+        float triID = 0.0f, triU = 0.0f, triV = 0.0f;
+        bool lookup = false;
+        for (;;) {
+            if (!skip) {
+                stackptr = stackptr - 1.0f;
+                if (stackptr < 0.0f) break;
+                int si = (int)stackptr;
+                float2 e = si < kStackLds ? lds[si * kBlock + tid] : deep[si - kStackLds];
+                curId = e.x; curT = e.y;
+                if (curT >= hitT) continue;
+                c0 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f);
+                c1 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f + 1.0f);
+                nodes++;
+            }
+            skip = false;
+            if (c0.x < 0.0f) {
+                float idA = curId + 1.0f, idB = c1.x;
+                float4 a0 = fetch32(a.aabb, a.aabb_texels, idA * 2.0f), a1 = fetch32(a.aabb, a.aabb_texels, idA * 2.0f + 1.0f);
+                float4 b0 = fetch32(a.aabb, a.aabb_texels, idB * 2.0f), b1 = fetch32(a.aabb, a.aabb_texels, idB * 2.0f + 1.0f);
+                nodes += 2;
+                float tA = box(mk(a0.y, a0.z, a0.w), mk(a1.y, a1.z, a1.w), O, inv);
+                float tB = box(mk(b0.y, b0.z, b0.w), mk(b1.y, b1.z, b1.w), O, inv);
+                if (tB < tA) {
+                    float ti = idB; idB = idA; idA = ti;
+                    float tt = tB; tB = tA; tA = tt;
+                    float4 x0 = b0; b0 = a0; a0 = x0;
+                    float4 x1 = b1; b1 = a1; a1 = x1;
+                }
+                if (tB < hitT) { curId = idB; curT = tB; c0 = b0; c1 = b1; skip = true; }
+                if (tA < hitT) {
+                    if (skip) {
+                        int si = (int)stackptr;
+                        if (si < kStackLds) lds[si * kBlock + tid] = make_float2(idB, tB);
+                        else if (si < kStackLevels) deep[si - kStackLds] = make_float2(idB, tB);
+                        else { ovf++; atomicOr(a.err, (unsigned)E_STACK); }
+                        stackptr = stackptr + 1.0f;
+                    }
+                    curId = idA; curT = tA; c0 = a0; c1 = a1; skip = true;
+                }
+                continue;
+            }
+            float id = 8.0f * c0.x;
+            float4 t0 = fetch32(a.tri, a.tri_texels, id), t1 = fetch32(a.tri, a.tri_texels, id + 1.0f),
+                   t2 = fetch32(a.tri, a.tri_texels, id + 2.0f);
+            leaves++;
+            float tu, tv;
+            float d = bvhTriangle(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
+            if (d < hitT) { hitT = d; triID = id; triU = tu; triV = tv; lookup = true; }
+        }
+        unsigned taps = 0;
+        if (lookup) {
+            float4 v2 = fetch32(a.tri, a.tri_texels, triID + 2.0f), v3 = fetch32(a.tri, a.tri_texels, triID + 3.0f),
+                   v4 = fetch32(a.tri, a.tri_texels, triID + 4.0f), v5 = fetch32(a.tri, a.tri_texels, triID + 5.0f);
+            float triW = 1.0f - triU - triV;
+            f3 nn = normalize(mk(v2.y, v2.z, v2.w) * triW + mk(v3.x, v3.y, v3.z) * triU + mk(v3.w, v4.x, v4.y) * triV);
+            float hu = triW * v4.z + triU * v5.x + triV * v5.z;
+            float hv = triW * v4.w + triU * v5.y + triV * v5.w;
+            if (kHasTex<PROG> && a.uses_bump) {   // perturbNormal (js/GLTFModelPathTracing_FragmentShader.js:72-92)
+                f3 S = onb_u(nn);
+                f3 T = cross(nn, S);
+                f3 N = normalize(nn);
+                if (dot(cross(S, T), N) < 0.0f) { S = S * -1.0f; T = T * -1.0f; }
+                float tx[4];
+                texBilinear(a.bump, hu, hv, tx);
+                taps += 4;
+                f3 mN = normalize(mk(tx[0] * 2.0f - 1.0f, tx[1] * 2.0f - 1.0f, tx[2] * 2.0f - 1.0f));
+                mN.x *= 1.0f; mN.y *= 1.0f;
+                nn = normalize(S * mN.x + T * mN.y + N * mN.z);
+            }
+            f3 hn = normalize(mul3t(a.model, nn));
+            w.hit0[i] = make_float4(hitT, u2f(8u), hu, hv);
+            w.hit1[i] = make_float4(hn.x, hn.y, hn.z, 0.0f);
+        }
+        if (COUNT) {
+            count_add<true>(a, C_NODE, nodes);
+            count_add<true>(a, C_LEAF, leaves);
+            count_add<true>(a, C_HIT, lookup ? 1u : 0u);
+            count_add<true>(a, C_RGBA8, taps);
+            count_add<true>(a, C_OVERFLOW, ovf);
+        }
+    }
+}
+
+// ============================================================================ shade (one loop iteration)
+template <int PROG, bool COUNT>
+__global__ __launch_bounds__(kBlock) void wf_shade(TraceArgs a, WfBufs w, int b)
+{
+    constexpr bool gltf = kIsGltf<PROG>;
+    const unsigned n = w.cnt[b];
+    const unsigned stride = gridDim.x * kBlock;
+    const int q = b & 1, q2 = q ^ 1;
+    for (unsigned base = blockIdx.x * kBlock; base < n; base += stride) {
+        const unsigned i = base + threadIdx.x;
+        bool alive = false;
+        float4 oA, oB, oC, oD;
+        if (i < n) {
+            const float4 A = w.qA[q][i], B = w.qB[q][i], C = w.qC[q][i], D = w.qD[q][i];
+            const float4 H0 = w.hit0[i], H1 = w.hit1[i];
+            const unsigned pix = f2u(A.w);
+            Path p;
+            p.ro = mk(A.x, A.y, A.z);
+            p.rd = mk(B.x, B.y, B.z);
+            p.counter = B.w;
+            p.s0 = f2u(D.x); p.s1 = f2u(D.y);
+            unsigned flags = f2u(D.z);
+            const unsigned bnb = f2u(D.w);
+            p.bn0 = unorm8(bnb & 255u); p.bn1 = unorm8((bnb >> 8) & 255u);
+            f3 mask = mk(C.x, C.y, C.z);
+            float roughness = C.w;
+            int diffuseCount = (int)(flags & F_DIFFUSE_MASK);
+            bool coat = flags & F_COAT, specular = flags & F_SPECULAR, sampleLight = flags & F_SAMPLE_LIGHT;
+            const bool prevMetal = flags & F_PREV_METAL;
+            unsigned taps = 0;
+
+            const float t = H0.x;
+            const int id = (int)f2u(H0.y);
+            f3 color = mk(1.0f, 1.0f, 1.0f);
+            int hitType = -100;
+            if (id >= 0 && id < 2) { color = a.sph[id].color; hitType = a.sph[id].type; }
+            else if (id >= 2 && id < 8) { color = a.qcolor[id - 2]; hitType = a.qtype[id - 2]; }
+            else if (id == 8) hitType = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
+
+            // js/GLTFModelPathTracing_FragmentShader.js:391-602 (one iteration, `bounces` = b)
+            do {
+                if (t == kINF) break;
+                f3 nrm = normalize(mk(H1.x, H1.y, H1.z));
+                f3 nl = dot(nrm, p.rd) < 0.0f ? normalize(nrm) : normalize(-nrm);
+                f3 x = p.ro + p.rd * t;
+                if (b == 0) {
+                    w.gb0[pix] = make_float4(nl.x, nl.y, nl.z, (float)id);
+                    float4 g1 = w.gb1[pix];
+                    w.gb1[pix] = make_float4(color.x, color.y, color.z, g1.w);
+                }
+                if (b == 1 && prevMetal) w.gb0[pix] = make_float4(nl.x, nl.y, nl.z, (float)id);
+                if (hitType == LIGHT) {
+                    if (diffuseCount == 0) w.gb1[pix].w = 1.01f;
+                    if (specular || sampleLight) {
+                        f3 acc = max3s(mask * color, 0.0f);
+                        w.rad[pix] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+                    }
+                    break;
+                }
+                if (sampleLight) break;
+
+                if (kHasTex<PROG> && hitType == PBR_MATERIAL) {
+                    float tx[4];
+                    texBilinear(a.albedo, H0.z, H0.w, tx);
+                    taps += 4;
+                    color = pow22(mk(tx[0], tx[1], tx[2]));
+                    f3 emission = mk(0, 0, 0);
+                    if (a.uses_emissive) { texBilinear(a.emissive, H0.z, H0.w, tx); taps += 4; emission = mk(tx[0], tx[1], tx[2]); }
+                    emission = pow22(emission);
+                    float maxE = gmax(emission.x, gmax(emission.y, emission.z));
+                    if (specular && maxE > 0.01f) {
+                        w.gb1[pix].w = 1.01f;
+                        f3 acc = max3s(mask * emission, 0.0f);
+                        w.rad[pix] = make_float4(acc.x, acc.y, acc.z, 0.0f);
+                        break;
+                    }
+                    hitType = DIFFUSE;
+                    f3 mr = mk(0, 0, 0);
+                    if (a.uses_metal) { texBilinear(a.metal, H0.z, H0.w, tx); taps += 4; mr = mk(tx[0], tx[1], tx[2]); }
+                    mr = pow22(mr);
+                    roughness = mr.y;
+                    if (mr.y > 0.01f) hitType = CLEARCOAT_DIFFUSE;
+                    if (mr.z > 0.01f) hitType = METAL;
+                }
+
+                bool diffuseTail = hitType == DIFFUSE;
+                bool next = false;
+                if (hitType == TRANSPARENT || hitType == CLEARCOAT_DIFFUSE) {
+                    const bool glass = hitType == TRANSPARENT;
+                    float sharp;
+                    if (glass) {
+                        if (diffuseCount == 0 && !coat && !a.moving) sharp = 1.01f;
+                        else if (diffuseCount > 0) sharp = 0.0f;
+                        else sharp = -1.0f;
+                    } else {
+                        coat = true;
+                        sharp = 0.0f;
+                    }
+                    float ratio;
+                    float Re = fresnel(p.rd, glass ? nrm : nl, 1.0f, glass ? 1.5f : 1.4f, ratio);
+                    float Tr = 1.0f - Re;
+                    float P = 0.25f + (0.5f * Re);
+                    float RP = Re / P, TP = Tr / (1.0f - P);
+                    if (blueNoise_rand(p) < P) {
+                        if (!glass && diffuseCount == 0) sharp = a.frame > 500.0f ? 1.01f : -1.0f;
+                        w.gb1[pix].w = sharp;
+                        mask = mask * RP;
+                        p.rd = reflect(p.rd, nl);
+                        p.ro = x + nl * a.eps;
+                        next = true;
+                    } else {
+                        w.gb1[pix].w = sharp;
+                        if (glass) {
+                            if (distance(nrm, nl) > 0.1f) {
+                                const float thickness = 0.01f;
+                                f3 cc = clamp3(color, 0.01f, 0.99f);
+                                mask = mask * mk(gexp(glog(cc.x) * thickness * t), gexp(glog(cc.y) * thickness * t),
+                                                 gexp(glog(cc.z) * thickness * t));
+                            }
+                            mask = mask * TP;
+                            p.rd = refract(p.rd, nl, ratio);
+                            p.ro = x - nl * a.eps;
+                            if (diffuseCount == 1) specular = true;
+                            next = true;
+                        } else {
+                            mask = mask * TP;
+                            diffuseTail = true;
+                        }
+                    }
+                }
+                if (!next && diffuseTail) {
+                    diffuseCount++;
+                    mask = mask * color;
+                    specular = false;
+                    if (diffuseCount == 1 && blueNoise_rand(p) < 0.5f) {
+                        p.rd = cosWeightedDir(p, nl);
+                    } else {
+                        float wgt;
+                        f3 dl = sampleQuadLight(p, a, x, nl, wgt);
+                        mask = mask * wgt;
+                        p.rd = dl;
+                        if (hitType == DIFFUSE || b < 3) sampleLight = true;
+                    }
+                    p.ro = x + nl * a.eps;
+                    next = true;
+                } else if (!next && hitType == METAL) {
+                    mask = mask * color;
+                    if (gltf) p.rd = specularLobeDir(p, reflect(p.rd, nl), roughness);
+                    else p.rd = reflect(p.rd, nl);
+                    p.ro = x + nl * a.eps;
+                    next = true;
+                }
+                // any other hitType: the GLSL loop continues with the ray unchanged
+                alive = b + 1 < 6;
+                (void)next;
+                const unsigned nf = (unsigned)diffuseCount | (coat ? F_COAT : 0u) | (specular ? F_SPECULAR : 0u) |
+                                    (sampleLight ? F_SAMPLE_LIGHT : 0u) | (hitType == METAL ? F_PREV_METAL : 0u);
+                oA = make_float4(p.ro.x, p.ro.y, p.ro.z, A.w);
+                oB = make_float4(p.rd.x, p.rd.y, p.rd.z, p.counter);
+                oC = make_float4(mask.x, mask.y, mask.z, roughness);
+                oD = make_float4(u2f(p.s0), u2f(p.s1), u2f(nf), D.w);
+            } while (false);
+            if (COUNT) count_add<true>(a, C_RGBA8, taps);
+        }
+        const unsigned slot = wave_append(&w.cnt[b + 1], alive);
+        if (alive) {
+            w.qA[q2][slot] = oA;
+            w.qB[q2][slot] = oB;
+            w.qC[q2][slot] = oC;
+            w.qD[q2][slot] = oD;
+        }
+    }
+}
+
+// ============================================================================ finish
+__global__ __launch_bounds__(kBlock) void wf_finish(TraceArgs a, WfBufs w)
+{
+    const unsigned tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int lx = (lane & 1) | ((lane >> 1) & 6);
+    const int ly = ((lane >> 1) & 1) | ((lane >> 3) & 6);
+    const int band = blockIdx.y * a.num_parts + a.part;
+    const int px = blockIdx.x * kTile + (wave & 1) * 8 + lx;
+    const int py = band * kTile + (wave >> 1) * 8 + ly;
+    const bool active = px < w.wq && py < w.hq;
+    float4 g0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), g1 = g0, r = g0;
+    if (active) {
+        const unsigned pix = (unsigned)py * (unsigned)w.wq + (unsigned)px;
+        g0 = w.gb0[pix]; g1 = w.gb1[pix]; r = w.rad[pix];
+    }
+    const bool xodd = lane & 1, yodd = lane & 2;
+    auto ddx = [&](float v) { float o = __shfl_xor(v, 1, 64); return xodd ? v - o : o - v; };
+    auto ddy = [&](float v) { float o = __shfl_xor(v, 2, 64); return yodd ? v - o : o - v; };
+    float dNx = fabsf(ddx(g0.x)) + fabsf(ddy(g0.x));
+    float dNy = fabsf(ddx(g0.y)) + fabsf(ddy(g0.y));
+    float dNz = fabsf(ddx(g0.z)) + fabsf(ddy(g0.z));
+    float normalDiff = gsmoothstep(0.2f, 0.6f, dNx) + gsmoothstep(0.2f, 0.6f, dNy) + gsmoothstep(0.2f, 0.6f, dNz);
+    float dObj = fabsf(ddx(g0.w)) > 0.0f ? 1.0f : 0.0f;
+    dObj += fabsf(ddy(g0.w)) > 0.0f ? 1.0f : 0.0f;
+    float objectDiff = gsmoothstep(0.0f, 0.5f, dObj);
+    f3 dcx = mk(ddx(g1.x), ddx(g1.y), ddx(g1.z));
+    f3 dcy = mk(ddy(g1.x), ddy(g1.y), ddy(g1.z));
+    float dCol = length(dcx) > 0.0f ? 1.0f : 0.0f;
+    dCol += length(dcy) > 0.0f ? 1.0f : 0.0f;
+    float colorDiff = gsmoothstep(0.0f, 0.5f, dCol);
+    if (px >= a.width || py >= a.height) return;
+    const long long pi = (long long)py * a.width + px;
+    float4 prev = a.prev[pi];
+    float cr = r.x, cg = r.y, cb = r.z, ca;
+    if (a.frame == 1.0f) prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    else if (a.moving) {
+        prev.x *= 0.5f; prev.y *= 0.5f; prev.z *= 0.5f;
+        cr *= 0.5f; cg *= 0.5f; cb *= 0.5f;
+        prev.w = 0.0f;
+    }
+    ca = 0.0f;
+    float sharp = g1.w;
+    if (colorDiff >= 1.0f || normalDiff >= 1.0f || objectDiff >= 1.0f) sharp = 1.01f;
+    if (sharp == 1.01f) ca = 1.01f;
+    if (sharp == -1.0f) ca = -1.0f;
+    if (prev.w == 1.01f) ca = 1.01f;
+    if (prev.w == -1.0f) ca = 0.0f;
+    a.out[pi] = make_float4(prev.x + cr, prev.y + cg, prev.z + cb, ca);
+}
+
+} // namespace pt
+
+// ------------------------------------------------------------------------------ launcher
+extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w,
+                                          int tiles_x, int bands, int persist_blocks, hipStream_t s)
+{
+    using namespace pt;
+    if (prog == PROG_GLTF && (a->uses_albedo || a->uses_bump)) prog = PROG_GLTF_TEX;
+    dim3 tiles(tiles_x, bands), blk(kBlock);
+    if (count) hipLaunchKernelGGL((wf_raygen<true>), tiles, blk, 0, s, *a, *w);
+    else hipLaunchKernelGGL((wf_raygen<false>), tiles, blk, 0, s, *a, *w);
+#define WF_BOUNCE(P, C)                                                                              \
+    for (int b = 0; b < 6; b++) {                                                                    \
+        hipLaunchKernelGGL((wf_extend<P, C>), dim3(persist_blocks), blk, 0, s, *a, *w, b);         \
+        if (kIsGltf<P>) hipLaunchKernelGGL((wf_bvh<P, C>), dim3(persist_blocks), blk, 0, s, *a, *w, b); \
+        hipLaunchKernelGGL((wf_shade<P, C>), dim3(persist_blocks), blk, 0, s, *a, *w, b);          \
+    }
+    if (count) {
+        switch (prog) {
+        case PROG_CORNELL: WF_BOUNCE(PROG_CORNELL, true) break;
+        case PROG_GLTF: WF_BOUNCE(PROG_GLTF, true) break;
+        case PROG_GLTF_TEX: WF_BOUNCE(PROG_GLTF_TEX, true) break;
+        default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (prog) {
+        case PROG_CORNELL: WF_BOUNCE(PROG_CORNELL, false) break;
+        case PROG_GLTF: WF_BOUNCE(PROG_GLTF, false) break;
+        case PROG_GLTF_TEX: WF_BOUNCE(PROG_GLTF_TEX, false) break;
+        default: return hipErrorInvalidValue;
+        }
+    }
+#undef WF_BOUNCE
+    hipLaunchKernelGGL(wf_finish, tiles, blk, 0, s, *a, *w);
+    return hipGetLastError();
+}

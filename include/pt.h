@@ -124,6 +124,11 @@ int pt_write_pixels(pt_ctx* ctx, pt_texture* tex, const void* src, size_t bytes)
  * 16-row bands b with b % num_parts == part (bands are whole 2x2 quads, so derivatives are
  * unchanged). screenOutput/copy stay full-frame. num_parts = 1 restores full frames. */
 int pt_set_row_partition(pt_ctx* ctx, int num_parts, int part);
+/* Path-tracing backend of this context: PT_BACKEND_WAVEFRONT (default: per-segment kernels over
+ * compacted path queues) or PT_BACKEND_MEGAKERNEL (one kernel, one lane per path). Results are
+ * bit-identical; the choice only changes speed. */
+enum pt_backend { PT_BACKEND_MEGAKERNEL = 0, PT_BACKEND_WAVEFRONT = 1 };
+int pt_set_backend(pt_ctx* ctx, int backend);
 /* Device pointer of a render target's RGBA32F storage (for RCCL collectives from the host). */
 void* pt_texture_device_ptr(pt_texture* tex);
 /* Device time of the last pt_render of each program kind, in ms (HIP events on the context

@@ -104,13 +104,23 @@ def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1):
     return accs, canvases, player
 
 
+BACKENDS = ["wavefront", "megakernel"]
+
+
+@pytest.fixture(params=BACKENDS)
+def backend(request, engine):
+    engine.set_backend(request.param)
+    yield request.param
+    engine.set_backend("wavefront")
+
+
 @pytest.mark.parametrize("name,frames", [
     ("cornell_256", None),
     ("gltf_teapot_320x180", None),
     ("gltf_duck_320x180", None),
     ("gltf_helmet_320x180", None),
 ])
-def test_stream_bitexact(engine, name, frames):
+def test_stream_bitexact(engine, backend, name, frames):
     """Whole recorded streams (path trace -> copy -> output per frame) match the oracle exactly."""
     meta = H.stream(name)
     ref_acc, ref_can, _ = H.oracle_replay(meta, frames, with_output=True)
@@ -120,7 +130,7 @@ def test_stream_bitexact(engine, name, frames):
         assert _bits_equal(rc, gc), "%s frame %d canvas: %s" % (name, i, _diff_report(rc, gc))
 
 
-def test_bunny_1080p_bitexact_and_counters(engine):
+def test_bunny_1080p_bitexact_and_counters(engine, backend):
     """BASELINE config 2 at full size (1920x1080, StanfordBunny via BVH_Fast_Builder layout)."""
     meta = H.stream("gltf_bunny_1080p")
     ref_acc, ref_can, ref_cnt = H.oracle_replay(meta, 2, with_output=True)
@@ -139,7 +149,7 @@ def test_bunny_1080p_bitexact_and_counters(engine):
 
 
 @pytest.mark.parametrize("parts", [2, 3, 8])
-def test_row_partition_is_exact(engine, parts):
+def test_row_partition_is_exact(engine, backend, parts):
     """Band sharding (the multi-GPU split) reproduces the full-frame result bit for bit."""
     meta = H.stream("gltf_teapot_320x180")
     full, _, _ = _replay_gpu(engine, meta, 2)
@@ -148,7 +158,7 @@ def test_row_partition_is_exact(engine, parts):
         assert _bits_equal(a, b), _diff_report(a, b)
 
 
-def test_odd_sizes_bitexact(engine):
+def test_odd_sizes_bitexact(engine, backend):
     """Odd target sizes: quad helpers beyond the edge, partial 16x16 tiles, partial bands."""
     meta = H.stream("gltf_teapot_320x180")
     ref_acc, ref_can, _ = H.oracle_replay(meta, 2, width=203, height=117, with_output=True)
@@ -158,7 +168,7 @@ def test_odd_sizes_bitexact(engine):
         assert _bits_equal(rc, gc), _diff_report(rc, gc)
 
 
-def test_in_place_history(engine):
+def test_in_place_history(engine, backend):
     """previousBuffer bound to the target itself (legal: each pixel reads only its own texel)."""
     import babylon_pt as bp
     meta = H.stream("cornell_256")
