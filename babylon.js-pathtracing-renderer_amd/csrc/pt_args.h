@@ -75,20 +75,30 @@ struct TraceArgs {
     unsigned* err;                  // ErrBits
 };
 
-// wavefront buffers (pt_wavefront.hip): path state travels with the queue as 4 x 16-byte SoA
-// records, double-buffered between bounces; per-pixel outputs are indexed py * wq + px
+// wavefront buffers (pt_wavefront.hip). Path queues are split into kShards shards of `shard_cap`
+// slots: shard s holds the paths of tiles t with t % kShards == s, and is produced and consumed by
+// blocks b with b % kShards == s, so a path never changes shard and each queue append is one
+// atomic per block-iteration on that shard's counter (no single hot word). Path state travels with
+// the queue as 4 x 16-byte SoA records, double-buffered between bounces; per-pixel outputs are
+// indexed py * wq + px.
+constexpr int kShards = 16;
+constexpr unsigned kHole = 0xFFFFFFFFu;   // queue-0 slot of a tile lane outside the frame
+
 struct WfBufs {
-    float4* qA[2];          // ro.xyz, pixel index (bits)
+    float4* qA[2];          // ro.xyz, pixel index (bits; kHole = empty slot)
     float4* qB[2];          // rd.xyz, blueNoise counter
     float4* qC[2];          // mask.xyz, metallicRoughness.g
     float4* qD[2];          // seed.xy (bits), flags (bits), blue-noise bytes (bits)
     float4* hit0;           // per slot of the current bounce: t, object id (bits), u, v
     float4* hit1;           // hitNormal.xyz
-    unsigned* bvhq;         // slots whose ray enters the model's root box this bounce
+    unsigned* bvhq;         // per shard: slots whose ray enters the model's root box this bounce
     float4* gb0;            // per pixel: objectNormal.xyz, objectID
     float4* gb1;            // per pixel: objectColor.xyz, pixelSharpness
     float4* rad;            // per pixel: CalculateRadiance() result
-    unsigned* cnt;          // [b] = live paths entering bounce b (0..6); [8 + b] = BVH queue of bounce b
+    float2* spill;          // BVH stack levels >= kStackLds: [level][persistent lane]
+    unsigned* cnt;          // [b * kShards + s]: live paths of shard s entering bounce b (b = 0..6)
+    unsigned* bcnt;         // [b * kShards + s]: BVH queue of shard s at bounce b
+    unsigned shard_cap;     // slots per shard
     int wq, hq;             // quad-rounded frame size
 };
 

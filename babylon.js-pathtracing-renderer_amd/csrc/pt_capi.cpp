@@ -78,7 +78,7 @@ struct pt_ctx {
     int cu_count = 256;
     pt::WfBufs wf = {};
     void* wf_mem = nullptr;
-    size_t wf_pixels = 0;
+    size_t wf_pixels = 0, wf_slots = 0, wf_spill = 0;
     hipEvent_t ev0[kProgSlots] = {}, ev1[kProgSlots] = {};
     bool ev_used[kProgSlots] = {};
     // timing window: per draw event pairs, reused across windows
@@ -248,30 +248,36 @@ int end_draw(pt_ctx* c, int prog)
     return PT_OK;
 }
 
-// (re)allocate the wavefront buffers for a wq x hq quad-rounded frame: one slab, carved
-int wf_reserve(pt_ctx* c, int wq, int hq)
+// (re)allocate the wavefront buffers for `tiles` 16x16 tiles of a wq x hq quad-rounded frame and
+// a persistent grid of `blocks` blocks: one slab, carved into the WfBufs arrays
+int wf_reserve(pt_ctx* c, int wq, int hq, int tiles, int blocks)
 {
-    const size_t P = (size_t)wq * hq;
-    if (P <= c->wf_pixels && c->wf_mem) {
-        c->wf.wq = wq; c->wf.hq = hq;
+    const unsigned cap = (unsigned)((tiles + pt::kShards - 1) / pt::kShards) * pt::kBlock;
+    const size_t slots = (size_t)cap * pt::kShards;
+    const size_t pixels = (size_t)wq * hq;
+    const size_t spill = (size_t)(pt::kStackLevels - pt::kStackLds) * blocks * pt::kBlock;
+    if (c->wf_mem && slots <= c->wf_slots && pixels <= c->wf_pixels && spill <= c->wf_spill) {
+        c->wf.shard_cap = cap; c->wf.wq = wq; c->wf.hq = hq;
         return PT_OK;
     }
     if (c->wf_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->wf_mem)); c->wf_mem = nullptr; }
-    const size_t f4 = P * sizeof(float4);
-    const size_t bytes = 8 * f4 + 2 * f4 + 3 * f4 + P * sizeof(unsigned) + 256;
+    const size_t f4s = slots * sizeof(float4), f4p = pixels * sizeof(float4);
+    const size_t bytes = 4096 + 10 * f4s + 3 * f4p + slots * sizeof(unsigned) + spill * sizeof(float2) + 16 * 256;
     HIPCHK(c, hipMalloc(&c->wf_mem, bytes));
     char* m = (char*)c->wf_mem;
     auto take = [&](size_t n) { char* r = m; m += (n + 255) & ~(size_t)255; return r; };
-    c->wf.cnt = (unsigned*)take(256);
+    c->wf.cnt = (unsigned*)take(4096);
+    c->wf.bcnt = c->wf.cnt + 8 * pt::kShards;
     for (int k = 0; k < 2; k++) {
-        c->wf.qA[k] = (float4*)take(f4); c->wf.qB[k] = (float4*)take(f4);
-        c->wf.qC[k] = (float4*)take(f4); c->wf.qD[k] = (float4*)take(f4);
+        c->wf.qA[k] = (float4*)take(f4s); c->wf.qB[k] = (float4*)take(f4s);
+        c->wf.qC[k] = (float4*)take(f4s); c->wf.qD[k] = (float4*)take(f4s);
     }
-    c->wf.hit0 = (float4*)take(f4); c->wf.hit1 = (float4*)take(f4);
-    c->wf.gb0 = (float4*)take(f4); c->wf.gb1 = (float4*)take(f4); c->wf.rad = (float4*)take(f4);
-    c->wf.bvhq = (unsigned*)take(P * sizeof(unsigned));
-    c->wf_pixels = P;
-    c->wf.wq = wq; c->wf.hq = hq;
+    c->wf.hit0 = (float4*)take(f4s); c->wf.hit1 = (float4*)take(f4s);
+    c->wf.gb0 = (float4*)take(f4p); c->wf.gb1 = (float4*)take(f4p); c->wf.rad = (float4*)take(f4p);
+    c->wf.bvhq = (unsigned*)take(slots * sizeof(unsigned));
+    c->wf.spill = (float2*)take(spill * sizeof(float2));
+    c->wf_slots = slots; c->wf_pixels = pixels; c->wf_spill = spill;
+    c->wf.shard_cap = cap; c->wf.wq = wq; c->wf.hq = hq;
     return PT_OK;
 }
 
@@ -327,18 +333,18 @@ int render_trace(pt_effect* fx, pt_texture* target)
     a.err = c->d_err;
     int gx = (target->w + pt::kTile - 1) / pt::kTile;
     int gy = bands_owned(c, target->h);
+    const int persist = ((c->cu_count * 4 + pt::kShards - 1) / pt::kShards) * pt::kShards;
     if (c->backend == PT_BACKEND_WAVEFRONT) {
-        int rc = wf_reserve(c, gx * pt::kTile, ((target->h + pt::kTile - 1) / pt::kTile) * pt::kTile);
+        // the quad-rounded frame is what gets shaded (helpers at odd edges included)
+        int rc = wf_reserve(c, (target->w + 1) & ~1, (target->h + 1) & ~1, gx * gy, persist);
         if (rc) return rc;
-        c->wf.wq = (target->w + 1) & ~1;   // quad-rounded frame: the pixels that are shaded
-        c->wf.hq = (target->h + 1) & ~1;
     }
     int rc = begin_draw(c, fx->prog);
     if (rc) return rc;
     if (gy > 0) {
         if (c->backend == PT_BACKEND_WAVEFRONT) {
-            HIPCHK(c, hipMemsetAsync(c->wf.cnt, 0, 64, c->stream));
-            HIPCHK(c, pt_launch_wavefront(fx->prog, c->counting ? 1 : 0, &a, &c->wf, gx, gy, c->cu_count * 8, c->stream));
+            HIPCHK(c, hipMemsetAsync(c->wf.cnt, 0, 16 * pt::kShards * sizeof(unsigned), c->stream));
+            HIPCHK(c, pt_launch_wavefront(fx->prog, c->counting ? 1 : 0, &a, &c->wf, gx, gy, persist, c->stream));
         } else {
             HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, gy, c->stream));
         }

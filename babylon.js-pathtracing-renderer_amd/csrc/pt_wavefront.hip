@@ -14,7 +14,8 @@
 //     wf_bvh      <P>    the BVH walk (js/GLTFModelPathTracing_FragmentShader.js:201-344) only for
 //                        those rays: every lane of a wave traverses
 //     wf_shade    <P>    one iteration of CalculateRadiance's loop body; surviving paths are appended
-//                        to queue b+1 (wave ballot + prefix + one atomic per wave)
+//                        to queue b+1 (wave ballots + block prefix + one atomic per block-iteration
+//                        on the shard's counter: kShards counters, never one hot word)
 //   wf_finish            main() after CalculateRadiance: 2x2-quad derivatives + accumulation
 //
 // Path state travels with the queue as four 16-byte SoA records (coalesced dwordx4 loads/stores);
@@ -49,19 +50,31 @@ struct HitRec {
 PT_D float u2f(unsigned u) { return __uint_as_float(u); }
 PT_D unsigned f2u(float f) { return __float_as_uint(f); }
 
-// wave-level stream compaction: returns this lane's slot in `queue` (valid only when `alive`)
-PT_D unsigned wave_append(unsigned* counter, bool alive)
+// block-level stream compaction: every thread of the block calls it (block-uniform loop); returns
+// this lane's slot offset in the shard (valid only when `alive`). One atomic per call per block.
+PT_D unsigned block_append(unsigned* counter, bool alive, unsigned* sh)
 {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const unsigned long long m = __ballot(alive);
-    const unsigned total = (unsigned)__popcll(m);
-    unsigned base = 0;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((long long)m) - 1;
-    if (total && lane == leader) base = atomicAdd(counter, total);
-    base = __shfl(base, leader < 0 ? 0 : leader, 64);
-    const unsigned long long below = m & ((1ull << lane) - 1ull);
-    return base + (unsigned)__popcll(below);
+    if (lane == 0) sh[wave] = (unsigned)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned total = sh[0] + sh[1] + sh[2] + sh[3];
+        sh[4] = total ? atomicAdd(counter, total) : 0u;
+    }
+    __syncthreads();
+    unsigned off = sh[4];
+    for (int k = 0; k < wave; k++) off += sh[k];
+    off += (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+    __syncthreads();   // sh[] is reused by the next call
+    return off;
 }
+
+// the shard a persistent block serves, its rank within the shard, and the shard's block count
+struct ShardIter {
+    unsigned s, k, nb;
+    PT_D ShardIter() : s(blockIdx.x % kShards), k(blockIdx.x / kShards), nb(gridDim.x / kShards) {}
+};
 
 template <bool COUNT>
 PT_D void count_add(const TraceArgs& a, int which, unsigned v)
@@ -117,9 +130,13 @@ __global__ __launch_bounds__(kBlock) void wf_raygen(TraceArgs a, WfBufs w)
         w.gb1[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         w.rad[pix] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    const unsigned slot = wave_append(&w.cnt[0], active);
+    // tile t -> shard t % kShards, deterministic slot (no atomics); lanes outside the frame are holes
+    const unsigned t = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned s = t % kShards;
+    const unsigned slot = s * w.shard_cap + (t / kShards) * kBlock + tid;
+    if (tid == 0) atomicAdd(&w.cnt[s], (unsigned)kBlock);
+    w.qA[0][slot] = make_float4(p.ro.x, p.ro.y, p.ro.z, u2f(active ? pix : kHole));
     if (active) {
-        w.qA[0][slot] = make_float4(p.ro.x, p.ro.y, p.ro.z, u2f(pix));
         w.qB[0][slot] = make_float4(p.rd.x, p.rd.y, p.rd.z, -1.0f);   // blueNoise counter starts at -1
         w.qC[0][slot] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);           // mask, roughness
         w.qD[0][slot] = make_float4(u2f(p.s0), u2f(p.s1), u2f(F_SPECULAR), u2f(bnb));
@@ -131,49 +148,53 @@ __global__ __launch_bounds__(kBlock) void wf_raygen(TraceArgs a, WfBufs w)
 template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kBlock) void wf_extend(TraceArgs a, WfBufs w, int b)
 {
-    const unsigned n = w.cnt[b];
-    const unsigned stride = gridDim.x * kBlock;
+    __shared__ unsigned sh[8];
+    const ShardIter it;
+    const unsigned n = w.cnt[b * kShards + it.s];
+    const unsigned shard0 = it.s * w.shard_cap;
     const int q = b & 1;
-    for (unsigned base = blockIdx.x * kBlock; base < n; base += stride) {
-        const unsigned i = base + threadIdx.x;
-        const bool live = i < n;
+    for (unsigned base = it.k * kBlock; base < n; base += it.nb * kBlock) {
+        const unsigned i = shard0 + base + threadIdx.x;
         bool toBvh = false;
-        if (live) {
-            float4 A = w.qA[q][i], B = w.qB[q][i];
-            f3 ro = mk(A.x, A.y, A.z), rd = mk(B.x, B.y, B.z);
-            float t = kINF;
-            int id = -1;
-            f3 sn = mk(0, 0, 0);
+        if (base + threadIdx.x < n) {
+            float4 A = w.qA[q][i];
+            if (f2u(A.w) != kHole) {
+                float4 B = w.qB[q][i];
+                f3 ro = mk(A.x, A.y, A.z), rd = mk(B.x, B.y, B.z);
+                float t = kINF;
+                int id = -1;
+                f3 sn = mk(0, 0, 0);
 #pragma unroll 1
-            for (int s = 0; s < 2; s++) {
-                const SphereArg& S = a.sph[s];
-                f3 nn;
-                float d = unitSphere(mul(S.inv, ro, 1.0f), mul(S.inv, rd, 0.0f), nn);
-                if (d < t) { t = d; id = s; sn = nn; }
-            }
+                for (int s = 0; s < 2; s++) {
+                    const SphereArg& S = a.sph[s];
+                    f3 nn;
+                    float d = unitSphere(mul(S.inv, ro, 1.0f), mul(S.inv, rd, 0.0f), nn);
+                    if (d < t) { t = d; id = s; sn = nn; }
+                }
 #pragma unroll 1
-            for (int k = 0; k < 6; k++) {
-                float d = gmin(quadTriangle(a.qtri[2 * k], ro, rd), quadTriangle(a.qtri[2 * k + 1], ro, rd));
-                if (d < t) { t = d; id = 2 + k; }
+                for (int k = 0; k < 6; k++) {
+                    float d = gmin(quadTriangle(a.qtri[2 * k], ro, rd), quadTriangle(a.qtri[2 * k + 1], ro, rd));
+                    if (d < t) { t = d; id = 2 + k; }
+                }
+                f3 hn = mk(0, 0, 0);
+                if (id >= 0 && id < 2) hn = normalize(mul3t(a.sph[id].inv, normalize(sn)));
+                else if (id >= 2) hn = normalize(a.qnormal[id - 2]);
+                if (COUNT) count_add<true>(a, C_SEGMENTS, 1);
+                if (kIsGltf<PROG>) {
+                    f3 O = mul(a.model, ro, 1.0f), D = mul(a.model, rd, 0.0f);
+                    f3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+                    float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
+                    if (COUNT) count_add<true>(a, C_NODE, 1);
+                    float tRoot = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
+                    toBvh = tRoot < t;
+                }
+                w.hit0[i] = make_float4(t, u2f((unsigned)id), 0.0f, 0.0f);
+                w.hit1[i] = make_float4(hn.x, hn.y, hn.z, 0.0f);
             }
-            f3 hn = mk(0, 0, 0);
-            if (id >= 0 && id < 2) hn = normalize(mul3t(a.sph[id].inv, normalize(sn)));
-            else if (id >= 2) hn = normalize(a.qnormal[id - 2]);
-            if (COUNT) count_add<true>(a, C_SEGMENTS, 1);
-            if (kIsGltf<PROG>) {
-                f3 O = mul(a.model, ro, 1.0f), D = mul(a.model, rd, 0.0f);
-                f3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
-                float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
-                if (COUNT) count_add<true>(a, C_NODE, 1);
-                float tRoot = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
-                toBvh = tRoot < t;
-            }
-            w.hit0[i] = make_float4(t, u2f((unsigned)id), 0.0f, 0.0f);
-            w.hit1[i] = make_float4(hn.x, hn.y, hn.z, 0.0f);
         }
         if (kIsGltf<PROG>) {
-            const unsigned slot = wave_append(&w.cnt[8 + b], toBvh);
-            if (toBvh) w.bvhq[slot] = i;
+            const unsigned off = block_append(&w.bcnt[b * kShards + it.s], toBvh, sh);
+            if (toBvh) w.bvhq[shard0 + off] = i;
         }
     }
 }
@@ -183,15 +204,19 @@ template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b)
 {
     __shared__ float2 lds[kStackLds * kBlock];
-    const unsigned n = w.cnt[8 + b];
-    const unsigned stride = gridDim.x * kBlock;
+    const ShardIter it;
+    const unsigned n = w.bcnt[b * kShards + it.s];
+    const unsigned shard0 = it.s * w.shard_cap;
     const int q = b & 1;
     const unsigned tid = threadIdx.x;
-    float2 deep[kStackLevels - kStackLds];
-    for (unsigned base = blockIdx.x * kBlock; base < n; base += stride) {
+    // stack levels beyond LDS: a global slab indexed [level][persistent lane] (no scratch: a
+    // scratch-using kernel throttles how many waves the CP keeps resident)
+    float2* deep = w.spill + (size_t)blockIdx.x * kBlock + tid;
+    const size_t dstride = (size_t)gridDim.x * kBlock;
+    for (unsigned base = it.k * kBlock; base < n; base += it.nb * kBlock) {
         const unsigned j = base + tid;
         if (j >= n) continue;
-        const unsigned i = w.bvhq[j];
+        const unsigned i = w.bvhq[shard0 + j];
         float4 A = w.qA[q][i], B = w.qB[q][i];
         float hitT = w.hit0[i].x;
         f3 ro = mk(A.x, A.y, A.z), rd = mk(B.x, B.y, B.z);
@@ -213,7 +238,7 @@ __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b
                 stackptr = stackptr - 1.0f;
                 if (stackptr < 0.0f) break;
                 int si = (int)stackptr;
-                float2 e = si < kStackLds ? lds[si * kBlock + tid] : deep[si - kStackLds];
+                float2 e = si < kStackLds ? lds[si * kBlock + tid] : deep[(si - kStackLds) * dstride];
                 curId = e.x; curT = e.y;
                 if (curT >= hitT) continue;
                 c0 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f);
@@ -239,7 +264,7 @@ __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b
                     if (skip) {
                         int si = (int)stackptr;
                         if (si < kStackLds) lds[si * kBlock + tid] = make_float2(idB, tB);
-                        else if (si < kStackLevels) deep[si - kStackLds] = make_float2(idB, tB);
+                        else if (si < kStackLevels) deep[(si - kStackLds) * dstride] = make_float2(idB, tB);
                         else { ovf++; atomicOr(a.err, (unsigned)E_STACK); }
                         stackptr = stackptr + 1.0f;
                     }
@@ -294,15 +319,18 @@ template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kBlock) void wf_shade(TraceArgs a, WfBufs w, int b)
 {
     constexpr bool gltf = kIsGltf<PROG>;
-    const unsigned n = w.cnt[b];
-    const unsigned stride = gridDim.x * kBlock;
+    __shared__ unsigned sh[8];
+    const ShardIter it;
+    const unsigned n = w.cnt[b * kShards + it.s];
+    const unsigned shard0 = it.s * w.shard_cap;
     const int q = b & 1, q2 = q ^ 1;
-    for (unsigned base = blockIdx.x * kBlock; base < n; base += stride) {
-        const unsigned i = base + threadIdx.x;
+    for (unsigned base = it.k * kBlock; base < n; base += it.nb * kBlock) {
+        const unsigned i = shard0 + base + threadIdx.x;
         bool alive = false;
         float4 oA, oB, oC, oD;
-        if (i < n) {
-            const float4 A = w.qA[q][i], B = w.qB[q][i], C = w.qC[q][i], D = w.qD[q][i];
+        const float4 A = base + threadIdx.x < n ? w.qA[q][i] : make_float4(0.0f, 0.0f, 0.0f, u2f(kHole));
+        if (f2u(A.w) != kHole) {
+            const float4 B = w.qB[q][i], C = w.qC[q][i], D = w.qD[q][i];
             const float4 H0 = w.hit0[i], H1 = w.hit1[i];
             const unsigned pix = f2u(A.w);
             Path p;
@@ -453,7 +481,7 @@ __global__ __launch_bounds__(kBlock) void wf_shade(TraceArgs a, WfBufs w, int b)
             } while (false);
             if (COUNT) count_add<true>(a, C_RGBA8, taps);
         }
-        const unsigned slot = wave_append(&w.cnt[b + 1], alive);
+        const unsigned slot = shard0 + block_append(&w.cnt[(b + 1) * kShards + it.s], alive, sh);
         if (alive) {
             w.qA[q2][slot] = oA;
             w.qB[q2][slot] = oB;

@@ -433,6 +433,44 @@ def path_uniform(frame, name):
     raise KeyError(name)
 
 
+# ------------------------------------------------------------------------------------------------
+# Multi-GPU framebuffer bands (pt_set_row_partition): 16-row bands dealt round-robin to ranks.
+# The helpers work on torch tensors on any device, so the same code runs on RCCL (GPU) and gloo (CPU).
+
+BAND = 16
+
+
+def padded_bands(height, world):
+    """Band count padded to a multiple of `world`, so every rank owns the same number of bands."""
+    nb = (height + BAND - 1) // BAND
+    return ((nb + world - 1) // world) * world
+
+
+def owned_rows(height, world, rank):
+    """Rows of the frame this rank shades (bands b with b % world == rank)."""
+    rows = []
+    for b in range(rank, (height + BAND - 1) // BAND, world):
+        rows.extend(range(b * BAND, min(height, (b + 1) * BAND)))
+    return rows
+
+
+def band_view(acc_padded, world):
+    """View a band-padded (padded_bands*16, W, 4) accumulation as (bands/world, world, 16, W, 4):
+    [:, r] is rank r's share, strided in memory (no repacking of the frame)."""
+    rows, w, c = acc_padded.shape
+    return acc_padded.view(rows // (BAND * world), world, BAND, w, c)
+
+
+def gather_bands(dist, acc_padded, world, rank, send_buf, gather_list, full_padded=None):
+    """Gather every rank's bands of `acc_padded` into rank 0's `full_padded` (RCCL or gloo)."""
+    send_buf.copy_(band_view(acc_padded, world)[:, rank])
+    dist.gather(send_buf, gather_list if rank == 0 else None, dst=0)
+    if rank == 0:
+        fv = band_view(full_padded, world)
+        for r in range(world):
+            fv[:, r].copy_(gather_list[r])
+
+
 def load_stream(path):
     with open(path) as f:
         return json.load(f)

@@ -105,8 +105,7 @@ def main():
     mesh = H.texture_payloads(meta, H.mesh(meta))
 
     rt_ptrs, acc_t, full_t = None, None, None
-    nb = (Hh + 15) // 16
-    pad_bands = ((nb + world - 1) // world) * world
+    pad_bands = bp.padded_bands(Hh, world)
     if dist is not None:
         import torch
         # the accumulation target is the first H rows of a band-padded torch buffer, so a rank's
@@ -119,15 +118,12 @@ def main():
     engine.resize_canvas(W, Hh)
     engine.set_row_partition(world, rank)
 
-    # band bookkeeping for the gather: rows of 16-row bands b with b % world == rank
     if dist is not None:
         import torch
         full_t = torch.zeros((pad_bands * 16, W, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
         send_t = torch.zeros((pad_bands // world, 16, W, 4), dtype=torch.float32, device="cuda")
         gather_list = [torch.empty_like(send_t) for _ in range(world)] if rank == 0 else None
-        out_rt = None
-        if rank == 0:
-            out_rt = bp.RenderTargetTexture("gathered", (W, Hh), engine, full_t.data_ptr())
+        out_rt = bp.RenderTargetTexture("gathered", (W, Hh), engine, full_t.data_ptr()) if rank == 0 else None
         out_wrapper = player.wrappers["screenOutputEffectWrapper"]
 
     def step(k):
@@ -142,12 +138,8 @@ def main():
             return
         # RCCL gather of the accumulation bands to rank 0, then screenOutput there
         engine.sync()
-        send_t.copy_(acc_t.view(pad_bands // world, world, 16, W, 4)[:, rank])
-        dist.gather(send_t, gather_list, dst=0)
+        bp.gather_bands(dist, acc_t, world, rank, send_t, gather_list, full_t)
         if rank == 0:
-            fv = full_t.view(pad_bands // world, world, 16, W, 4)
-            for r in range(world):
-                fv[:, r].copy_(gather_list[r])
             torch.cuda.current_stream().synchronize()
             fx = out_wrapper.effect
             fx.setTexture("accumulationBuffer", out_rt)

@@ -1,0 +1,61 @@
+"""Multi-GPU path on CPU: world_size 2 over gloo. Each rank shades its 16-row bands (the split
+pt_set_row_partition makes on the GPU; here the CPU oracle renders the owned rows), the bands are
+gathered to rank 0 with the same helpers bench.py uses over RCCL, and the assembled frame must equal
+the single-process full-frame render bit for bit."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import helpers as H
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, name, w, h, out_path):
+    import babylon_pt as bp
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        meta = H.stream(name)
+        sc = H.oracle_scene(meta, w, h)
+        u = H.with_resolution(H.path_call(meta["frames"][0])["uniforms"], w, h)
+        pad = bp.padded_bands(h, world)
+        acc = torch.zeros((pad * 16, w, 4), dtype=torch.float32)
+        prev = np.zeros((h, w, 4), np.float32)
+        for b in range(rank, (h + 15) // 16, world):        # this rank's bands only
+            r0, r1 = b * 16, min(h, (b + 1) * 16)
+            out, _ = sc.path_trace(u, prev, r0, r1, nthreads=2)
+            acc[r0:r1] = torch.from_numpy(out[r0:r1])
+        assert sorted(bp.owned_rows(h, world, rank)) == [r for b in range(rank, (h + 15) // 16, world)
+                                                        for r in range(b * 16, min(h, b * 16 + 16))]
+        send = torch.zeros((pad // world, 16, w, 4), dtype=torch.float32)
+        glist = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+        full = torch.zeros((pad * 16, w, 4), dtype=torch.float32) if rank == 0 else None
+        bp.gather_bands(dist, acc, world, rank, send, glist, full)
+        if rank == 0:
+            np.save(out_path, full[:h].numpy())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_band_gather_assembles_the_frame(tmp_path, world):
+    name, w, h = "gltf_teapot_320x180", 96, 72
+    out = str(tmp_path / "full.npy")
+    mp.spawn(_worker, args=(world, _free_port(), name, w, h, out), nprocs=world, join=True)
+    got = np.load(out)
+    meta = H.stream(name)
+    ref, _, _ = H.oracle_replay(meta, 1, width=w, height=h)
+    assert np.array_equal(got.view(np.uint32), ref[0].view(np.uint32))
