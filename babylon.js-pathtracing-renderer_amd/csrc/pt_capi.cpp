@@ -66,7 +66,8 @@ struct pt_effect {
 
 struct pt_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // the stream all work is enqueued on
+    hipStream_t own_stream = nullptr;  // the context's own stream (pt_set_stream(NULL) restores it)
     std::string err;
     uchar4* canvas = nullptr;
     int cw = 0, ch = 0;
@@ -465,7 +466,8 @@ pt_ctx* pt_ctx_create(int device, int* err)
     c->device = device;
     c->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    c->stream = c->own_stream;
     if (e == hipSuccess) e = hipMalloc(&c->d_err, 256);
     if (e == hipSuccess) e = hipMalloc(&c->d_counters, pt::C_NUM * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(c->d_err, 0, 256);
@@ -496,7 +498,7 @@ void pt_ctx_destroy(pt_ctx* c)
     if (c->wf_mem) hipFree(c->wf_mem);
     if (c->d_err) hipFree(c->d_err);
     if (c->d_counters) hipFree(c->d_counters);
-    if (c->stream) hipStreamDestroy(c->stream);
+    if (c->own_stream) hipStreamDestroy(c->own_stream);
     delete c;
 }
 
@@ -694,6 +696,15 @@ int pt_write_pixels(pt_ctx* c, pt_texture* t, const void* src, size_t bytes)
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(t->d, src, bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PT_OK;
+}
+
+int pt_set_stream(pt_ctx* c, void* stream)
+{
+    if (!c) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));   // work already queued finishes first
+    c->stream = stream ? (hipStream_t)stream : c->own_stream;
     return PT_OK;
 }
 

@@ -38,7 +38,7 @@ SYMBOLS = [
     "pt_texture_create_rgba32f", "pt_texture_create_rgba8", "pt_render_target_create", "pt_render_target_wrap",
     "pt_render_target_resize", "pt_texture_size", "pt_texture_destroy",
     "pt_render", "pt_read_pixels", "pt_write_pixels",
-    "pt_set_row_partition", "pt_set_backend", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
+    "pt_set_row_partition", "pt_set_backend", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
     "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_math_probe", "pt_version",
 ]
 
@@ -72,7 +72,7 @@ def lib():
         "pt_render": ([vp, vp], i32), "pt_read_pixels": ([vp, vp, vp, ctypes.c_size_t], i32),
         "pt_write_pixels": ([vp, vp, vp, ctypes.c_size_t], i32),
         "pt_set_row_partition": ([vp, i32, i32], i32), "pt_texture_device_ptr": ([vp], vp),
-        "pt_set_backend": ([vp, i32], i32),
+        "pt_set_backend": ([vp, i32], i32), "pt_set_stream": ([vp, vp], i32),
         "pt_last_render_ms": ([vp, i32, f32p], i32), "pt_set_counting": ([vp, i32], i32),
         "pt_timing_begin": ([vp], i32),
         "pt_timing_end": ([vp, i32, ctypes.POINTER(ctypes.c_double), ip], i32),
@@ -127,6 +127,10 @@ class Engine:
 
     def set_row_partition(self, parts, part):
         self.check(lib().pt_set_row_partition(self.ctx, parts, part), "pt_set_row_partition")
+
+    def set_stream(self, hip_stream):
+        """Enqueue on a caller-owned stream (an int handle, e.g. torch.cuda.current_stream().cuda_stream)."""
+        self.check(lib().pt_set_stream(self.ctx, ctypes.c_void_p(hip_stream) if hip_stream else None), "pt_set_stream")
 
     def set_backend(self, backend):
         """'wavefront' (default) or 'megakernel': same bits, different schedule."""

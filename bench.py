@@ -114,6 +114,9 @@ def main():
         copy_t = torch.zeros((Hh, W, 4), dtype=torch.float32, device="cuda")
         rt_ptrs = {"pathTracingRenderTarget": acc_t.data_ptr(), "screenCopyRenderTarget": copy_t.data_ptr()}
         torch.cuda.synchronize()
+    if dist is not None:
+        # draws, the band gather (RCCL) and rank 0's screenOutput are ordered on one stream
+        engine.set_stream(torch.cuda.current_stream().cuda_stream)
     player = bp.StreamPlayer(engine, meta, H.bluenoise(), mesh, W, Hh, rt_ptrs)
     engine.resize_canvas(W, Hh)
     engine.set_row_partition(world, rank)
@@ -136,11 +139,10 @@ def main():
         if dist is None:
             player.play_call(out_call)
             return
-        # RCCL gather of the accumulation bands to rank 0, then screenOutput there
-        engine.sync()
+        # RCCL gather of the accumulation bands to rank 0, then screenOutput there (all on the
+        # current stream: no host synchronisation inside the frame)
         bp.gather_bands(dist, acc_t, world, rank, send_t, gather_list, full_t)
         if rank == 0:
-            torch.cuda.current_stream().synchronize()
             fx = out_wrapper.effect
             fx.setTexture("accumulationBuffer", out_rt)
             u = out_call["uniforms"]

@@ -129,6 +129,10 @@ int pt_set_row_partition(pt_ctx* ctx, int num_parts, int part);
  * bit-identical; the choice only changes speed. */
 enum pt_backend { PT_BACKEND_MEGAKERNEL = 0, PT_BACKEND_WAVEFRONT = 1 };
 int pt_set_backend(pt_ctx* ctx, int backend);
+/* Enqueue this context's work on a caller-owned HIP stream (e.g. torch.cuda.current_stream(), so
+ * that draws and RCCL collectives are ordered without host syncs); NULL restores the context's own
+ * stream. The caller keeps the stream alive while the context uses it. */
+int pt_set_stream(pt_ctx* ctx, void* hip_stream);
 /* Device pointer of a render target's RGBA32F storage (for RCCL collectives from the host). */
 void* pt_texture_device_ptr(pt_texture* tex);
 /* Device time of the last pt_render of each program kind, in ms (HIP events on the context
