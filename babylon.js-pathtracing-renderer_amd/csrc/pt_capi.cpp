@@ -784,6 +784,23 @@ int pt_reset_counters(pt_ctx* c)
     return PT_OK;
 }
 
+int pt_queue_stats(pt_ctx* c, uint32_t out[16])
+{
+    if (!c || !out) return PT_ERR_ARG;
+    std::memset(out, 0, 16 * sizeof(uint32_t));
+    if (!c->wf_mem) return PT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<unsigned> h(16 * pt::kShards);
+    HIPCHK(c, hipMemcpy(h.data(), c->wf.cnt, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
+    for (int b = 0; b < 7; b++)
+        for (int s = 0; s < pt::kShards; s++) {
+            out[b] += h[b * pt::kShards + s];
+            if (b < 6) out[8 + b] += h[(8 + b) * pt::kShards + s];
+        }
+    return PT_OK;
+}
+
 int pt_math_probe(pt_ctx* c, int op, const float* x, const float* y, float* out, int n)
 {
     if (!c || !x || !out || n <= 0) return PT_ERR_ARG;

@@ -301,6 +301,15 @@ static napi_value ReadCounters(napi_env env, napi_callback_info info)
 }
 static napi_value ResetCounters(napi_env env, napi_callback_info info)
 { napi_value a[MAXARGS]; if (args(env, info, a, 1) < 0) return NULL; return num(env, pt_reset_counters((pt_ctx*)handle(env, a[0]))); }
+static napi_value QueueStats(napi_env env, napi_callback_info info)
+{
+    napi_value a[MAXARGS], r; if (args(env, info, a, 1) < 0) return NULL;
+    uint32_t q[16] = { 0 };
+    pt_queue_stats((pt_ctx*)handle(env, a[0]), q);
+    CHECK(napi_create_array_with_length(env, 16, &r));
+    for (uint32_t i = 0; i < 16; i++) napi_set_element(env, r, i, num(env, q[i]));
+    return r;
+}
 static napi_value Version(napi_env env, napi_callback_info info)
 {
     napi_value r; (void)info;
@@ -322,7 +331,7 @@ static napi_value Init(napi_env env, napi_value exports)
         { "pt_render", Render }, { "pt_read_pixels", ReadPixels }, { "pt_write_pixels", WritePixels },
         { "pt_set_row_partition", RowPartition }, { "pt_set_backend", SetBackend }, { "pt_set_stream", SetStream }, { "pt_texture_device_ptr", TexDevicePtr },
         { "pt_last_render_ms", LastRenderMs }, { "pt_timing_begin", TimingBegin }, { "pt_timing_end", TimingEnd },
-        { "pt_set_counting", SetCounting }, { "pt_read_counters", ReadCounters }, { "pt_reset_counters", ResetCounters },
+        { "pt_set_counting", SetCounting }, { "pt_read_counters", ReadCounters }, { "pt_reset_counters", ResetCounters }, { "pt_queue_stats", QueueStats },
         { "pt_version", Version },
     };
     for (size_t i = 0; i < sizeof(F) / sizeof(F[0]); i++) {

@@ -39,7 +39,7 @@ SYMBOLS = [
     "pt_render_target_resize", "pt_texture_size", "pt_texture_destroy",
     "pt_render", "pt_read_pixels", "pt_write_pixels",
     "pt_set_row_partition", "pt_set_backend", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
-    "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_math_probe", "pt_version",
+    "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_version",
 ]
 
 _lib = None
@@ -77,7 +77,8 @@ def lib():
         "pt_timing_begin": ([vp], i32),
         "pt_timing_end": ([vp, i32, ctypes.POINTER(ctypes.c_double), ip], i32),
         "pt_read_counters": ([vp, ctypes.POINTER(ctypes.c_uint64)], i32), "pt_reset_counters": ([vp], i32),
-        "pt_math_probe": ([vp, i32, vp, vp, vp, i32], i32), "pt_version": ([], ctypes.c_char_p),
+        "pt_math_probe": ([vp, i32, vp, vp, vp, i32], i32),
+        "pt_queue_stats": ([vp, ctypes.POINTER(ctypes.c_uint32)], i32), "pt_version": ([], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -161,6 +162,12 @@ class Engine:
         self.check(lib().pt_read_counters(self.ctx, buf), "pt_read_counters")
         keys = ("paths", "segments", "node_fetches", "leaf_tests", "hit_lookups", "rgba8_taps", "stack_overflow")
         return {k: int(v) for k, v in zip(keys, buf)}
+
+    def queue_stats(self):
+        """Wavefront queue sizes of the last draw: paths per bounce and BVH rays per bounce."""
+        buf = (ctypes.c_uint32 * 16)()
+        self.check(lib().pt_queue_stats(self.ctx, buf), "pt_queue_stats")
+        return {"paths": list(buf[0:7]), "bvh": list(buf[8:14])}
 
     def math_probe(self, op, x, y=None):
         x = np.ascontiguousarray(x, dtype=np.float32)

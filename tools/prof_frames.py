@@ -27,3 +27,5 @@ for k in range(a.frames):
         p.play_call(call)
 e.sync()
 print("ok", a.stream, a.frames)
+if os.environ.get("PT_QSTATS"):
+    print("queue stats:", e.queue_stats())
