@@ -69,6 +69,7 @@ struct TraceArgs {
     long long aabb_texels;
     const float4* tri;
     long long tri_texels;
+    const float4* bvh_pairs;   // child-pair records of tAABBTexture (PROG_PAIRS variants only)
     Tex8 albedo, bump, metal, emissive;
     // diagnostics
     unsigned long long* counters;   // C_NUM entries, only with counting builds

@@ -27,6 +27,8 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
+hipError_t pt_launch_bvh_pairs(const float4* aabb, long long texels, float4* rec, unsigned nrec, unsigned* bad,
+                               hipStream_t s);
 hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x, int bands,
                                int persist_blocks, hipStream_t s);
 }
@@ -55,6 +57,11 @@ struct pt_texture {
     int sampling = PT_SAMPLING_NEAREST;
     int invert_y = 0;
     bool external = false;   // caller-owned device memory (pt_render_target_wrap)
+    unsigned long long gen = 0;   // bumped by every host write of the texels
+    // child-pair BVH records derived from this texture (pt_bvh_pairs), valid for pairs_gen
+    float4* pairs = nullptr;
+    unsigned long long pairs_gen = ~0ull;
+    bool pairs_ok = false;
 };
 
 struct pt_effect {
@@ -75,7 +82,9 @@ struct pt_ctx {
     unsigned long long* d_counters = nullptr;
     bool counting = false;
     int num_parts = 1, part = 0;
-    int backend = PT_BACKEND_WAVEFRONT;
+    int backend = PT_BACKEND_MEGAKERNEL;
+    int bvh_layout = PT_BVH_PAIRS;
+    int bvh_used = -1;
     int cu_count = 256;
     pt::WfBufs wf = {};
     void* wf_mem = nullptr;
@@ -282,6 +291,29 @@ int wf_reserve(pt_ctx* c, int wq, int hq, int tiles, int blocks)
     return PT_OK;
 }
 
+// The child-pair records of a BVH texture, rebuilt when its texels changed since the last build.
+// Only for data textures (their texels change only through this API) of at most 2^24 texels (node
+// ids exact in float). Returns the records, or nullptr when the reference walk must be used.
+const float4* ensure_pairs(pt_ctx* c, pt_texture* t, int* rc)
+{
+    *rc = PT_OK;
+    const long long texels = (long long)t->w * t->h;
+    if (c->bvh_layout != PT_BVH_PAIRS || t->kind != TEX_F32 || texels > (1ll << 24)) return nullptr;
+    if (t->pairs_gen == t->gen) return t->pairs_ok ? t->pairs : nullptr;
+    const unsigned nrec = (unsigned)((texels + 1) / 2);
+    hipError_t e = hipSuccess;
+    if (!t->pairs) e = hipMalloc(&t->pairs, (size_t)nrec * 64);
+    unsigned bad = 0;
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_err + 1, 0, sizeof(unsigned), c->stream);
+    if (e == hipSuccess) e = pt_launch_bvh_pairs((const float4*)t->d, texels, t->pairs, nrec, c->d_err + 1, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(&bad, c->d_err + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);   // once per upload of the texture
+    if (e != hipSuccess) { *rc = hipfail(c, e, "BVH child-pair build"); return nullptr; }
+    t->pairs_gen = t->gen;
+    t->pairs_ok = bad == 0;
+    return t->pairs_ok ? t->pairs : nullptr;
+}
+
 int render_trace(pt_effect* fx, pt_texture* target)
 {
     pt_ctx* c = fx->ctx;
@@ -325,6 +357,10 @@ int render_trace(pt_effect* fx, pt_texture* target)
         a.aabb_texels = (long long)bvh->w * bvh->h;
         a.tri = (const float4*)tri->d;
         a.tri_texels = (long long)tri->w * tri->h;
+        int prc = PT_OK;
+        a.bvh_pairs = ensure_pairs(c, bvh, &prc);
+        if (prc) return prc;
+        c->bvh_used = a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
         a.albedo = tex8(sampler(fx, "tAlbedoTexture"));
         a.bump = tex8(sampler(fx, "tBumpTexture"));
         a.metal = tex8(sampler(fx, "tMetallicTexture"));
@@ -659,6 +695,7 @@ void pt_texture_destroy(pt_texture* t)
         for (auto& kv : fx->samplers)
             if (kv.second == t) kv.second = nullptr;
     if (t->d && !t->external) { hipStreamSynchronize(c->stream); hipFree(t->d); }
+    if (t->pairs) { hipStreamSynchronize(c->stream); hipFree(t->pairs); }
     c->textures.erase(t);
     delete t;
 }
@@ -696,6 +733,7 @@ int pt_write_pixels(pt_ctx* c, pt_texture* t, const void* src, size_t bytes)
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(t->d, src, bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    t->gen++;
     return PT_OK;
 }
 
@@ -714,6 +752,15 @@ int pt_set_backend(pt_ctx* c, int backend)
     c->backend = backend;
     return PT_OK;
 }
+
+int pt_set_bvh_layout(pt_ctx* c, int layout)
+{
+    if (!c || (layout != PT_BVH_REFERENCE && layout != PT_BVH_PAIRS)) return PT_ERR_ARG;
+    c->bvh_layout = layout;
+    return PT_OK;
+}
+
+int pt_bvh_layout_used(pt_ctx* c) { return c ? c->bvh_used : PT_ERR_ARG; }
 
 int pt_set_row_partition(pt_ctx* c, int num_parts, int part)
 {

@@ -18,8 +18,14 @@ enum { PROG_CORNELL = 3, PROG_GLTF = 4 };
 // PROG_GLTF_TEX: the glTF program instantiated with its PBR / normal-map code (models with an
 // albedo or bump texture); PROG_GLTF is the same program with those branches compiled out.
 enum { PROG_GLTF_TEX = 104 };
-template <int P> constexpr bool kIsGltf = P == PROG_GLTF || P == PROG_GLTF_TEX;
-template <int P> constexpr bool kHasTex = P == PROG_GLTF_TEX;
+// +PROG_PAIRS: the same programs walking the child-pair BVH records (bvhWalkPairs) instead of the
+// reference's texel pairs (bvhWalkRef); chosen per draw by the host (pt_capi.cpp ensure_pairs)
+enum { PROG_PAIRS = 1000 };
+template <int P> constexpr int kBase = P % PROG_PAIRS;
+template <int P> constexpr bool kIsGltf = kBase<P> == PROG_GLTF || kBase<P> == PROG_GLTF_TEX;
+template <int P> constexpr bool kHasTex = kBase<P> == PROG_GLTF_TEX;
+template <int P> constexpr bool kPairs = P >= PROG_PAIRS;
+constexpr bool kIsGltfRt(int p) { return p == PROG_GLTF || p == PROG_GLTF_TEX; }
 // waves per SIMD the register allocator must leave room for (128 VGPRs -> 4; the textured
 // variant keeps 2 rather than spill)
 template <int P> constexpr int kMinWaves = kHasTex<P> ? 2 : 4;
@@ -196,5 +202,132 @@ PT_D void texBilinear(const Tex8& t, float u, float v, float out[4])
 }
 
 PT_D f3 pow22(f3 c) { return mk(gpow(c.x, 2.2f), gpow(c.y, 2.2f), gpow(c.z, 2.2f)); }
+
+// ------------------------------------------------------------------------------ BVH walks
+// Both walks visit the nodes of js/GLTFModelPathTracing_FragmentShader.js:201-298 in the same
+// order, cull with the same comparisons and test the same leaves, so they return the same hit;
+// `nodes` counts the reference's node fetches (2 texels each) either way.
+//
+// The stack policy Stk provides get(level) / put(level, float2) for levels < kStackLevels.
+
+struct BvhResult {
+    float triID, triU, triV;
+    bool lookup;
+    unsigned nodes, leaves, ovf;
+};
+
+template <class Stk>
+PT_D void stackPush(const TraceArgs& a, Stk& st, int si, float2 e, unsigned& ovf)
+{
+    if (si < kStackLevels) st.put(si, e);
+    else { ovf++; atomicOr(a.err, (unsigned)E_STACK); }   // GLSL would write out of bounds
+}
+
+// The reference layout: a pushed entry is (node id, tNear); a pop re-fetches the node's two texels.
+// Entry: c0/c1 = the root's texels, curT = its box distance (already counted by the caller).
+template <class Stk>
+PT_D void bvhWalkRef(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float4 c0, float4 c1, float curT,
+                     float& hitT, Stk& st, BvhResult& r)
+{
+    float stackptr = 0.0f, curId = 0.0f;
+    bool skip = curT < hitT;
+    for (;;) {
+        if (!skip) {
+            stackptr = stackptr - 1.0f;
+            if (stackptr < 0.0f) break;
+            float2 e = st.get((int)stackptr);
+            curId = e.x; curT = e.y;
+            if (curT >= hitT) continue;
+            c0 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f);
+            c1 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f + 1.0f);
+            r.nodes++;
+        }
+        skip = false;
+        if (c0.x < 0.0f) {   // inner node: both children, near first
+            float idA = curId + 1.0f, idB = c1.x;
+            float4 a0 = fetch32(a.aabb, a.aabb_texels, idA * 2.0f), a1 = fetch32(a.aabb, a.aabb_texels, idA * 2.0f + 1.0f);
+            float4 b0 = fetch32(a.aabb, a.aabb_texels, idB * 2.0f), b1 = fetch32(a.aabb, a.aabb_texels, idB * 2.0f + 1.0f);
+            r.nodes += 2;
+            float tA = box(mk(a0.y, a0.z, a0.w), mk(a1.y, a1.z, a1.w), O, inv);
+            float tB = box(mk(b0.y, b0.z, b0.w), mk(b1.y, b1.z, b1.w), O, inv);
+            if (tB < tA) {
+                float ti = idB; idB = idA; idA = ti;
+                float tt = tB; tB = tA; tA = tt;
+                float4 x0 = b0; b0 = a0; a0 = x0;
+                float4 x1 = b1; b1 = a1; a1 = x1;
+            }
+            if (tB < hitT) { curId = idB; curT = tB; c0 = b0; c1 = b1; skip = true; }
+            if (tA < hitT) {
+                if (skip) {
+                    stackPush(a, st, (int)stackptr, make_float2(idB, tB), r.ovf);
+                    stackptr = stackptr + 1.0f;
+                }
+                curId = idA; curT = tA; c0 = a0; c1 = a1; skip = true;
+            }
+            continue;
+        }
+        // leaf: one triangle per leaf
+        float id = 8.0f * c0.x;
+        float4 t0 = fetch32(a.tri, a.tri_texels, id), t1 = fetch32(a.tri, a.tri_texels, id + 1.0f),
+               t2 = fetch32(a.tri, a.tri_texels, id + 2.0f);
+        r.leaves++;
+        float tu, tv;
+        float d = bvhTriangle(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
+        if (d < hitT) { hitT = d; r.triID = id; r.triU = tu; r.triV = tv; r.lookup = true; }
+    }
+}
+
+// Child-pair records (built by pt_bvh_pairs from the reference texture; only for trees whose
+// links are exact in-range integers, see pt_capi.cpp): record n = 64 contiguous bytes holding
+// the boxes of BOTH children of inner node n and their codes,
+//   r0 = A.min.xyz, A.max.x   r1 = A.max.yz, B.min.xy   r2 = B.min.z, B.max.xyz   r3 = codeA, codeB
+// with A = n+1, B = the node's right-child link, and code = id for an inner child, -1-idObject
+// for a leaf. An inner step is one 64-byte line instead of two 32-byte nodes in different lines,
+// and a pop needs no fetch: the stack entry (tNear, code) already says what the node is.
+template <class Stk>
+PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float rootHdr, float curT,
+                       float& hitT, Stk& st, BvhResult& r)
+{
+    const float4* R = a.bvh_pairs;
+    float code = rootHdr < 0.0f ? 0.0f : -1.0f - rootHdr;
+    int sp = 0;
+    bool skip = curT < hitT;
+    for (;;) {
+        if (!skip) {
+            sp--;
+            if (sp < 0) break;
+            float2 e = st.get(sp);
+            if (e.x >= hitT) continue;
+            code = e.y;
+            r.nodes++;
+        }
+        skip = false;
+        if (code >= 0.0f) {
+            const float4* rec = R + 4u * (unsigned)code;
+            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+            r.nodes += 2;
+            float tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
+            float tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+            float cA = r3.x, cB = r3.y;
+            if (tB < tA) {
+                float tt = tB; tB = tA; tA = tt;
+                float tc = cB; cB = cA; cA = tc;
+            }
+            if (tB < hitT) { code = cB; skip = true; }
+            if (tA < hitT) {
+                if (skip) { stackPush(a, st, sp, make_float2(tB, cB), r.ovf); sp++; }
+                code = cA; skip = true;
+            }
+            continue;
+        }
+        float id = 8.0f * (-1.0f - code);
+        float4 t0 = fetch32(a.tri, a.tri_texels, id), t1 = fetch32(a.tri, a.tri_texels, id + 1.0f),
+               t2 = fetch32(a.tri, a.tri_texels, id + 2.0f);
+        r.leaves++;
+        float tu, tv;
+        float d = bvhTriangle(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
+        if (d < hitT) { hitT = d; r.triID = id; r.triU = tu; r.triV = tv; r.lookup = true; }
+    }
+}
 
 } // namespace pt

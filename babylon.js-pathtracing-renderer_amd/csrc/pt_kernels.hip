@@ -43,6 +43,30 @@ struct Cnt {
     unsigned seg, node, leaf, hit, tap, ovf;
 };
 
+// BVH stack levels: the first kStackLds per lane in LDS at [level][lane] (conflict-free), deeper
+// ones in a private array
+typedef float vf2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) vf2 lds_float2;
+typedef __attribute__((address_space(5))) vf2 prv_float2;
+struct MegaStack {
+    lds_float2* lds;
+    unsigned slot;
+    prv_float2* deep;
+    PT_D float2 get(int si) const
+    {
+        vf2 e;
+        if (si < kStackLds) e = lds[si * kBlock + slot];
+        else e = deep[si - kStackLds];
+        return make_float2(e.x, e.y);
+    }
+    PT_D void put(int si, float2 e)
+    {
+        const vf2 v = { e.x, e.y };
+        if (si < kStackLds) lds[si * kBlock + slot] = v;
+        else deep[si - kStackLds] = v;
+    }
+};
+
 // SceneIntersect: js/BabylonPathTracing_FragmentShader.js:47-112 (Cornell) and
 // js/GLTFModelPathTracing_FragmentShader.js:116-346 (glTF, with the BVH walk). The object loops
 // stay rolled (#pragma unroll 1): each iteration re-reads its sphere / triangle from the kernarg
@@ -81,67 +105,19 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     }
     if (!kIsGltf<PROG>) return;
 
-    // ---- BVH walk over the BVH_Fast_Builder texture layout (js/GLTFModelPathTracing_FragmentShader.js:201-298)
+    // ---- BVH walk (js/GLTFModelPathTracing_FragmentShader.js:201-298), pt_device.h
     f3 O = mul(a.model, rayO, 1.0f), D = mul(a.model, rayD, 0.0f);
     f3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
     const bool dbl = (!a.uses_albedo && a.model_mat == TRANSPARENT);
-    float stackptr = 0.0f;
     float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
-    if (COUNT) cnt.node++;
-    float curId = 0.0f;
-    float curT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
-    lds[lane_slot] = make_float2(curId, curT);   // stackLevels[0] = root
-    bool skip = curT < h.t;
-    float triID = 0.0f, triU = 0.0f, triV = 0.0f;
-    bool lookup = false;
-    for (;;) {
-        if (!skip) {
-            stackptr = stackptr - 1.0f;
-            if (stackptr < 0.0f) break;
-            int si = (int)stackptr;
-            float2 e = si < kStackLds ? lds[si * kBlock + lane_slot] : deep[si - kStackLds];
-            curId = e.x; curT = e.y;
-            if (curT >= h.t) continue;
-            c0 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f);
-            c1 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f + 1.0f);
-            if (COUNT) cnt.node++;
-        }
-        skip = false;
-        if (c0.x < 0.0f) {   // inner node: both children, near first
-            float idA = curId + 1.0f, idB = c1.x;
-            float4 a0 = fetch32(a.aabb, a.aabb_texels, idA * 2.0f), a1 = fetch32(a.aabb, a.aabb_texels, idA * 2.0f + 1.0f);
-            float4 b0 = fetch32(a.aabb, a.aabb_texels, idB * 2.0f), b1 = fetch32(a.aabb, a.aabb_texels, idB * 2.0f + 1.0f);
-            if (COUNT) cnt.node += 2;
-            float tA = box(mk(a0.y, a0.z, a0.w), mk(a1.y, a1.z, a1.w), O, inv);
-            float tB = box(mk(b0.y, b0.z, b0.w), mk(b1.y, b1.z, b1.w), O, inv);
-            if (tB < tA) {
-                float ti = idB; idB = idA; idA = ti;
-                float tt = tB; tB = tA; tA = tt;
-                float4 x0 = b0; b0 = a0; a0 = x0;
-                float4 x1 = b1; b1 = a1; a1 = x1;
-            }
-            if (tB < h.t) { curId = idB; curT = tB; c0 = b0; c1 = b1; skip = true; }
-            if (tA < h.t) {
-                if (skip) {
-                    int si = (int)stackptr;
-                    if (si < kStackLds) lds[si * kBlock + lane_slot] = make_float2(idB, tB);
-                    else if (si < kStackLevels) deep[si - kStackLds] = make_float2(idB, tB);
-                    else { if (COUNT) cnt.ovf++; atomicOr(a.err, (unsigned)E_STACK); }
-                    stackptr = stackptr + 1.0f;
-                }
-                curId = idA; curT = tA; c0 = a0; c1 = a1; skip = true;
-            }
-            continue;
-        }
-        // leaf: one triangle per leaf
-        float id = 8.0f * c0.x;
-        float4 t0 = fetch32(a.tri, a.tri_texels, id), t1 = fetch32(a.tri, a.tri_texels, id + 1.0f),
-               t2 = fetch32(a.tri, a.tri_texels, id + 2.0f);
-        if (COUNT) cnt.leaf++;
-        float tu, tv;
-        float d = bvhTriangle(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
-        if (d < h.t) { h.t = d; triID = id; triU = tu; triV = tv; lookup = true; }
-    }
+    float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
+    BvhResult br = { 0.0f, 0.0f, 0.0f, false, 1u, 0u, 0u };
+    MegaStack st{ (lds_float2*)lds, lane_slot, (prv_float2*)deep };
+    if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, c0.x, rootT, h.t, st, br);
+    else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, h.t, st, br);
+    if (COUNT) { cnt.node += br.nodes; cnt.leaf += br.leaves; cnt.ovf += br.ovf; }
+    const bool lookup = br.lookup;
+    const float triID = br.triID, triU = br.triU, triV = br.triV;
     if (lookup) {
         float4 v2 = fetch32(a.tri, a.tri_texels, triID + 2.0f), v3 = fetch32(a.tri, a.tri_texels, triID + 3.0f),
                v4 = fetch32(a.tri, a.tri_texels, triID + 4.0f), v5 = fetch32(a.tri, a.tri_texels, triID + 5.0f);
@@ -405,6 +381,10 @@ template __global__ void pt_trace<PROG_GLTF, false>(TraceArgs);
 template __global__ void pt_trace<PROG_GLTF, true>(TraceArgs);
 template __global__ void pt_trace<PROG_GLTF_TEX, false>(TraceArgs);
 template __global__ void pt_trace<PROG_GLTF_TEX, true>(TraceArgs);
+template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF, false>(TraceArgs);
+template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF, true>(TraceArgs);
+template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF_TEX, false>(TraceArgs);
+template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF_TEX, true>(TraceArgs);
 
 // ------------------------------------------------------------------------------ screenCopy
 __global__ __launch_bounds__(256) void pt_copy(CopyArgs a)
@@ -479,6 +459,39 @@ __global__ __launch_bounds__(256) void pt_output(OutputArgs a)
         a.out_f[i] = make_float4(o[0], o[1], o[2], 1.0f);
 }
 
+// ------------------------------------------------------------------------------ child-pair BVH records
+// Record n of bvhWalkPairs (pt_device.h) from the reference texture, read with the same fetch32 /
+// float index arithmetic the reference walk uses, so every box and code equals what that walk
+// would fetch. `bad` collects the nodes that break the records' preconditions: an inner node's
+// right-child link that is not an exact integer in [0, nrec), or a leaf idObject that is not an
+// exact integer in [0, 2^24) (codes must round-trip through -1-x). The host then keeps the
+// reference walk for that texture.
+__global__ __launch_bounds__(256) void pt_bvh_pairs(const float4* aabb, long long texels, float4* rec, unsigned nrec,
+                                                    unsigned* bad)
+{
+    const unsigned n = blockIdx.x * 256u + threadIdx.x;
+    if (n >= nrec) return;
+    const float fn = (float)n;   // exact: nrec <= 2^23
+    const float4 c0 = fetch32(aabb, texels, fn * 2.0f), c1 = fetch32(aabb, texels, fn * 2.0f + 1.0f);
+    bool ok;
+    float4 r0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), r1 = r0, r2 = r0, r3 = r0;
+    if (c0.x < 0.0f) {
+        const float idA = fn + 1.0f, idB = c1.x;
+        const float4 a0 = fetch32(aabb, texels, idA * 2.0f), a1 = fetch32(aabb, texels, idA * 2.0f + 1.0f);
+        const float4 b0 = fetch32(aabb, texels, idB * 2.0f), b1 = fetch32(aabb, texels, idB * 2.0f + 1.0f);
+        ok = idB >= 0.0f && idB < (float)nrec && floorf(idB) == idB;
+        r0 = make_float4(a0.y, a0.z, a0.w, a1.y);
+        r1 = make_float4(a1.z, a1.w, b0.y, b0.z);
+        r2 = make_float4(b0.w, b1.y, b1.z, b1.w);
+        r3 = make_float4(a0.x < 0.0f ? idA : -1.0f - a0.x, b0.x < 0.0f ? idB : -1.0f - b0.x, 0.0f, 0.0f);
+    } else {
+        ok = floorf(c0.x) == c0.x && c0.x < 16777216.0f;   // NaN and inf fail
+    }
+    float4* o = rec + 4ull * n;
+    o[0] = r0; o[1] = r1; o[2] = r2; o[3] = r3;
+    if (!ok) atomicOr(bad, 1u);
+}
+
 // ------------------------------------------------------------------------------ self-test
 __global__ void pt_math_probe_kernel(int op, const float* x, const float* y, float* out, int n)
 {
@@ -516,6 +529,7 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
     dim3 grid(grid_x, grid_y), block(pt::kBlock);
     // texture-free glTF models (the bench's StanfordBunny) take the variant without PBR code
     if (prog == pt::PROG_GLTF && (a->uses_albedo || a->uses_bump)) prog = pt::PROG_GLTF_TEX;
+    if (pt::kIsGltfRt(prog) && a->bvh_pairs) prog += pt::PROG_PAIRS;
 #define PT_LAUNCH(P)                                                                              \
     do {                                                                                          \
         if (count) hipLaunchKernelGGL((pt::pt_trace<P, true>), grid, block, 0, s, *a);             \
@@ -525,9 +539,18 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
     case pt::PROG_CORNELL: PT_LAUNCH(pt::PROG_CORNELL); break;
     case pt::PROG_GLTF: PT_LAUNCH(pt::PROG_GLTF); break;
     case pt::PROG_GLTF_TEX: PT_LAUNCH(pt::PROG_GLTF_TEX); break;
+    case pt::PROG_PAIRS + pt::PROG_GLTF: PT_LAUNCH(pt::PROG_PAIRS + pt::PROG_GLTF); break;
+    case pt::PROG_PAIRS + pt::PROG_GLTF_TEX: PT_LAUNCH(pt::PROG_PAIRS + pt::PROG_GLTF_TEX); break;
     default: return hipErrorInvalidValue;
     }
 #undef PT_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_bvh_pairs(const float4* aabb, long long texels, float4* rec, unsigned nrec, unsigned* bad,
+                               hipStream_t s)
+{
+    hipLaunchKernelGGL(pt::pt_bvh_pairs, dim3((nrec + 255) / 256), dim3(256), 0, s, aabb, texels, rec, nrec, bad);
     return hipGetLastError();
 }
 

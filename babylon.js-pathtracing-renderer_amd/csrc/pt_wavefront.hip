@@ -200,6 +200,30 @@ __global__ __launch_bounds__(kBlock) void wf_extend(TraceArgs a, WfBufs w, int b
 }
 
 // ============================================================================ BVH walk
+// stack levels >= kStackLds live in a global slab indexed [level][persistent lane]
+typedef float vf2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) vf2 lds_float2;
+typedef __attribute__((address_space(1))) vf2 glb_float2;
+struct WfStack {
+    lds_float2* lds;
+    unsigned slot;
+    glb_float2* deep;
+    size_t dstride;
+    PT_D float2 get(int si) const
+    {
+        vf2 e;
+        if (si < kStackLds) e = lds[si * kBlock + slot];
+        else e = deep[(si - kStackLds) * dstride];
+        return make_float2(e.x, e.y);
+    }
+    PT_D void put(int si, float2 e)
+    {
+        const vf2 v = { e.x, e.y };
+        if (si < kStackLds) lds[si * kBlock + slot] = v;
+        else deep[(si - kStackLds) * dstride] = v;
+    }
+};
+
 template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b)
 {
@@ -223,63 +247,16 @@ __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b
         f3 O = mul(a.model, ro, 1.0f), D = mul(a.model, rd, 0.0f);
         f3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
         const bool dbl = (!a.uses_albedo && a.model_mat == TRANSPARENT);
-        unsigned nodes = 0, leaves = 0, ovf = 0;
         // the root was fetched and tested by wf_extend (and counted there); its box is hit
         float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
-        float curId = 0.0f;
-        float curT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
-        lds[tid] = make_float2(curId, curT);
-        float stackptr = 0.0f;
-        bool skip = curT < hitT;
-        float triID = 0.0f, triU = 0.0f, triV = 0.0f;
-        bool lookup = false;
-        for (;;) {
-            if (!skip) {
-                stackptr = stackptr - 1.0f;
-                if (stackptr < 0.0f) break;
-                int si = (int)stackptr;
-                float2 e = si < kStackLds ? lds[si * kBlock + tid] : deep[(si - kStackLds) * dstride];
-                curId = e.x; curT = e.y;
-                if (curT >= hitT) continue;
-                c0 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f);
-                c1 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f + 1.0f);
-                nodes++;
-            }
-            skip = false;
-            if (c0.x < 0.0f) {
-                float idA = curId + 1.0f, idB = c1.x;
-                float4 a0 = fetch32(a.aabb, a.aabb_texels, idA * 2.0f), a1 = fetch32(a.aabb, a.aabb_texels, idA * 2.0f + 1.0f);
-                float4 b0 = fetch32(a.aabb, a.aabb_texels, idB * 2.0f), b1 = fetch32(a.aabb, a.aabb_texels, idB * 2.0f + 1.0f);
-                nodes += 2;
-                float tA = box(mk(a0.y, a0.z, a0.w), mk(a1.y, a1.z, a1.w), O, inv);
-                float tB = box(mk(b0.y, b0.z, b0.w), mk(b1.y, b1.z, b1.w), O, inv);
-                if (tB < tA) {
-                    float ti = idB; idB = idA; idA = ti;
-                    float tt = tB; tB = tA; tA = tt;
-                    float4 x0 = b0; b0 = a0; a0 = x0;
-                    float4 x1 = b1; b1 = a1; a1 = x1;
-                }
-                if (tB < hitT) { curId = idB; curT = tB; c0 = b0; c1 = b1; skip = true; }
-                if (tA < hitT) {
-                    if (skip) {
-                        int si = (int)stackptr;
-                        if (si < kStackLds) lds[si * kBlock + tid] = make_float2(idB, tB);
-                        else if (si < kStackLevels) deep[(si - kStackLds) * dstride] = make_float2(idB, tB);
-                        else { ovf++; atomicOr(a.err, (unsigned)E_STACK); }
-                        stackptr = stackptr + 1.0f;
-                    }
-                    curId = idA; curT = tA; c0 = a0; c1 = a1; skip = true;
-                }
-                continue;
-            }
-            float id = 8.0f * c0.x;
-            float4 t0 = fetch32(a.tri, a.tri_texels, id), t1 = fetch32(a.tri, a.tri_texels, id + 1.0f),
-                   t2 = fetch32(a.tri, a.tri_texels, id + 2.0f);
-            leaves++;
-            float tu, tv;
-            float d = bvhTriangle(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
-            if (d < hitT) { hitT = d; triID = id; triU = tu; triV = tv; lookup = true; }
-        }
+        float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
+        BvhResult br = { 0.0f, 0.0f, 0.0f, false, 0u, 0u, 0u };
+        WfStack st{ (lds_float2*)lds, tid, (glb_float2*)deep, dstride };
+        if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, c0.x, rootT, hitT, st, br);
+        else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, hitT, st, br);
+        const unsigned nodes = br.nodes, leaves = br.leaves, ovf = br.ovf;
+        const bool lookup = br.lookup;
+        const float triID = br.triID, triU = br.triU, triV = br.triV;
         unsigned taps = 0;
         if (lookup) {
             float4 v2 = fetch32(a.tri, a.tri_texels, triID + 2.0f), v3 = fetch32(a.tri, a.tri_texels, triID + 3.0f),
@@ -550,6 +527,7 @@ extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceAr
 {
     using namespace pt;
     if (prog == PROG_GLTF && (a->uses_albedo || a->uses_bump)) prog = PROG_GLTF_TEX;
+    if (kIsGltfRt(prog) && a->bvh_pairs) prog += PROG_PAIRS;
     dim3 tiles(tiles_x, bands), blk(kBlock);
     if (count) hipLaunchKernelGGL((wf_raygen<true>), tiles, blk, 0, s, *a, *w);
     else hipLaunchKernelGGL((wf_raygen<false>), tiles, blk, 0, s, *a, *w);
@@ -564,6 +542,8 @@ extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceAr
         case PROG_CORNELL: WF_BOUNCE(PROG_CORNELL, true) break;
         case PROG_GLTF: WF_BOUNCE(PROG_GLTF, true) break;
         case PROG_GLTF_TEX: WF_BOUNCE(PROG_GLTF_TEX, true) break;
+        case PROG_PAIRS + PROG_GLTF: WF_BOUNCE(PROG_PAIRS + PROG_GLTF, true) break;
+        case PROG_PAIRS + PROG_GLTF_TEX: WF_BOUNCE(PROG_PAIRS + PROG_GLTF_TEX, true) break;
         default: return hipErrorInvalidValue;
         }
     } else {
@@ -571,6 +551,8 @@ extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceAr
         case PROG_CORNELL: WF_BOUNCE(PROG_CORNELL, false) break;
         case PROG_GLTF: WF_BOUNCE(PROG_GLTF, false) break;
         case PROG_GLTF_TEX: WF_BOUNCE(PROG_GLTF_TEX, false) break;
+        case PROG_PAIRS + PROG_GLTF: WF_BOUNCE(PROG_PAIRS + PROG_GLTF, false) break;
+        case PROG_PAIRS + PROG_GLTF_TEX: WF_BOUNCE(PROG_PAIRS + PROG_GLTF_TEX, false) break;
         default: return hipErrorInvalidValue;
         }
     }

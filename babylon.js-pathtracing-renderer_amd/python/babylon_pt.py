@@ -38,7 +38,7 @@ SYMBOLS = [
     "pt_texture_create_rgba32f", "pt_texture_create_rgba8", "pt_render_target_create", "pt_render_target_wrap",
     "pt_render_target_resize", "pt_texture_size", "pt_texture_destroy",
     "pt_render", "pt_read_pixels", "pt_write_pixels",
-    "pt_set_row_partition", "pt_set_backend", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
+    "pt_set_row_partition", "pt_set_backend", "pt_set_bvh_layout", "pt_bvh_layout_used", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
     "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_version",
 ]
 
@@ -73,6 +73,7 @@ def lib():
         "pt_write_pixels": ([vp, vp, vp, ctypes.c_size_t], i32),
         "pt_set_row_partition": ([vp, i32, i32], i32), "pt_texture_device_ptr": ([vp], vp),
         "pt_set_backend": ([vp, i32], i32), "pt_set_stream": ([vp, vp], i32),
+        "pt_set_bvh_layout": ([vp, i32], i32), "pt_bvh_layout_used": ([vp], i32),
         "pt_last_render_ms": ([vp, i32, f32p], i32), "pt_set_counting": ([vp, i32], i32),
         "pt_timing_begin": ([vp], i32),
         "pt_timing_end": ([vp, i32, ctypes.POINTER(ctypes.c_double), ip], i32),
@@ -134,8 +135,20 @@ class Engine:
         self.check(lib().pt_set_stream(self.ctx, ctypes.c_void_p(hip_stream) if hip_stream else None), "pt_set_stream")
 
     def set_backend(self, backend):
-        """'wavefront' (default) or 'megakernel': same bits, different schedule."""
+        """'megakernel' (default) or 'wavefront': same bits, different schedule."""
         self.check(lib().pt_set_backend(self.ctx, {"megakernel": 0, "wavefront": 1}[backend]), "pt_set_backend")
+
+    BVH_LAYOUTS = {"reference": 0, "pairs": 1}
+
+    def set_bvh_layout(self, layout):
+        """'pairs' (default: child-pair records, falls back to the reference walk for malformed
+        trees) or 'reference' (walk the reference texel pairs): same bits, different memory path."""
+        self.check(lib().pt_set_bvh_layout(self.ctx, self.BVH_LAYOUTS[layout]), "pt_set_bvh_layout")
+
+    def bvh_layout_used(self):
+        """Layout walked by the last glTF draw: 'pairs', 'reference' or None."""
+        v = lib().pt_bvh_layout_used(self.ctx)
+        return {0: "reference", 1: "pairs"}.get(v)
 
     def last_render_ms(self, program):
         ms = ctypes.c_float(0)

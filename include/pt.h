@@ -124,11 +124,19 @@ int pt_write_pixels(pt_ctx* ctx, pt_texture* tex, const void* src, size_t bytes)
  * 16-row bands b with b % num_parts == part (bands are whole 2x2 quads, so derivatives are
  * unchanged). screenOutput/copy stay full-frame. num_parts = 1 restores full frames. */
 int pt_set_row_partition(pt_ctx* ctx, int num_parts, int part);
-/* Path-tracing backend of this context: PT_BACKEND_WAVEFRONT (default: per-segment kernels over
- * compacted path queues) or PT_BACKEND_MEGAKERNEL (one kernel, one lane per path). Results are
+/* Path-tracing backend of this context: PT_BACKEND_MEGAKERNEL (default: one kernel, one lane per
+ * path) or PT_BACKEND_WAVEFRONT (per-segment kernels over compacted path queues). Results are
  * bit-identical; the choice only changes speed. */
 enum pt_backend { PT_BACKEND_MEGAKERNEL = 0, PT_BACKEND_WAVEFRONT = 1 };
 int pt_set_backend(pt_ctx* ctx, int backend);
+/* BVH walk of the glTF program. PT_BVH_PAIRS (default) re-packs tAABBTexture once per upload into
+ * 64-byte child-pair records (both children's boxes in one line, pops without a fetch) and walks
+ * those; a texture whose links are not exact in-range integers keeps PT_BVH_REFERENCE, the walk
+ * over the reference's own texel pairs. Same nodes, same order, same results either way.
+ * pt_bvh_layout_used reports what the last glTF draw of the context walked (-1: none yet). */
+enum pt_bvh_layout { PT_BVH_REFERENCE = 0, PT_BVH_PAIRS = 1 };
+int pt_set_bvh_layout(pt_ctx* ctx, int layout);
+int pt_bvh_layout_used(pt_ctx* ctx);
 /* Enqueue this context's work on a caller-owned HIP stream (e.g. torch.cuda.current_stream(), so
  * that draws and RCCL collectives are ordered without host syncs); NULL restores the context's own
  * stream. The caller keeps the stream alive while the context uses it. */

@@ -42,11 +42,11 @@ def output_call(frame):
     return next(c for c in frame if c["shader"] == "screenOutputFragmentShader")
 
 
-def oracle_scene(meta, width=None, height=None):
+def oracle_scene(meta, width=None, height=None, mesh_arrays=None):
     import ptoracle as po
     w, h = width or meta["width"], height or meta["height"]
     if meta["scene"] == "gltf":
-        m = mesh(meta)
+        m = mesh_arrays if mesh_arrays is not None else mesh(meta)
         return po.Scene("gltf", w, h, bluenoise(), m["bvh"], m["tri"])
     return po.Scene(meta["scene"], w, h, bluenoise())
 
@@ -61,11 +61,11 @@ def with_resolution(uniforms, w, h):
     return u
 
 
-def oracle_replay(meta, frames=None, width=None, height=None, nthreads=0, with_output=False):
+def oracle_replay(meta, frames=None, width=None, height=None, nthreads=0, with_output=False, mesh=None):
     """Run the oracle over the recorded stream: returns accumulation after each frame (+ canvas)."""
     import ptoracle as po
     w, h = width or meta["width"], height or meta["height"]
-    sc = oracle_scene(meta, w, h)
+    sc = oracle_scene(meta, w, h, mesh)
     acc = np.zeros((h, w, 4), np.float32)
     accs, canvases, counters = [], [], []
     for f in meta["frames"][:frames]:

@@ -104,14 +104,17 @@ def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1):
     return accs, canvases, player
 
 
-BACKENDS = ["wavefront", "megakernel"]
+# (schedule, BVH layout): every combination must give the same bits
+BACKENDS = [("megakernel", "pairs"), ("megakernel", "reference"), ("wavefront", "pairs"), ("wavefront", "reference")]
 
 
-@pytest.fixture(params=BACKENDS)
+@pytest.fixture(params=BACKENDS, ids=["-".join(b) for b in BACKENDS])
 def backend(request, engine):
-    engine.set_backend(request.param)
+    engine.set_backend(request.param[0])
+    engine.set_bvh_layout(request.param[1])
     yield request.param
-    engine.set_backend("wavefront")
+    engine.set_backend("megakernel")
+    engine.set_bvh_layout("pairs")
 
 
 @pytest.mark.parametrize("name,frames", [
@@ -125,6 +128,8 @@ def test_stream_bitexact(engine, backend, name, frames):
     meta = H.stream(name)
     ref_acc, ref_can, _ = H.oracle_replay(meta, frames, with_output=True)
     got_acc, got_can, _ = _replay_gpu(engine, meta, frames)
+    if meta["scene"] == "gltf":
+        assert engine.bvh_layout_used() == backend[1]
     for i, (ra, ga, rc, gc) in enumerate(zip(ref_acc, got_acc, ref_can, got_can)):
         assert _bits_equal(ra, ga), "%s frame %d accumulation: %s" % (name, i, _diff_report(ra, ga))
         assert _bits_equal(rc, gc), "%s frame %d canvas: %s" % (name, i, _diff_report(rc, gc))
@@ -181,6 +186,35 @@ def test_in_place_history(engine, backend):
         player.play_call(call)
     engine.sync()
     assert _bits_equal(ref_acc[2], rt.read())
+
+
+@pytest.mark.parametrize("backend_name", ["megakernel", "wavefront"])
+def test_malformed_bvh_links_fall_back_exactly(engine, backend_name):
+    """A tree whose right-child links are not exact integers (legal input: the GLSL just fetches
+    whatever texel the float index lands on) cannot be re-packed; the draw must fall back to the
+    reference-layout walk and still match the oracle bit for bit."""
+    import babylon_pt as bp
+    meta = H.stream("gltf_teapot_320x180")
+    mesh = H.mesh(meta)
+    bvh = mesh["bvh"].copy()                    # (nodes, 8): texel pair per node
+    inner = np.nonzero(bvh[:, 0] < 0)[0]
+    bvh[inner[3], 4] += 0.5                     # node's right-child link -> between two texels
+    bvh[inner[7], 4] = -3.0                     # ... and one pointing before the texture
+    bad = dict(mesh, bvh=bvh)
+    engine.set_backend(backend_name)
+    try:
+        ref_acc, _, _ = H.oracle_replay(meta, 2, mesh=bad)
+        player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, bad))
+        got = []
+        for i in range(2):
+            player.play_frame(i)
+            engine.sync()
+            got.append(player.textures["pathTracingRenderTarget"].read())
+        assert engine.bvh_layout_used() == "reference"
+    finally:
+        engine.set_backend("megakernel")
+    for ra, ga in zip(ref_acc, got):
+        assert _bits_equal(ra, ga), _diff_report(ra, ga)
 
 
 def test_errors_are_codes_not_crashes(engine):

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Timing experiments on the bench workload: device ms per path-trace launch for each backend, with
+the mesh in place and with the mesh moved out of view (root box test only), to split the frame cost
+into BVH walk vs everything else. Prints one JSON object per variant."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "babylon.js-pathtracing-renderer_amd", "python"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import babylon_pt as bp  # noqa: E402
+import helpers as H      # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--stream", default="gltf_bunny_1080p")
+ap.add_argument("--frames", type=int, default=20)
+ap.add_argument("--backends", default="megakernel,wavefront")
+ap.add_argument("--layouts", default="pairs,reference")
+a = ap.parse_args()
+meta = H.stream(a.stream)
+e = bp.Engine(0)
+mesh = H.texture_payloads(meta, H.mesh(meta)) if meta["scene"] == "gltf" else None
+p = bp.StreamPlayer(e, meta, H.bluenoise(), mesh)
+prog = meta["scene"]
+import itertools  # noqa: E402
+for backend, layout in itertools.product(a.backends.split(","), a.layouts.split(",")):
+    e.set_backend(backend)
+    e.set_bvh_layout(layout)
+    for variant in ("mesh", "no_mesh"):
+        over = None
+        if variant == "no_mesh":
+            call0 = [c for c in p.meta["frames"][-1] if c["effect"] == "pathTracingEffectWrapper"][0]
+            m = list(call0["uniforms"]["uGLTF_Model_InvMatrix"][1])
+            m[12] += 1.0e4
+            over = {"uGLTF_Model_InvMatrix": ["f", m]}
+        for k in range(3):
+            for call in p.synth_frame(k):
+                p.play_call(call, over if call["effect"] == "pathTracingEffectWrapper" else None)
+        e.sync()
+        e.timing_begin()
+        for k in range(a.frames):
+            for call in p.synth_frame(3 + k):
+                p.play_call(call, over if call["effect"] == "pathTracingEffectWrapper" else None)
+        ms, n = e.timing_end(prog)
+        print(json.dumps({"backend": backend, "layout": layout, "used": e.bvh_layout_used(), "variant": variant, "ms_per_launch": ms / max(n, 1), "n": n}), flush=True)
