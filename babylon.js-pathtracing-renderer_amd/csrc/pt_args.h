@@ -11,7 +11,7 @@ namespace pt {
 constexpr int kBlock = 256;          // 4 waves; a block shades a 16x16 pixel tile
 constexpr int kTile = 16;            // tile edge == row-band height used for sharding
 constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing_FragmentShader.js:95
-constexpr int kStackLds = 12;        // levels kept in LDS per lane; deeper levels go to scratch
+constexpr int kStackLds = 12;        // levels kept in LDS per lane; deeper levels go to a global slab
 
 enum Counter { C_PATHS, C_SEGMENTS, C_NODE, C_LEAF, C_HIT, C_RGBA8, C_OVERFLOW, C_NUM };
 enum ErrBits { E_STACK = 1u };
@@ -69,7 +69,11 @@ struct TraceArgs {
     long long aabb_texels;
     const float4* tri;
     long long tri_texels;
-    const float4* bvh_pairs;   // child-pair records of tAABBTexture (PROG_PAIRS variants only)
+    const float4* bvh_pairs;   // child-pair inner records of tAABBTexture (PROG_PAIRS variants only)
+    const float4* bvh_leaves;  // ... and its leaf records
+    float bvh_root_code;       // code of node 0
+    float2* spill;             // megakernel BVH stack levels >= kStackLds: [level][grid lane]
+    unsigned long long spill_stride;
     Tex8 albedo, bump, metal, emissive;
     // diagnostics
     unsigned long long* counters;   // C_NUM entries, only with counting builds

@@ -12,7 +12,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <set>
@@ -27,8 +29,12 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
-hipError_t pt_launch_bvh_pairs(const float4* aabb, long long texels, float4* rec, unsigned nrec, unsigned* bad,
-                               hipStream_t s);
+hipError_t pt_launch_persist(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x,
+                             unsigned n_wave_tiles, unsigned per_wave, unsigned refill, hipStream_t s);
+hipError_t pt_launch_finish(const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x, int bands, hipStream_t s);
+hipError_t pt_launch_pairs_pass(int pass, const float4* aabb, long long texels, const float4* tri, long long tri_texels,
+                                unsigned nrec, unsigned char* inner, unsigned char* leafref, unsigned* counts,
+                                float* code, float4* inner_rec, float4* leaf_rec, unsigned* bad, hipStream_t s);
 hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x, int bands,
                                int persist_blocks, hipStream_t s);
 }
@@ -58,9 +64,14 @@ struct pt_texture {
     int invert_y = 0;
     bool external = false;   // caller-owned device memory (pt_render_target_wrap)
     unsigned long long gen = 0;   // bumped by every host write of the texels
-    // child-pair BVH records derived from this texture (pt_bvh_pairs), valid for pairs_gen
-    float4* pairs = nullptr;
-    unsigned long long pairs_gen = ~0ull;
+    // child-pair BVH records derived from this texture and the triangle texture drawn with it
+    // (pt_pairs_* passes), valid while both keep the generations they were built from
+    void* pairs_mem = nullptr;
+    const float4* pairs_inner = nullptr;
+    const float4* pairs_leaf = nullptr;
+    float pairs_root = 0.0f;
+    const pt_texture* pairs_tri = nullptr;
+    unsigned long long pairs_gen = ~0ull, pairs_tri_gen = ~0ull;
     bool pairs_ok = false;
 };
 
@@ -89,6 +100,13 @@ struct pt_ctx {
     pt::WfBufs wf = {};
     void* wf_mem = nullptr;
     size_t wf_pixels = 0, wf_slots = 0, wf_spill = 0;
+    float2* mk_spill = nullptr;   // megakernel BVH stack spill slab
+    size_t mk_spill_lanes = 0;
+    pt::WfBufs gb = {};           // persistent backend: per-pixel G-buffer + radiance
+    void* gb_mem = nullptr;
+    size_t gb_pixels = 0;
+    unsigned persist_tiles = 4;   // 8x8 wave tiles per wave (PT_PERSIST_TILES)
+    unsigned persist_refill = 16; // finished lanes that trigger a refill (PT_PERSIST_REFILL)
     hipEvent_t ev0[kProgSlots] = {}, ev1[kProgSlots] = {};
     bool ev_used[kProgSlots] = {};
     // timing window: per draw event pairs, reused across windows
@@ -291,27 +309,95 @@ int wf_reserve(pt_ctx* c, int wq, int hq, int tiles, int blocks)
     return PT_OK;
 }
 
-// The child-pair records of a BVH texture, rebuilt when its texels changed since the last build.
-// Only for data textures (their texels change only through this API) of at most 2^24 texels (node
-// ids exact in float). Returns the records, or nullptr when the reference walk must be used.
-const float4* ensure_pairs(pt_ctx* c, pt_texture* t, int* rc)
+int spill_reserve(pt_ctx* c, size_t lanes)
+{
+    if (lanes <= c->mk_spill_lanes) return PT_OK;
+    if (c->mk_spill) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->mk_spill)); c->mk_spill = nullptr; }
+    c->mk_spill_lanes = 0;
+    HIPCHK(c, hipMalloc(&c->mk_spill, lanes * (pt::kStackLevels - pt::kStackLds) * sizeof(float2)));
+    c->mk_spill_lanes = lanes;
+    return PT_OK;
+}
+
+int gb_reserve(pt_ctx* c, int wq, int hq)
+{
+    const size_t pixels = (size_t)wq * hq;
+    if (pixels > c->gb_pixels) {
+        if (c->gb_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->gb_mem)); c->gb_mem = nullptr; }
+        c->gb_pixels = 0;
+        const size_t f4p = ((pixels * sizeof(float4)) + 255) & ~(size_t)255;
+        HIPCHK(c, hipMalloc(&c->gb_mem, 3 * f4p));
+        c->gb.gb0 = (float4*)c->gb_mem;
+        c->gb.gb1 = (float4*)((char*)c->gb_mem + f4p);
+        c->gb.rad = (float4*)((char*)c->gb_mem + 2 * f4p);
+        c->gb_pixels = pixels;
+    }
+    c->gb.wq = wq; c->gb.hq = hq;
+    return PT_OK;
+}
+
+// The child-pair records of a BVH texture (with the triangle texture drawn alongside), rebuilt
+// when either texture's texels changed since the last build. Only for data textures (their
+// texels change only through this API) of at most 2^24 texels (node ids and ranks exact in
+// float). Returns false when the reference walk must be used. One host round trip per build.
+bool ensure_pairs(pt_ctx* c, pt_texture* t, const pt_texture* tri, int* rc)
 {
     *rc = PT_OK;
     const long long texels = (long long)t->w * t->h;
-    if (c->bvh_layout != PT_BVH_PAIRS || t->kind != TEX_F32 || texels > (1ll << 24)) return nullptr;
-    if (t->pairs_gen == t->gen) return t->pairs_ok ? t->pairs : nullptr;
+    if (c->bvh_layout != PT_BVH_PAIRS || t->kind != TEX_F32 || tri->kind != TEX_F32 || texels > (1ll << 24)) return false;
+    if (t->pairs_gen == t->gen && t->pairs_tri == tri && t->pairs_tri_gen == tri->gen) return t->pairs_ok;
+    if (t->pairs_mem) { hipStreamSynchronize(c->stream); hipFree(t->pairs_mem); t->pairs_mem = nullptr; }
+    t->pairs_ok = false;
+    t->pairs_gen = t->gen; t->pairs_tri = tri; t->pairs_tri_gen = tri->gen;
     const unsigned nrec = (unsigned)((texels + 1) / 2);
-    hipError_t e = hipSuccess;
-    if (!t->pairs) e = hipMalloc(&t->pairs, (size_t)nrec * 64);
+    const unsigned nblk = (nrec + 1023) / 1024;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    unsigned char *inner = nullptr, *leafref = nullptr, *scratch = nullptr;
+    unsigned* counts = nullptr;
+    float* code = nullptr;
+    hipError_t e = hipMalloc(&scratch, 2 * al(nrec) + al(2 * nblk * sizeof(unsigned)) + al(nrec * sizeof(float)));
+    std::vector<unsigned> h(2 * nblk);
     unsigned bad = 0;
+    if (e == hipSuccess) {
+        inner = scratch; leafref = scratch + al(nrec);
+        counts = (unsigned*)(scratch + 2 * al(nrec));
+        code = (float*)((char*)counts + al(2 * nblk * sizeof(unsigned)));
+        e = hipMemsetAsync(leafref, 0, nrec, c->stream);
+    }
     if (e == hipSuccess) e = hipMemsetAsync(c->d_err + 1, 0, sizeof(unsigned), c->stream);
-    if (e == hipSuccess) e = pt_launch_bvh_pairs((const float4*)t->d, texels, t->pairs, nrec, c->d_err + 1, c->stream);
+    const float4* aabb = (const float4*)t->d;
+    const float4* trid = (const float4*)tri->d;
+    const long long ttex = (long long)tri->w * tri->h;
+    auto pass = [&](int k, float4* ir, float4* lr) {
+        return pt_launch_pairs_pass(k, aabb, texels, trid, ttex, nrec, inner, leafref, counts, code, ir, lr, c->d_err + 1, c->stream);
+    };
+    if (e == hipSuccess) e = pass(1, nullptr, nullptr);
+    if (e == hipSuccess) e = pass(2, nullptr, nullptr);
+    if (e == hipSuccess) e = hipMemcpyAsync(h.data(), counts, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(&bad, c->d_err + 1, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);   // once per upload of the texture
-    if (e != hipSuccess) { *rc = hipfail(c, e, "BVH child-pair build"); return nullptr; }
-    t->pairs_gen = t->gen;
-    t->pairs_ok = bad == 0;
-    return t->pairs_ok ? t->pairs : nullptr;
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    size_t n_inner = 0, n_leaf = 0;
+    if (e == hipSuccess && !bad) {
+        for (unsigned b = 0; b < nblk; b++) {   // exclusive scan of the per-block counts
+            unsigned ci = h[2 * b], cl = h[2 * b + 1];
+            h[2 * b] = (unsigned)n_inner; h[2 * b + 1] = (unsigned)n_leaf;
+            n_inner += ci; n_leaf += cl;
+        }
+        e = hipMalloc(&t->pairs_mem, al(n_inner * 64) + al(n_leaf * 48) + 256);
+        if (e == hipSuccess) {
+            t->pairs_inner = (const float4*)t->pairs_mem;
+            t->pairs_leaf = (const float4*)((char*)t->pairs_mem + al(n_inner * 64));
+            e = hipMemcpyAsync(counts, h.data(), h.size() * sizeof(unsigned), hipMemcpyHostToDevice, c->stream);
+        }
+        if (e == hipSuccess) e = pass(3, nullptr, nullptr);
+        if (e == hipSuccess) e = pass(4, (float4*)t->pairs_inner, (float4*)t->pairs_leaf);
+        if (e == hipSuccess) e = hipMemcpyAsync(&t->pairs_root, code, sizeof(float), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    }
+    if (scratch) { hipStreamSynchronize(c->stream); hipFree(scratch); }
+    if (e != hipSuccess) { *rc = hipfail(c, e, "BVH child-pair build"); return false; }
+    t->pairs_ok = !bad;
+    return t->pairs_ok;
 }
 
 int render_trace(pt_effect* fx, pt_texture* target)
@@ -358,7 +444,11 @@ int render_trace(pt_effect* fx, pt_texture* target)
         a.tri = (const float4*)tri->d;
         a.tri_texels = (long long)tri->w * tri->h;
         int prc = PT_OK;
-        a.bvh_pairs = ensure_pairs(c, bvh, &prc);
+        if (ensure_pairs(c, bvh, tri, &prc)) {
+            a.bvh_pairs = bvh->pairs_inner;
+            a.bvh_leaves = bvh->pairs_leaf;
+            a.bvh_root_code = bvh->pairs_root;
+        }
         if (prc) return prc;
         c->bvh_used = a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
         a.albedo = tex8(sampler(fx, "tAlbedoTexture"));
@@ -376,12 +466,32 @@ int render_trace(pt_effect* fx, pt_texture* target)
         int rc = wf_reserve(c, (target->w + 1) & ~1, (target->h + 1) & ~1, gx * gy, persist);
         if (rc) return rc;
     }
+    const unsigned n_wave_tiles = (unsigned)gx * gy * 4u;
+    if (c->backend == PT_BACKEND_PERSISTENT) {
+        int rc = gb_reserve(c, (target->w + 1) & ~1, (target->h + 1) & ~1);
+        if (rc) return rc;
+        const unsigned waves = (n_wave_tiles + c->persist_tiles - 1) / c->persist_tiles;
+        const size_t lanes = (size_t)((waves + 3) / 4) * pt::kBlock;
+        if (fx->prog == PT_PROG_GLTF && (rc = spill_reserve(c, lanes))) return rc;
+        a.spill = c->mk_spill;
+        a.spill_stride = lanes;
+    } else if (c->backend == PT_BACKEND_MEGAKERNEL && fx->prog == PT_PROG_GLTF) {
+        const size_t lanes = (size_t)gx * gy * pt::kBlock;
+        int rc = spill_reserve(c, lanes);
+        if (rc) return rc;
+        a.spill = c->mk_spill;
+        a.spill_stride = lanes;
+    }
     int rc = begin_draw(c, fx->prog);
     if (rc) return rc;
     if (gy > 0) {
         if (c->backend == PT_BACKEND_WAVEFRONT) {
             HIPCHK(c, hipMemsetAsync(c->wf.cnt, 0, 16 * pt::kShards * sizeof(unsigned), c->stream));
             HIPCHK(c, pt_launch_wavefront(fx->prog, c->counting ? 1 : 0, &a, &c->wf, gx, gy, persist, c->stream));
+        } else if (c->backend == PT_BACKEND_PERSISTENT) {
+            HIPCHK(c, pt_launch_persist(fx->prog, c->counting ? 1 : 0, &a, &c->gb, gx, n_wave_tiles, c->persist_tiles,
+                                        c->persist_refill, c->stream));
+            HIPCHK(c, pt_launch_finish(&a, &c->gb, gx, gy, c->stream));
         } else {
             HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, gy, c->stream));
         }
@@ -501,6 +611,8 @@ pt_ctx* pt_ctx_create(int device, int* err)
     auto* c = new pt_ctx();
     c->device = device;
     c->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    if (const char* v = std::getenv("PT_PERSIST_TILES")) c->persist_tiles = (unsigned)std::max(1, std::atoi(v));
+    if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
     c->stream = c->own_stream;
@@ -532,6 +644,8 @@ void pt_ctx_destroy(pt_ctx* c)
     }
     if (c->canvas) hipFree(c->canvas);
     if (c->wf_mem) hipFree(c->wf_mem);
+    if (c->mk_spill) hipFree(c->mk_spill);
+    if (c->gb_mem) hipFree(c->gb_mem);
     if (c->d_err) hipFree(c->d_err);
     if (c->d_counters) hipFree(c->d_counters);
     if (c->own_stream) hipStreamDestroy(c->own_stream);
@@ -695,7 +809,9 @@ void pt_texture_destroy(pt_texture* t)
         for (auto& kv : fx->samplers)
             if (kv.second == t) kv.second = nullptr;
     if (t->d && !t->external) { hipStreamSynchronize(c->stream); hipFree(t->d); }
-    if (t->pairs) { hipStreamSynchronize(c->stream); hipFree(t->pairs); }
+    if (t->pairs_mem) { hipStreamSynchronize(c->stream); hipFree(t->pairs_mem); }
+    for (auto* o : c->textures)   // records built against this triangle texture are stale
+        if (o->pairs_tri == t) { o->pairs_tri = nullptr; o->pairs_gen = ~0ull; }
     c->textures.erase(t);
     delete t;
 }
@@ -748,7 +864,8 @@ int pt_set_stream(pt_ctx* c, void* stream)
 
 int pt_set_backend(pt_ctx* c, int backend)
 {
-    if (!c || (backend != PT_BACKEND_MEGAKERNEL && backend != PT_BACKEND_WAVEFRONT)) return PT_ERR_ARG;
+    if (!c || (backend != PT_BACKEND_MEGAKERNEL && backend != PT_BACKEND_WAVEFRONT && backend != PT_BACKEND_PERSISTENT))
+        return PT_ERR_ARG;
     c->backend = backend;
     return PT_OK;
 }

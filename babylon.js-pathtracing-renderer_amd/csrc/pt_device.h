@@ -26,9 +26,13 @@ template <int P> constexpr bool kIsGltf = kBase<P> == PROG_GLTF || kBase<P> == P
 template <int P> constexpr bool kHasTex = kBase<P> == PROG_GLTF_TEX;
 template <int P> constexpr bool kPairs = P >= PROG_PAIRS;
 constexpr bool kIsGltfRt(int p) { return p == PROG_GLTF || p == PROG_GLTF_TEX; }
-// waves per SIMD the register allocator must leave room for (128 VGPRs -> 4; the textured
-// variant keeps 2 rather than spill)
-template <int P> constexpr int kMinWaves = kHasTex<P> ? 2 : 4;
+// waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 96 -> 5; the
+// textured variant keeps 2 rather than spill)
+// (measured on bunny 1080p: the child-pair walk gains 5-7% at 5 waves, the reference walk loses)
+#ifndef PT_MINWAVES_PAIRS
+#define PT_MINWAVES_PAIRS 5
+#endif
+template <int P> constexpr int kMinWaves = kHasTex<P> ? 2 : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
 
 // ------------------------------------------------------------------------------ per-lane state
 struct Path {
@@ -277,19 +281,23 @@ PT_D void bvhWalkRef(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float4 c0
     }
 }
 
-// Child-pair records (built by pt_bvh_pairs from the reference texture; only for trees whose
-// links are exact in-range integers, see pt_capi.cpp): record n = 64 contiguous bytes holding
-// the boxes of BOTH children of inner node n and their codes,
-//   r0 = A.min.xyz, A.max.x   r1 = A.max.yz, B.min.xy   r2 = B.min.z, B.max.xyz   r3 = codeA, codeB
-// with A = n+1, B = the node's right-child link, and code = id for an inner child, -1-idObject
-// for a leaf. An inner step is one 64-byte line instead of two 32-byte nodes in different lines,
-// and a pop needs no fetch: the stack entry (tNear, code) already says what the node is.
+// Child-pair records (pt_pairs_* in pt_kernels.hip; only for trees whose links are exact in-range
+// integers, see pt_capi.cpp ensure_pairs). Nodes are addressed by a code: rank >= 0 of an inner
+// node in the dense inner-record array, or -1 - rank of a leaf in the dense leaf-record array.
+//   inner record (64 B, one line): A.min.xyz A.max.x | A.max.yz B.min.xy | B.min.z B.max.xyz | codeA codeB
+//     (A = the node's left child n+1, B = its right-child link)
+//   leaf record (48 B): the leaf triangle's vertex texels (9 floats), its idObject
+// An inner step is one 64-byte line instead of two 32-byte nodes in different lines, a pop needs
+// no fetch (the stack entry (tNear, code) already says what the node is), and a leaf's vertices
+// sit in a dense 48-byte record instead of the first third of a 128-byte triangle texel group:
+// both arrays together are about 3.4 MB for StanfordBunny, within one XCD's L2.
 template <class Stk>
-PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float rootHdr, float curT,
-                       float& hitT, Stk& st, BvhResult& r)
+PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float curT, float& hitT, Stk& st,
+                       BvhResult& r)
 {
     const float4* R = a.bvh_pairs;
-    float code = rootHdr < 0.0f ? 0.0f : -1.0f - rootHdr;
+    const float4* LR = a.bvh_leaves;
+    float code = a.bvh_root_code;
     int sp = 0;
     bool skip = curT < hitT;
     for (;;) {
@@ -320,13 +328,12 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float r
             }
             continue;
         }
-        float id = 8.0f * (-1.0f - code);
-        float4 t0 = fetch32(a.tri, a.tri_texels, id), t1 = fetch32(a.tri, a.tri_texels, id + 1.0f),
-               t2 = fetch32(a.tri, a.tri_texels, id + 2.0f);
+        const float4* lf = LR + 3u * (unsigned)(-1.0f - code);
+        const float4 t0 = lf[0], t1 = lf[1], t2 = lf[2];
         r.leaves++;
         float tu, tv;
         float d = bvhTriangle(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
-        if (d < hitT) { hitT = d; r.triID = id; r.triU = tu; r.triV = tv; r.lookup = true; }
+        if (d < hitT) { hitT = d; r.triID = 8.0f * t2.y; r.triU = tu; r.triV = tv; r.lookup = true; }
     }
 }
 

@@ -14,9 +14,9 @@
 //    DPP/ds_swizzle exchanges (__shfl_xor 1 and 2) instead of a G-buffer round trip through HBM;
 //  * the scene constants (SetupScene) live in the kernarg segment -> SGPRs;
 //  * the BVH short stack (stackLevels[28] of (node, tNear)) keeps its first kStackLds levels per
-//    lane in LDS at [level][lane] (conflict-free); deeper levels (never reached by the reference
-//    meshes' rays, but legal for depth <= 28 trees) go to a private array = scratch, which the
-//    runtime backs only for resident waves;
+//    lane in LDS at [level][lane] (conflict-free); deeper levels (rare for the reference meshes'
+//    rays, but legal for depth <= 28 trees) go to a global slab [level][grid lane], not to a
+//    private array: scratch would be reserved for every resident wave;
 //  * BVH nodes are read as the reference's 32-byte texel pairs (two dwordx4 loads per node) and
 //    leaf triangles as three dwordx4 loads: the AoS texture layout is already the right one for
 //    incoherent per-lane gathers (one 32/48-B segment per lane, vs 8-9 lines for SoA).
@@ -47,23 +47,24 @@ struct Cnt {
 // ones in a private array
 typedef float vf2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) vf2 lds_float2;
-typedef __attribute__((address_space(5))) vf2 prv_float2;
+typedef __attribute__((address_space(1))) vf2 glb_float2;
 struct MegaStack {
     lds_float2* lds;
     unsigned slot;
-    prv_float2* deep;
+    glb_float2* deep;     // this lane's level kStackLds in the spill slab, levels `stride` apart
+    unsigned long long stride;
     PT_D float2 get(int si) const
     {
         vf2 e;
         if (si < kStackLds) e = lds[si * kBlock + slot];
-        else e = deep[si - kStackLds];
+        else e = deep[(si - kStackLds) * stride];
         return make_float2(e.x, e.y);
     }
     PT_D void put(int si, float2 e)
     {
         const vf2 v = { e.x, e.y };
         if (si < kStackLds) lds[si * kBlock + slot] = v;
-        else deep[si - kStackLds] = v;
+        else deep[(si - kStackLds) * stride] = v;
     }
 };
 
@@ -112,8 +113,8 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
     float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
     BvhResult br = { 0.0f, 0.0f, 0.0f, false, 1u, 0u, 0u };
-    MegaStack st{ (lds_float2*)lds, lane_slot, (prv_float2*)deep };
-    if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, c0.x, rootT, h.t, st, br);
+    MegaStack st{ (lds_float2*)lds, lane_slot, (glb_float2*)deep, a.spill_stride };
+    if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
     else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, h.t, st, br);
     if (COUNT) { cnt.node += br.nodes; cnt.leaf += br.leaves; cnt.ovf += br.ovf; }
     const bool lookup = br.lookup;
@@ -152,123 +153,182 @@ struct GOut {
 
 
 // CalculateRadiance: js/GLTFModelPathTracing_FragmentShader.js:351-609 and
-// js/BabylonPathTracing_FragmentShader.js:117-344 (METAL is a mirror there).
+// js/BabylonPathTracing_FragmentShader.js:117-344 (METAL is a mirror there), as one step per
+// iteration of its `for (bounces < 6)` loop so that the persistent kernel can interleave paths.
 // The reference's per-material branches are folded so that each sampling routine has ONE call
 // site (TRANSPARENT and CLEARCOAT_DIFFUSE share the Fresnel split; CLEARCOAT's transmitted branch
 // joins DIFFUSE's "cosine bounce or light sample" tail). The sequence of rng()/blueNoise_rand()
 // draws and every IEEE op per path are exactly the GLSL's.
+struct PState {
+    f3 mask;
+    float roughness;        // metallicRoughness.g persists across bounces (:368, :496)
+    int diffuseCount, hitType, bounce;
+    bool coat, specular, sampleLight;
+};
+
+PT_D void pathBegin(PState& s, GOut& g)
+{
+    s.mask = mk(1, 1, 1);
+    s.roughness = 0.0f;
+    s.diffuseCount = 0; s.hitType = -100; s.bounce = 0;
+    s.coat = false; s.specular = true; s.sampleLight = false;
+    g.nrm = mk(0, 0, 0); g.col = mk(0, 0, 0); g.id = 0.0f; g.sharp = 0.0f;   // pinned `out` zeros
+}
+
+// One loop iteration. Returns false when the path has ended; `accum` then holds the radiance
+// before the final max(accum, 0).
 template <int PROG, bool COUNT>
-PT_D f3 radiance(const TraceArgs& a, Path& p, GOut& g, float2* lds, unsigned lane_slot, float2* deep, Cnt& cnt)
+PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, GOut& g, f3& accum, float2* lds, unsigned lane_slot,
+                     float2* deep, Cnt& cnt)
 {
     constexpr bool gltf = kIsGltf<PROG>;
     Hit h;
-    f3 accum = mk(0, 0, 0), mask = mk(1, 1, 1);
-    float roughness = 0.0f;   // metallicRoughness.g persists across bounces (:368, :496)
-    int diffuseCount = 0, hitType = -100;
-    bool coat = false, specular = true, sampleLight = false;
+    const int bounces = s.bounce;
+    const int prevType = s.hitType;
+    sceneIntersect<PROG, COUNT>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt);
+    int hitType = h.type;
+    s.hitType = hitType;
+    if (h.t == kINF) return false;
+    f3 n = normalize(h.normal);
+    f3 nl = dot(n, p.rd) < 0.0f ? normalize(n) : normalize(-n);
+    f3 x = p.ro + p.rd * h.t;
+    if (bounces == 0) { g.nrm = nl; g.col = h.color; g.id = (float)h.id; }
+    if (bounces == 1 && prevType == METAL) { g.nrm = nl; g.id = (float)h.id; }
 
-#pragma unroll 1
-    for (int bounces = 0; bounces < 6; bounces++) {
-        const int prevType = hitType;
-        sceneIntersect<PROG, COUNT>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt);
-        hitType = h.type;
-        if (h.t == kINF) break;
-        f3 n = normalize(h.normal);
-        f3 nl = dot(n, p.rd) < 0.0f ? normalize(n) : normalize(-n);
-        f3 x = p.ro + p.rd * h.t;
-        if (bounces == 0) { g.nrm = nl; g.col = h.color; g.id = (float)h.id; }
-        if (bounces == 1 && prevType == METAL) { g.nrm = nl; g.id = (float)h.id; }
-
-        if (hitType == LIGHT) {
-            if (diffuseCount == 0) g.sharp = 1.01f;
-            if (specular || sampleLight) accum = mask * h.color;
-            break;
-        }
-        if (sampleLight) break;
-
-        if (kHasTex<PROG> && hitType == PBR_MATERIAL) {
-            float tx[4];
-            texBilinear(a.albedo, h.u, h.v, tx);
-            if (COUNT) cnt.tap += 4;
-            h.color = pow22(mk(tx[0], tx[1], tx[2]));
-            f3 emission = mk(0, 0, 0);
-            if (a.uses_emissive) { texBilinear(a.emissive, h.u, h.v, tx); if (COUNT) cnt.tap += 4; emission = mk(tx[0], tx[1], tx[2]); }
-            emission = pow22(emission);
-            float maxE = gmax(emission.x, gmax(emission.y, emission.z));
-            if (specular && maxE > 0.01f) { g.sharp = 1.01f; accum = mask * emission; break; }
-            hitType = DIFFUSE;
-            f3 mr = mk(0, 0, 0);
-            if (a.uses_metal) { texBilinear(a.metal, h.u, h.v, tx); if (COUNT) cnt.tap += 4; mr = mk(tx[0], tx[1], tx[2]); }
-            mr = pow22(mr);
-            roughness = mr.y;
-            if (mr.y > 0.01f) hitType = CLEARCOAT_DIFFUSE;
-            if (mr.z > 0.01f) hitType = METAL;
-        }
-
-        bool diffuseTail = hitType == DIFFUSE;
-        if (hitType == TRANSPARENT || hitType == CLEARCOAT_DIFFUSE) {
-            const bool glass = hitType == TRANSPARENT;
-            if (glass) {
-                if (diffuseCount == 0 && !coat && !a.moving) g.sharp = 1.01f;
-                else if (diffuseCount > 0) g.sharp = 0.0f;
-                else g.sharp = -1.0f;
-            } else {
-                coat = true;
-                g.sharp = 0.0f;
-            }
-            float ratio;
-            float Re = fresnel(p.rd, glass ? n : nl, 1.0f, glass ? 1.5f : 1.4f, ratio);
-            float Tr = 1.0f - Re;
-            float P = 0.25f + (0.5f * Re);
-            float RP = Re / P, TP = Tr / (1.0f - P);
-            if (blueNoise_rand(p) < P) {            // specular reflection off the interface
-                if (!glass && diffuseCount == 0) g.sharp = a.frame > 500.0f ? 1.01f : -1.0f;
-                mask = mask * RP;
-                p.rd = reflect(p.rd, nl);
-                p.ro = x + nl * a.eps;
-                continue;
-            }
-            if (glass) {                             // refraction through the dielectric
-                if (distance(n, nl) > 0.1f) {
-                    const float thickness = 0.01f;
-                    f3 cc = clamp3(h.color, 0.01f, 0.99f);
-                    mask = mask * mk(gexp(glog(cc.x) * thickness * h.t), gexp(glog(cc.y) * thickness * h.t),
-                                     gexp(glog(cc.z) * thickness * h.t));
-                }
-                mask = mask * TP;
-                p.rd = refract(p.rd, nl, ratio);
-                p.ro = x - nl * a.eps;
-                if (diffuseCount == 1) specular = true;
-                continue;
-            }
-            mask = mask * TP;                        // clear coat transmits into its diffuse base
-            diffuseTail = true;
-        }
-        if (diffuseTail) {
-            diffuseCount++;
-            mask = mask * h.color;
-            specular = false;
-            if (diffuseCount == 1 && blueNoise_rand(p) < 0.5f) {
-                p.rd = cosWeightedDir(p, nl);
-            } else {
-                float w;
-                f3 dl = sampleQuadLight(p, a, x, nl, w);
-                mask = mask * w;
-                p.rd = dl;
-                if (hitType == DIFFUSE || bounces < 3) sampleLight = true;
-            }
-            p.ro = x + nl * a.eps;
-            continue;
-        }
-        if (hitType == METAL) {
-            mask = mask * h.color;
-            if (gltf) p.rd = specularLobeDir(p, reflect(p.rd, nl), roughness);
-            else p.rd = reflect(p.rd, nl);
-            p.ro = x + nl * a.eps;
-            continue;
-        }
+    if (hitType == LIGHT) {
+        if (s.diffuseCount == 0) g.sharp = 1.01f;
+        if (s.specular || s.sampleLight) accum = s.mask * h.color;
+        return false;
     }
+    if (s.sampleLight) return false;
+
+    if (kHasTex<PROG> && hitType == PBR_MATERIAL) {
+        float tx[4];
+        texBilinear(a.albedo, h.u, h.v, tx);
+        if (COUNT) cnt.tap += 4;
+        h.color = pow22(mk(tx[0], tx[1], tx[2]));
+        f3 emission = mk(0, 0, 0);
+        if (a.uses_emissive) { texBilinear(a.emissive, h.u, h.v, tx); if (COUNT) cnt.tap += 4; emission = mk(tx[0], tx[1], tx[2]); }
+        emission = pow22(emission);
+        float maxE = gmax(emission.x, gmax(emission.y, emission.z));
+        if (s.specular && maxE > 0.01f) { g.sharp = 1.01f; accum = s.mask * emission; return false; }
+        hitType = DIFFUSE;
+        f3 mr = mk(0, 0, 0);
+        if (a.uses_metal) { texBilinear(a.metal, h.u, h.v, tx); if (COUNT) cnt.tap += 4; mr = mk(tx[0], tx[1], tx[2]); }
+        mr = pow22(mr);
+        s.roughness = mr.y;
+        if (mr.y > 0.01f) hitType = CLEARCOAT_DIFFUSE;
+        if (mr.z > 0.01f) hitType = METAL;
+        s.hitType = hitType;
+    }
+
+    const bool more = bounces + 1 < 6;
+    s.bounce = bounces + 1;
+    bool diffuseTail = hitType == DIFFUSE;
+    if (hitType == TRANSPARENT || hitType == CLEARCOAT_DIFFUSE) {
+        const bool glass = hitType == TRANSPARENT;
+        if (glass) {
+            if (s.diffuseCount == 0 && !s.coat && !a.moving) g.sharp = 1.01f;
+            else if (s.diffuseCount > 0) g.sharp = 0.0f;
+            else g.sharp = -1.0f;
+        } else {
+            s.coat = true;
+            g.sharp = 0.0f;
+        }
+        float ratio;
+        float Re = fresnel(p.rd, glass ? n : nl, 1.0f, glass ? 1.5f : 1.4f, ratio);
+        float Tr = 1.0f - Re;
+        float P = 0.25f + (0.5f * Re);
+        float RP = Re / P, TP = Tr / (1.0f - P);
+        if (blueNoise_rand(p) < P) {            // specular reflection off the interface
+            if (!glass && s.diffuseCount == 0) g.sharp = a.frame > 500.0f ? 1.01f : -1.0f;
+            s.mask = s.mask * RP;
+            p.rd = reflect(p.rd, nl);
+            p.ro = x + nl * a.eps;
+            return more;
+        }
+        if (glass) {                             // refraction through the dielectric
+            if (distance(n, nl) > 0.1f) {
+                const float thickness = 0.01f;
+                f3 cc = clamp3(h.color, 0.01f, 0.99f);
+                s.mask = s.mask * mk(gexp(glog(cc.x) * thickness * h.t), gexp(glog(cc.y) * thickness * h.t),
+                                     gexp(glog(cc.z) * thickness * h.t));
+            }
+            s.mask = s.mask * TP;
+            p.rd = refract(p.rd, nl, ratio);
+            p.ro = x - nl * a.eps;
+            if (s.diffuseCount == 1) s.specular = true;
+            return more;
+        }
+        s.mask = s.mask * TP;                    // clear coat transmits into its diffuse base
+        diffuseTail = true;
+    }
+    if (diffuseTail) {
+        s.diffuseCount++;
+        s.mask = s.mask * h.color;
+        s.specular = false;
+        if (s.diffuseCount == 1 && blueNoise_rand(p) < 0.5f) {
+            p.rd = cosWeightedDir(p, nl);
+        } else {
+            float w;
+            f3 dl = sampleQuadLight(p, a, x, nl, w);
+            s.mask = s.mask * w;
+            p.rd = dl;
+            if (hitType == DIFFUSE || bounces < 3) s.sampleLight = true;
+        }
+        p.ro = x + nl * a.eps;
+        return more;
+    }
+    if (hitType == METAL) {
+        s.mask = s.mask * h.color;
+        if (gltf) p.rd = specularLobeDir(p, reflect(p.rd, nl), s.roughness);
+        else p.rd = reflect(p.rd, nl);
+        p.ro = x + nl * a.eps;
+    }
+    return more;   // any other hitType: the GLSL loop continues with the ray unchanged
+}
+
+template <int PROG, bool COUNT>
+PT_D f3 radiance(const TraceArgs& a, Path& p, GOut& g, float2* lds, unsigned lane_slot, float2* deep, Cnt& cnt)
+{
+    PState s;
+    pathBegin(s, g);
+    f3 accum = mk(0, 0, 0);
+#pragma unroll 1
+    while (bounceStep<PROG, COUNT>(a, p, s, g, accum, lds, lane_slot, deep, cnt)) {}
     return max3s(accum, 0.0f);
+}
+
+// main()'s camera ray for pixel (px, py) (js/PathTracingCommon.js:1259-1292)
+PT_D void cameraRay(const TraceArgs& a, int px, int py, Path& p)
+{
+    const float* m = a.cam.m;
+    f3 camRight = mk(m[0], m[1], m[2]), camUp = mk(m[4], m[5], m[6]), camFwd = mk(m[8], m[9], m[10]);
+    f3 camPos = mk(m[12], m[13], m[14]);
+    float fcx = (float)px + 0.5f, fcy = (float)py + 0.5f;
+    p.s0 = (uint32_t)a.frame * (uint32_t)fcx;
+    p.s1 = (uint32_t)(a.frame + 1.0f) * (uint32_t)fcy;
+    p.counter = -1.0f;
+    int bx = (int)gmod(fcx + floorf(a.rnd[0] * 256.0f), 256.0f);
+    int by = (int)gmod(fcy + floorf(a.rnd[1] * 256.0f), 256.0f);
+    p.bn0 = 0.0f; p.bn1 = 0.0f;
+    if (bx < a.bluenoise.w && by < a.bluenoise.h) {
+        uchar4 b = a.bluenoise.p[by * a.bluenoise.w + bx];
+        p.bn0 = unorm8(b.x); p.bn1 = unorm8(b.y);
+    }
+    float ox = tentFilter(rng(p));
+    float oy = tentFilter(rng(p));
+    float ppx = ((fcx + ox) / a.res[0]) * 2.0f - 1.0f;
+    float ppy = ((fcy + oy) / a.res[1]) * 2.0f - 1.0f;
+    f3 rayDir = normalize((camRight * ppx) * a.ulen + (camUp * ppy) * a.vlen + camFwd);
+    f3 focal = rayDir * a.focus;
+    float ang = rng(p) * kTwoPi;
+    float rad = rng(p) * a.aperture;
+    float sn, cs;
+    gsincos(ang, sn, cs);
+    f3 apert = (camRight * cs + camUp * sn) * sqrtf(rad);
+    p.rd = normalize(focal - apert);
+    p.ro = camPos + apert;
 }
 
 PT_D float xorq(float v, int m) { return __shfl_xor(v, m, 64); }
@@ -284,45 +344,20 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
     const int band = blockIdx.y * a.num_parts + a.part;         // global 16-row band of this block
     const int px = blockIdx.x * kTile + (wave & 1) * 8 + lx;
     const int py = band * kTile + (wave >> 1) * 8 + ly;
-    float2 deep[kStackLevels - kStackLds];
+    // stack levels >= kStackLds: a global slab [level][lane of the grid] (a private array would be
+    // scratch, which the runtime reserves for every resident wave)
+    float2* deep = a.spill + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + tid;
 
     // lanes whose whole 2x2 quad lies beyond the (even-rounded) target do no work; quad helpers
     // that only complete a quad at an odd edge are shaded like GL helper invocations
     const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1);
     Cnt cnt = { 0, 0, 0, 0, 0, 0 };
     GOut g;   // pinned: the `out` parameters of CalculateRadiance start at 0
-    g.nrm = mk(0, 0, 0); g.col = mk(0, 0, 0); g.id = 0.0f; g.sharp = 0.0f;
+    g.nrm = mk(0, 0, 0); g.col = mk(0, 0, 0); g.id = 0.0f; g.sharp = 0.0f;   // (lanes without a path)
     f3 r = mk(0, 0, 0);
     if (active) {
-        // ---- main(): camera ray (js/PathTracingCommon.js:1259-1292)
-        const float* m = a.cam.m;
-        f3 camRight = mk(m[0], m[1], m[2]), camUp = mk(m[4], m[5], m[6]), camFwd = mk(m[8], m[9], m[10]);
-        f3 camPos = mk(m[12], m[13], m[14]);
-        float fcx = (float)px + 0.5f, fcy = (float)py + 0.5f;
         Path p;
-        p.s0 = (uint32_t)a.frame * (uint32_t)fcx;
-        p.s1 = (uint32_t)(a.frame + 1.0f) * (uint32_t)fcy;
-        p.counter = -1.0f;
-        int bx = (int)gmod(fcx + floorf(a.rnd[0] * 256.0f), 256.0f);
-        int by = (int)gmod(fcy + floorf(a.rnd[1] * 256.0f), 256.0f);
-        p.bn0 = 0.0f; p.bn1 = 0.0f;
-        if (bx < a.bluenoise.w && by < a.bluenoise.h) {
-            uchar4 b = a.bluenoise.p[by * a.bluenoise.w + bx];
-            p.bn0 = unorm8(b.x); p.bn1 = unorm8(b.y);
-        }
-        float ox = tentFilter(rng(p));
-        float oy = tentFilter(rng(p));
-        float ppx = ((fcx + ox) / a.res[0]) * 2.0f - 1.0f;
-        float ppy = ((fcy + oy) / a.res[1]) * 2.0f - 1.0f;
-        f3 rayDir = normalize((camRight * ppx) * a.ulen + (camUp * ppy) * a.vlen + camFwd);
-        f3 focal = rayDir * a.focus;
-        float ang = rng(p) * kTwoPi;
-        float rad = rng(p) * a.aperture;
-        float sn, cs;
-        gsincos(ang, sn, cs);
-        f3 apert = (camRight * cs + camUp * sn) * sqrtf(rad);
-        p.rd = normalize(focal - apert);
-        p.ro = camPos + apert;
+        cameraRay(a, px, py, p);
         r = radiance<PROG, COUNT>(a, p, g, lds_stack, tid, deep, cnt);
     }
 
@@ -385,6 +420,95 @@ template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF, false>(TraceArgs);
 template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF, true>(TraceArgs);
 template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF_TEX, false>(TraceArgs);
 template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF_TEX, true>(TraceArgs);
+
+// ------------------------------------------------------------------------------ persistent paths
+// pt_persist<PROG,COUNT>: the same per-pixel program with path regeneration. A wave owns a list
+// of `per_wave` 8x8 wave tiles (the static kernel's lane order) and keeps its 64 lanes busy: when
+// at least `refill` lanes have finished their path, they take the next pixels of the list and
+// start their camera rays, so the wave no longer idles while its longest path runs out its six
+// bounces. A finished path stores its G-buffer (objectNormal/ID/Color, pixelSharpness) and
+// radiance by pixel; wf_finish then does the 2x2 derivatives and the accumulation.
+template <int PROG, bool COUNT>
+__global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_persist(TraceArgs a, WfBufs w, int tiles_x,
+                                                                       unsigned n_wave_tiles, unsigned per_wave,
+                                                                       unsigned refill)
+{
+    __shared__ float2 lds_stack[kStackLds * kBlock];
+    const unsigned tid = threadIdx.x;
+    const unsigned lane = tid & 63u, wave = tid >> 6;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    const unsigned wid = blockIdx.x * (kBlock / 64) + wave;
+    unsigned next = wid * per_wave * 64u;
+    const unsigned end = min(next + per_wave * 64u, n_wave_tiles * 64u);
+    float2* deep = a.spill + (size_t)blockIdx.x * kBlock + tid;
+    Cnt cnt = { 0, 0, 0, 0, 0, 0 };
+    unsigned paths = 0;
+    Path p;
+    PState s;
+    GOut g;
+    f3 accum = mk(0, 0, 0);
+    unsigned pix = 0;
+    bool alive = false;
+    for (;;) {
+        const unsigned long long dead = __ballot(!alive);
+        const unsigned ndead = (unsigned)__popcll(dead);
+        if (next < end && (ndead >= refill || ndead == 64u)) {
+            if (!alive) {
+                const unsigned q = next + (unsigned)__popcll(dead & below);
+                if (q < end) {
+                    const unsigned L = q >> 6, l = q & 63u;
+                    const unsigned per_band = (unsigned)tiles_x * 4u;
+                    const unsigned bl = L / per_band, rem = L - bl * per_band;
+                    const unsigned tx = rem >> 2, sub = rem & 3u;
+                    const int band = (int)bl * a.num_parts + a.part;
+                    const int lx = (int)((l & 1u) | ((l >> 1) & 6u)), ly = (int)(((l >> 1) & 1u) | ((l >> 3) & 6u));
+                    const int px = (int)tx * kTile + (int)(sub & 1u) * 8 + lx;
+                    const int py = band * kTile + (int)(sub >> 1) * 8 + ly;
+                    if (px < w.wq && py < w.hq) {
+                        cameraRay(a, px, py, p);
+                        pathBegin(s, g);
+                        accum = mk(0, 0, 0);
+                        pix = (unsigned)py * (unsigned)w.wq + (unsigned)px;
+                        alive = true;
+                        if (COUNT) paths++;
+                    }
+                }
+            }
+            next += ndead;
+        }
+        if (__ballot(alive) == 0ull) {
+            if (next >= end) break;
+            continue;
+        }
+        if (alive && !bounceStep<PROG, COUNT>(a, p, s, g, accum, lds_stack, tid, deep, cnt)) {
+            const f3 r = max3s(accum, 0.0f);
+            w.gb0[pix] = make_float4(g.nrm.x, g.nrm.y, g.nrm.z, g.id);
+            w.gb1[pix] = make_float4(g.col.x, g.col.y, g.col.z, g.sharp);
+            w.rad[pix] = make_float4(r.x, r.y, r.z, 0.0f);
+            alive = false;
+        }
+    }
+    if (COUNT) {
+        unsigned long long* C = a.counters;
+        if (paths) atomicAdd(&C[C_PATHS], (unsigned long long)paths);
+        atomicAdd(&C[C_SEGMENTS], (unsigned long long)cnt.seg);
+        atomicAdd(&C[C_NODE], (unsigned long long)cnt.node);
+        atomicAdd(&C[C_LEAF], (unsigned long long)cnt.leaf);
+        atomicAdd(&C[C_HIT], (unsigned long long)cnt.hit);
+        atomicAdd(&C[C_RGBA8], (unsigned long long)(cnt.tap + paths));
+        atomicAdd(&C[C_OVERFLOW], (unsigned long long)cnt.ovf);
+    }
+}
+
+#define PT_PERSIST_INST(P)                                                                          \
+    template __global__ void pt_persist<P, false>(TraceArgs, WfBufs, int, unsigned, unsigned, unsigned); \
+    template __global__ void pt_persist<P, true>(TraceArgs, WfBufs, int, unsigned, unsigned, unsigned);
+PT_PERSIST_INST(PROG_CORNELL)
+PT_PERSIST_INST(PROG_GLTF)
+PT_PERSIST_INST(PROG_GLTF_TEX)
+PT_PERSIST_INST(PROG_PAIRS + PROG_GLTF)
+PT_PERSIST_INST(PROG_PAIRS + PROG_GLTF_TEX)
+#undef PT_PERSIST_INST
 
 // ------------------------------------------------------------------------------ screenCopy
 __global__ __launch_bounds__(256) void pt_copy(CopyArgs a)
@@ -460,36 +584,116 @@ __global__ __launch_bounds__(256) void pt_output(OutputArgs a)
 }
 
 // ------------------------------------------------------------------------------ child-pair BVH records
-// Record n of bvhWalkPairs (pt_device.h) from the reference texture, read with the same fetch32 /
-// float index arithmetic the reference walk uses, so every box and code equals what that walk
-// would fetch. `bad` collects the nodes that break the records' preconditions: an inner node's
-// right-child link that is not an exact integer in [0, nrec), or a leaf idObject that is not an
-// exact integer in [0, 2^24) (codes must round-trip through -1-x). The host then keeps the
-// reference walk for that texture.
-__global__ __launch_bounds__(256) void pt_bvh_pairs(const float4* aabb, long long texels, float4* rec, unsigned nrec,
-                                                    unsigned* bad)
+// Built once per (tAABBTexture, tTriangleTexture) upload; walked by bvhWalkPairs (pt_device.h).
+// Every value is read from the reference textures with the same fetch32 / float index arithmetic
+// the reference walk uses, so the boxes, codes and triangles equal what that walk would fetch.
+//   pass 1  kinds: inner node (idObject < 0); leaf referenced as a child of an inner node (or the
+//           root); `bad` flags links the records cannot express (right child not an exact integer
+//           in [0, nrec), left child n+1 beyond the texture) -> the host keeps the reference walk
+//   pass 2  per 1024-node block counts; the host scans them
+//   pass 3  dense ranks -> codes: inner rank, or -1 - leaf rank
+//   pass 4  inner records (64 B): A.min.xyz A.max.x | A.max.yz B.min.xy | B.min.z B.max.xyz |
+//           codeA codeB; leaf records (48 B): the three vertex texels' first 9 floats, idObject
+constexpr int kPairsBlock = 1024;   // nodes per scan block (256 threads x 4)
+
+__global__ __launch_bounds__(256) void pt_pairs_kinds(const float4* aabb, long long texels, unsigned nrec,
+                                                      unsigned char* inner, unsigned char* leafref, unsigned* bad)
 {
     const unsigned n = blockIdx.x * 256u + threadIdx.x;
     if (n >= nrec) return;
     const float fn = (float)n;   // exact: nrec <= 2^23
     const float4 c0 = fetch32(aabb, texels, fn * 2.0f), c1 = fetch32(aabb, texels, fn * 2.0f + 1.0f);
-    bool ok;
-    float4 r0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), r1 = r0, r2 = r0, r3 = r0;
-    if (c0.x < 0.0f) {
+    const bool in = c0.x < 0.0f;
+    inner[n] = in ? 1 : 0;
+    if (n == 0 && !in) leafref[0] = 1;
+    if (!in) return;
+    const float idA = fn + 1.0f, idB = c1.x;
+    const bool ok = idB >= 0.0f && idB < (float)nrec && floorf(idB) == idB && n + 1u < nrec;
+    if (!ok) { atomicOr(bad, 1u); return; }
+    const float4 a0 = fetch32(aabb, texels, idA * 2.0f), b0 = fetch32(aabb, texels, idB * 2.0f);
+    if (!(a0.x < 0.0f)) leafref[n + 1u] = 1;
+    if (!(b0.x < 0.0f)) leafref[(unsigned)idB] = 1;
+}
+
+__global__ __launch_bounds__(256) void pt_pairs_count(const unsigned char* inner, const unsigned char* leafref,
+                                                      unsigned nrec, unsigned* counts)
+{
+    __shared__ unsigned si[256], sl[256];
+    unsigned ci = 0, cl = 0;
+    for (int k = 0; k < 4; k++) {
+        const unsigned n = blockIdx.x * kPairsBlock + threadIdx.x * 4u + k;
+        if (n < nrec) { ci += inner[n]; cl += leafref[n]; }
+    }
+    si[threadIdx.x] = ci; sl[threadIdx.x] = cl;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if ((int)threadIdx.x < o) { si[threadIdx.x] += si[threadIdx.x + o]; sl[threadIdx.x] += sl[threadIdx.x + o]; }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) { counts[2 * blockIdx.x] = si[0]; counts[2 * blockIdx.x + 1] = sl[0]; }
+}
+
+__global__ __launch_bounds__(256) void pt_pairs_rank(const unsigned char* inner, const unsigned char* leafref,
+                                                     unsigned nrec, const unsigned* offsets, float* code)
+{
+    __shared__ unsigned si[256], sl[256];
+    unsigned fi[4], fl[4], ci = 0, cl = 0;
+    for (int k = 0; k < 4; k++) {
+        const unsigned n = blockIdx.x * kPairsBlock + threadIdx.x * 4u + k;
+        fi[k] = n < nrec ? inner[n] : 0u;
+        fl[k] = n < nrec ? leafref[n] : 0u;
+        ci += fi[k]; cl += fl[k];
+    }
+    si[threadIdx.x] = ci; sl[threadIdx.x] = cl;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {   // inclusive Hillis-Steele scan
+        unsigned vi = threadIdx.x >= (unsigned)o ? si[threadIdx.x - o] : 0u;
+        unsigned vl = threadIdx.x >= (unsigned)o ? sl[threadIdx.x - o] : 0u;
+        __syncthreads();
+        si[threadIdx.x] += vi; sl[threadIdx.x] += vl;
+        __syncthreads();
+    }
+    unsigned ri = offsets[2 * blockIdx.x] + si[threadIdx.x] - ci;
+    unsigned rl = offsets[2 * blockIdx.x + 1] + sl[threadIdx.x] - cl;
+    for (int k = 0; k < 4; k++) {
+        const unsigned n = blockIdx.x * kPairsBlock + threadIdx.x * 4u + k;
+        if (n >= nrec) break;
+        float cd = 0.0f;
+        if (fi[k]) cd = (float)ri;
+        else if (fl[k]) cd = -1.0f - (float)rl;
+        code[n] = cd;
+        ri += fi[k]; rl += fl[k];
+    }
+}
+
+__global__ __launch_bounds__(256) void pt_pairs_build(const float4* aabb, long long texels, const float4* tri,
+                                                      long long tri_texels, unsigned nrec, const float* code,
+                                                      float4* inner_rec, float4* leaf_rec,
+                                                      const unsigned char* inner, const unsigned char* leafref)
+{
+    const unsigned n = blockIdx.x * 256u + threadIdx.x;
+    if (n >= nrec) return;
+    const float fn = (float)n;
+    if (inner[n]) {
+        const float4 c1 = fetch32(aabb, texels, fn * 2.0f + 1.0f);
         const float idA = fn + 1.0f, idB = c1.x;
         const float4 a0 = fetch32(aabb, texels, idA * 2.0f), a1 = fetch32(aabb, texels, idA * 2.0f + 1.0f);
         const float4 b0 = fetch32(aabb, texels, idB * 2.0f), b1 = fetch32(aabb, texels, idB * 2.0f + 1.0f);
-        ok = idB >= 0.0f && idB < (float)nrec && floorf(idB) == idB;
-        r0 = make_float4(a0.y, a0.z, a0.w, a1.y);
-        r1 = make_float4(a1.z, a1.w, b0.y, b0.z);
-        r2 = make_float4(b0.w, b1.y, b1.z, b1.w);
-        r3 = make_float4(a0.x < 0.0f ? idA : -1.0f - a0.x, b0.x < 0.0f ? idB : -1.0f - b0.x, 0.0f, 0.0f);
-    } else {
-        ok = floorf(c0.x) == c0.x && c0.x < 16777216.0f;   // NaN and inf fail
+        float4* o = inner_rec + 4ull * (unsigned)code[n];
+        o[0] = make_float4(a0.y, a0.z, a0.w, a1.y);
+        o[1] = make_float4(a1.z, a1.w, b0.y, b0.z);
+        o[2] = make_float4(b0.w, b1.y, b1.z, b1.w);
+        o[3] = make_float4(code[n + 1u], code[(unsigned)idB], 0.0f, 0.0f);
+    } else if (leafref[n]) {
+        const float hdr = fetch32(aabb, texels, fn * 2.0f).x;
+        const float id = 8.0f * hdr;
+        const float4 t0 = fetch32(tri, tri_texels, id), t1 = fetch32(tri, tri_texels, id + 1.0f),
+                     t2 = fetch32(tri, tri_texels, id + 2.0f);
+        float4* o = leaf_rec + 3ull * (unsigned)(-1.0f - code[n]);
+        o[0] = t0;
+        o[1] = t1;
+        o[2] = make_float4(t2.x, hdr, 0.0f, 0.0f);
     }
-    float4* o = rec + 4ull * n;
-    o[0] = r0; o[1] = r1; o[2] = r2; o[3] = r3;
-    if (!ok) atomicOr(bad, 1u);
 }
 
 // ------------------------------------------------------------------------------ self-test
@@ -547,10 +751,46 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
     return hipGetLastError();
 }
 
-hipError_t pt_launch_bvh_pairs(const float4* aabb, long long texels, float4* rec, unsigned nrec, unsigned* bad,
-                               hipStream_t s)
+hipError_t pt_launch_persist(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x,
+                             unsigned n_wave_tiles, unsigned per_wave, unsigned refill, hipStream_t s)
 {
-    hipLaunchKernelGGL(pt::pt_bvh_pairs, dim3((nrec + 255) / 256), dim3(256), 0, s, aabb, texels, rec, nrec, bad);
+    if (prog == pt::PROG_GLTF && (a->uses_albedo || a->uses_bump)) prog = pt::PROG_GLTF_TEX;
+    if (pt::kIsGltfRt(prog) && a->bvh_pairs) prog += pt::PROG_PAIRS;
+    const unsigned waves = (n_wave_tiles + per_wave - 1) / per_wave;
+    dim3 grid((waves + 3) / 4), block(pt::kBlock);
+#define PT_LAUNCH(P)                                                                                          \
+    do {                                                                                                      \
+        if (count) hipLaunchKernelGGL((pt::pt_persist<P, true>), grid, block, 0, s, *a, *w, tiles_x, n_wave_tiles, per_wave, refill); \
+        else hipLaunchKernelGGL((pt::pt_persist<P, false>), grid, block, 0, s, *a, *w, tiles_x, n_wave_tiles, per_wave, refill); \
+    } while (0)
+    switch (prog) {
+    case pt::PROG_CORNELL: PT_LAUNCH(pt::PROG_CORNELL); break;
+    case pt::PROG_GLTF: PT_LAUNCH(pt::PROG_GLTF); break;
+    case pt::PROG_GLTF_TEX: PT_LAUNCH(pt::PROG_GLTF_TEX); break;
+    case pt::PROG_PAIRS + pt::PROG_GLTF: PT_LAUNCH(pt::PROG_PAIRS + pt::PROG_GLTF); break;
+    case pt::PROG_PAIRS + pt::PROG_GLTF_TEX: PT_LAUNCH(pt::PROG_PAIRS + pt::PROG_GLTF_TEX); break;
+    default: return hipErrorInvalidValue;
+    }
+#undef PT_LAUNCH
+    return hipGetLastError();
+}
+
+// the four passes of the child-pair build; `offsets` is filled by the host between pass 2 and 3
+hipError_t pt_launch_pairs_pass(int pass, const float4* aabb, long long texels, const float4* tri, long long tri_texels,
+                                unsigned nrec, unsigned char* inner, unsigned char* leafref, unsigned* counts,
+                                float* code, float4* inner_rec, float4* leaf_rec, unsigned* bad, hipStream_t s)
+{
+    const dim3 nodes((nrec + 255) / 256), blocks((nrec + pt::kPairsBlock - 1) / pt::kPairsBlock), b256(256);
+    switch (pass) {
+    case 1: hipLaunchKernelGGL(pt::pt_pairs_kinds, nodes, b256, 0, s, aabb, texels, nrec, inner, leafref, bad); break;
+    case 2: hipLaunchKernelGGL(pt::pt_pairs_count, blocks, b256, 0, s, inner, leafref, nrec, counts); break;
+    case 3: hipLaunchKernelGGL(pt::pt_pairs_rank, blocks, b256, 0, s, inner, leafref, nrec, counts, code); break;
+    case 4:
+        hipLaunchKernelGGL(pt::pt_pairs_build, nodes, b256, 0, s, aabb, texels, tri, tri_texels, nrec, code, inner_rec,
+                           leaf_rec, inner, leafref);
+        break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

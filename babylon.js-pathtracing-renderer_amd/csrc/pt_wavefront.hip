@@ -252,7 +252,7 @@ __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b
         float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
         BvhResult br = { 0.0f, 0.0f, 0.0f, false, 0u, 0u, 0u };
         WfStack st{ (lds_float2*)lds, tid, (glb_float2*)deep, dstride };
-        if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, c0.x, rootT, hitT, st, br);
+        if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, rootT, hitT, st, br);
         else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, hitT, st, br);
         const unsigned nodes = br.nodes, leaves = br.leaves, ovf = br.ovf;
         const bool lookup = br.lookup;
@@ -558,5 +558,11 @@ extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceAr
     }
 #undef WF_BOUNCE
     hipLaunchKernelGGL(wf_finish, tiles, blk, 0, s, *a, *w);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t pt_launch_finish(const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x, int bands, hipStream_t s)
+{
+    hipLaunchKernelGGL(pt::wf_finish, dim3(tiles_x, bands), dim3(pt::kBlock), 0, s, *a, *w);
     return hipGetLastError();
 }

@@ -23,7 +23,7 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.environ.get("PT_LIBPT", os.path.join(PKG, "libpt.so"))
+LIB_PATH = os.environ.get("PT_LIBPT") or os.path.join(PKG, "libpt.so")
 
 PROG = {"screenCopy": 1, "screenOutput": 2, "cornell": 3, "gltf": 4, "hdri": 5, "sky": 6, "quadric": 7}
 ERRORS = {0: "PT_OK", -1: "PT_ERR_ARG", -2: "PT_ERR_HIP", -3: "PT_ERR_SHADER", -4: "PT_ERR_STATE",
@@ -135,8 +135,9 @@ class Engine:
         self.check(lib().pt_set_stream(self.ctx, ctypes.c_void_p(hip_stream) if hip_stream else None), "pt_set_stream")
 
     def set_backend(self, backend):
-        """'megakernel' (default) or 'wavefront': same bits, different schedule."""
-        self.check(lib().pt_set_backend(self.ctx, {"megakernel": 0, "wavefront": 1}[backend]), "pt_set_backend")
+        """'megakernel' (default), 'wavefront' or 'persistent': same bits, different schedule."""
+        self.check(lib().pt_set_backend(self.ctx, {"megakernel": 0, "wavefront": 1, "persistent": 2}[backend]),
+                   "pt_set_backend")
 
     BVH_LAYOUTS = {"reference": 0, "pairs": 1}
 

@@ -125,9 +125,10 @@ int pt_write_pixels(pt_ctx* ctx, pt_texture* tex, const void* src, size_t bytes)
  * unchanged). screenOutput/copy stay full-frame. num_parts = 1 restores full frames. */
 int pt_set_row_partition(pt_ctx* ctx, int num_parts, int part);
 /* Path-tracing backend of this context: PT_BACKEND_MEGAKERNEL (default: one kernel, one lane per
- * path) or PT_BACKEND_WAVEFRONT (per-segment kernels over compacted path queues). Results are
- * bit-identical; the choice only changes speed. */
-enum pt_backend { PT_BACKEND_MEGAKERNEL = 0, PT_BACKEND_WAVEFRONT = 1 };
+ * path), PT_BACKEND_WAVEFRONT (per-segment kernels over compacted path queues) or
+ * PT_BACKEND_PERSISTENT (waves regenerate finished lanes with new pixels; G-buffer + finish pass).
+ * Results are bit-identical; the choice only changes speed. */
+enum pt_backend { PT_BACKEND_MEGAKERNEL = 0, PT_BACKEND_WAVEFRONT = 1, PT_BACKEND_PERSISTENT = 2 };
 int pt_set_backend(pt_ctx* ctx, int backend);
 /* BVH walk of the glTF program. PT_BVH_PAIRS (default) re-packs tAABBTexture once per upload into
  * 64-byte child-pair records (both children's boxes in one line, pops without a fetch) and walks

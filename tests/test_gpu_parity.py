@@ -105,7 +105,7 @@ def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1):
 
 
 # (schedule, BVH layout): every combination must give the same bits
-BACKENDS = [("megakernel", "pairs"), ("megakernel", "reference"), ("wavefront", "pairs"), ("wavefront", "reference")]
+BACKENDS = [(b, l) for b in ("megakernel", "persistent", "wavefront") for l in ("pairs", "reference")]
 
 
 @pytest.fixture(params=BACKENDS, ids=["-".join(b) for b in BACKENDS])
@@ -188,7 +188,7 @@ def test_in_place_history(engine, backend):
     assert _bits_equal(ref_acc[2], rt.read())
 
 
-@pytest.mark.parametrize("backend_name", ["megakernel", "wavefront"])
+@pytest.mark.parametrize("backend_name", ["megakernel", "persistent", "wavefront"])
 def test_malformed_bvh_links_fall_back_exactly(engine, backend_name):
     """A tree whose right-child links are not exact integers (legal input: the GLSL just fetches
     whatever texel the float index lands on) cannot be re-packed; the draw must fall back to the
