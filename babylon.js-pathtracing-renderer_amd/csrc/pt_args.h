@@ -11,7 +11,10 @@ namespace pt {
 constexpr int kBlock = 256;          // 4 waves; a block shades a 16x16 pixel tile
 constexpr int kTile = 16;            // tile edge == row-band height used for sharding
 constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing_FragmentShader.js:95
-constexpr int kStackLds = 12;        // levels kept in LDS per lane; deeper levels go to a global slab
+#ifndef PT_STACK_LDS
+#define PT_STACK_LDS 10
+#endif
+constexpr int kStackLds = PT_STACK_LDS;        // levels kept in LDS per lane; deeper levels go to a global slab
 
 enum Counter { C_PATHS, C_SEGMENTS, C_NODE, C_LEAF, C_HIT, C_RGBA8, C_OVERFLOW, C_NUM };
 enum ErrBits { E_STACK = 1u };

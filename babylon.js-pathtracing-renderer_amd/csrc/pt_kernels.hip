@@ -146,9 +146,35 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     }
 }
 
+// CalculateRadiance's `out` parameters objectNormal / objectColor / objectID / pixelSharpness:
+// in registers (GOut) or, for the megakernel, in LDS [field][lane] (GOutLds), which takes eight
+// live values out of the VGPR budget of the bounce loop
 struct GOut {
     f3 nrm, col;
     float id, sharp;
+    PT_D void clear() { nrm = mk(0, 0, 0); col = mk(0, 0, 0); id = 0.0f; sharp = 0.0f; }
+    PT_D void setNrm(f3 v) { nrm = v; }
+    PT_D void setCol(f3 v) { col = v; }
+    PT_D void setId(float v) { id = v; }
+    PT_D void setSharp(float v) { sharp = v; }
+};
+typedef __attribute__((address_space(3))) float lds_float;
+struct GOutLds {
+    lds_float* p;
+    unsigned slot;
+    PT_D void put(int f, float v) { p[f * kBlock + slot] = v; }
+    PT_D float get(int f) const { return p[f * kBlock + slot]; }
+    PT_D void clear() { for (int f = 0; f < 8; f++) put(f, 0.0f); }
+    PT_D void setNrm(f3 v) { put(0, v.x); put(1, v.y); put(2, v.z); }
+    PT_D void setCol(f3 v) { put(3, v.x); put(4, v.y); put(5, v.z); }
+    PT_D void setId(float v) { put(6, v); }
+    PT_D void setSharp(float v) { put(7, v); }
+    PT_D GOut load() const
+    {
+        GOut g;
+        g.nrm = mk(get(0), get(1), get(2)); g.col = mk(get(3), get(4), get(5)); g.id = get(6); g.sharp = get(7);
+        return g;
+    }
 };
 
 
@@ -166,19 +192,20 @@ struct PState {
     bool coat, specular, sampleLight;
 };
 
-PT_D void pathBegin(PState& s, GOut& g)
+template <class G>
+PT_D void pathBegin(PState& s, G& g)
 {
     s.mask = mk(1, 1, 1);
     s.roughness = 0.0f;
     s.diffuseCount = 0; s.hitType = -100; s.bounce = 0;
     s.coat = false; s.specular = true; s.sampleLight = false;
-    g.nrm = mk(0, 0, 0); g.col = mk(0, 0, 0); g.id = 0.0f; g.sharp = 0.0f;   // pinned `out` zeros
+    g.clear();   // pinned `out` zeros
 }
 
 // One loop iteration. Returns false when the path has ended; `accum` then holds the radiance
 // before the final max(accum, 0).
-template <int PROG, bool COUNT>
-PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, GOut& g, f3& accum, float2* lds, unsigned lane_slot,
+template <int PROG, bool COUNT, class G>
+PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, float2* lds, unsigned lane_slot,
                      float2* deep, Cnt& cnt)
 {
     constexpr bool gltf = kIsGltf<PROG>;
@@ -192,11 +219,11 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, GOut& g, f3& accum,
     f3 n = normalize(h.normal);
     f3 nl = dot(n, p.rd) < 0.0f ? normalize(n) : normalize(-n);
     f3 x = p.ro + p.rd * h.t;
-    if (bounces == 0) { g.nrm = nl; g.col = h.color; g.id = (float)h.id; }
-    if (bounces == 1 && prevType == METAL) { g.nrm = nl; g.id = (float)h.id; }
+    if (bounces == 0) { g.setNrm(nl); g.setCol(h.color); g.setId((float)h.id); }
+    if (bounces == 1 && prevType == METAL) { g.setNrm(nl); g.setId((float)h.id); }
 
     if (hitType == LIGHT) {
-        if (s.diffuseCount == 0) g.sharp = 1.01f;
+        if (s.diffuseCount == 0) g.setSharp(1.01f);
         if (s.specular || s.sampleLight) accum = s.mask * h.color;
         return false;
     }
@@ -211,7 +238,7 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, GOut& g, f3& accum,
         if (a.uses_emissive) { texBilinear(a.emissive, h.u, h.v, tx); if (COUNT) cnt.tap += 4; emission = mk(tx[0], tx[1], tx[2]); }
         emission = pow22(emission);
         float maxE = gmax(emission.x, gmax(emission.y, emission.z));
-        if (s.specular && maxE > 0.01f) { g.sharp = 1.01f; accum = s.mask * emission; return false; }
+        if (s.specular && maxE > 0.01f) { g.setSharp(1.01f); accum = s.mask * emission; return false; }
         hitType = DIFFUSE;
         f3 mr = mk(0, 0, 0);
         if (a.uses_metal) { texBilinear(a.metal, h.u, h.v, tx); if (COUNT) cnt.tap += 4; mr = mk(tx[0], tx[1], tx[2]); }
@@ -228,12 +255,12 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, GOut& g, f3& accum,
     if (hitType == TRANSPARENT || hitType == CLEARCOAT_DIFFUSE) {
         const bool glass = hitType == TRANSPARENT;
         if (glass) {
-            if (s.diffuseCount == 0 && !s.coat && !a.moving) g.sharp = 1.01f;
-            else if (s.diffuseCount > 0) g.sharp = 0.0f;
-            else g.sharp = -1.0f;
+            if (s.diffuseCount == 0 && !s.coat && !a.moving) g.setSharp(1.01f);
+            else if (s.diffuseCount > 0) g.setSharp(0.0f);
+            else g.setSharp(-1.0f);
         } else {
             s.coat = true;
-            g.sharp = 0.0f;
+            g.setSharp(0.0f);
         }
         float ratio;
         float Re = fresnel(p.rd, glass ? n : nl, 1.0f, glass ? 1.5f : 1.4f, ratio);
@@ -241,7 +268,7 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, GOut& g, f3& accum,
         float P = 0.25f + (0.5f * Re);
         float RP = Re / P, TP = Tr / (1.0f - P);
         if (blueNoise_rand(p) < P) {            // specular reflection off the interface
-            if (!glass && s.diffuseCount == 0) g.sharp = a.frame > 500.0f ? 1.01f : -1.0f;
+            if (!glass && s.diffuseCount == 0) g.setSharp(a.frame > 500.0f ? 1.01f : -1.0f);
             s.mask = s.mask * RP;
             p.rd = reflect(p.rd, nl);
             p.ro = x + nl * a.eps;
@@ -288,14 +315,14 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, GOut& g, f3& accum,
     return more;   // any other hitType: the GLSL loop continues with the ray unchanged
 }
 
-template <int PROG, bool COUNT>
-PT_D f3 radiance(const TraceArgs& a, Path& p, GOut& g, float2* lds, unsigned lane_slot, float2* deep, Cnt& cnt)
+template <int PROG, bool COUNT, class G>
+PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_slot, float2* deep, Cnt& cnt)
 {
     PState s;
     pathBegin(s, g);
     f3 accum = mk(0, 0, 0);
 #pragma unroll 1
-    while (bounceStep<PROG, COUNT>(a, p, s, g, accum, lds, lane_slot, deep, cnt)) {}
+    while (bounceStep<PROG, COUNT, G>(a, p, s, g, accum, lds, lane_slot, deep, cnt)) {}
     return max3s(accum, 0.0f);
 }
 
@@ -337,6 +364,7 @@ template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
 {
     __shared__ float2 lds_stack[kStackLds * kBlock];
+    __shared__ float lds_gout[8 * kBlock];
     const unsigned tid = threadIdx.x;
     const int lane = tid & 63, wave = tid >> 6;
     const int lx = (lane & 1) | ((lane >> 1) & 6);
@@ -352,14 +380,15 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
     // that only complete a quad at an odd edge are shaded like GL helper invocations
     const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1);
     Cnt cnt = { 0, 0, 0, 0, 0, 0 };
-    GOut g;   // pinned: the `out` parameters of CalculateRadiance start at 0
-    g.nrm = mk(0, 0, 0); g.col = mk(0, 0, 0); g.id = 0.0f; g.sharp = 0.0f;   // (lanes without a path)
+    GOutLds gl{ (lds_float*)lds_gout, tid };
+    gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
     f3 r = mk(0, 0, 0);
     if (active) {
         Path p;
         cameraRay(a, px, py, p);
-        r = radiance<PROG, COUNT>(a, p, g, lds_stack, tid, deep, cnt);
+        r = radiance<PROG, COUNT>(a, p, gl, lds_stack, tid, deep, cnt);
     }
+    const GOut g = gl.load();
 
     // ---- 2x2 fine derivatives (js/PathTracingCommon.js:1306-1320): partner lanes ^1 (x) and ^2 (y)
     const bool xodd = lane & 1, yodd = lane & 2;

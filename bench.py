@@ -184,6 +184,7 @@ def main():
         player.play_call(player.synth_frame(k)[0])
     cnt = engine.counters()
     engine.set_counting(False)
+    layout = engine.bvh_layout_used()
     bytes_per_launch = algorithmic_bytes(cnt) / nc
     if dist is not None:
         import torch
@@ -226,7 +227,8 @@ def main():
                       "screen_output": round(out_ms / max(1, pt_n), 4)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                     "kernel": "pt_trace<GLTF>", "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                     "kernel": "pt_trace<%sGLTF>" % ("PAIRS+" if layout == "pairs" else ""),
+                     "algorithmic_bytes_per_launch": int(bytes_per_launch),
                      "counts_per_launch": {k: v / nc for k, v in cnt.items()}},
     }
     if args.cpu_budget > 0:

@@ -1,6 +1,6 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -rf -x > gpurun_out/pytest_gpu_r01h.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu_r01h.log
+timeout -k 10 600 python -m pytest tests -m gpu -q -rf -x > gpurun_out/pytest_gpu_r01j.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_gpu_r01j.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-bash tools/gpu_variants.sh b
+bash tools/gpu_variants.sh c
