@@ -31,8 +31,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 FRAME_SIZES = {1: (1920, 1080), 2: (3840, 1080), 4: (3840, 2160), 8: (7680, 2160)}
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 # algorithmic bytes per counted event
-BYTES = {"node_fetches": 32, "leaf_tests": 48, "hit_lookups": 64, "rgba8_taps": 4}
-PIXEL_IO = 32                  # previousBuffer texel read + accumulation texel write
+BYTES = {"node_fetches": 32, "leaf_tests": 48, "hit_lookups": 128, "rgba8_taps": 4}
+PIXEL_IO = 32                  # previousBuffer texel read + accumulation texel write (+4 B blue noise = an rgba8 tap)
 
 
 def frame_size(n):
