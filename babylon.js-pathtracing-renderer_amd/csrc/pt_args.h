@@ -44,6 +44,17 @@ struct Tex8 {               // RGBA8 sampler: texels row-major from row 0 (inver
     int w, h;
 };
 
+// Uniform-only terms of Get_Sky_Color (js/PathTracingCommon.js:416-475), evaluated once per draw
+// on the host with the pinned sequences
+struct SkyArgs {
+    ptg::f3 sun;            // uSunDirection
+    ptg::f3 rayleigh, mie;  // rayleighAtX, mieAtX
+    ptg::f3 rm;             // rayleighAtX + mieAtX
+    float sunE, sunE19000;  // SunIntensity(dot(UP, sun)), sunE * 19000
+    float fade;             // clamp(pow(1 - cosSunUpAngle, 5), 0, 1)
+    float retExp;           // 1 / (1.2 + 1.2 * sunfade)
+};
+
 // Per-draw kernel arguments. Wave-uniform: read with scalar loads from the kernarg segment; the
 // per-object loops index them dynamically so they are re-read from the scalar cache instead of
 // being hoisted into (vector) registers.
@@ -60,6 +71,8 @@ struct TraceArgs {
     TriArg qtri[12];
     ptg::f3 qnormal[6], qcolor[6];
     int qtype[6];
+    int nquads;             // N_QUADS: 6 (Cornell, glTF), 4 (sky: no ceiling, no quad light)
+    SkyArgs sky;
     QuadArg light;          // quads[5], sampled by sampleAxisAlignedQuadLight
     float light_r2;         // distance(v0,v1)*distance(v0,v3) of quads[5]
     // glTF material switches (js/GLTFModelPathTracing_FragmentShader.js:21-25)

@@ -199,6 +199,25 @@ float hdist(ptg::f3 a, ptg::f3 b)
     return std::sqrt(x * x + y * y + z * z);
 }
 
+// The uniform-only terms of Get_Sky_Color (js/PathTracingCommon.js:373-475) with the pinned
+// sequences of pt_glsl.h, once per draw instead of once per sky sample
+void sky_setup(const pt_effect* fx, pt::SkyArgs& k)
+{
+    using namespace ptg;
+    k.sun = v3(uf(fx, "uSunDirection", 0), uf(fx, "uSunDirection", 1), uf(fx, "uSunDirection", 2));
+    const float cosSunUpAngle = dot(mk(0.0f, 1.0f, 0.0f), k.sun);
+    const float z = gclamp(cosSunUpAngle, -1.0f, 1.0f);   // SunIntensity
+    k.sunE = 200.0f * gmax(0.0f, 1.0f - gpow(2.71828182845904524f, -((1.6110731556870734f - gacos(z)) / 1.5f)));
+    k.sunE19000 = k.sunE * 19000.0f;
+    k.rayleigh = mk(5.804542996261093E-6f, 1.3562911419845635E-5f, 3.0265902468824876E-5f) * 2.0f;
+    const float c = (0.2f * 0.5f) * 10E-18f;               // totalMie
+    k.mie = (mk(1.8399918514433978E14f, 2.7798023919660528E14f, 4.0790479543861094E14f) * (0.434f * c)) * 0.03f;
+    k.rm = k.rayleigh + k.mie;
+    k.fade = gclamp(gpow(1.0f - cosSunUpAngle, 5.0f), 0.0f, 1.0f);
+    const float sunfade = 1.0f - gclamp(1.0f - gexp((k.sun.y / 450000.0f)), 0.0f, 1.0f);
+    k.retExp = 1.0f / (1.2f + (1.2f * sunfade));
+}
+
 // SetupScene() of js/BabylonPathTracing_FragmentShader.js:348-378 and
 // js/GLTFModelPathTracing_FragmentShader.js:613-643, evaluated once per draw.
 void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
@@ -212,7 +231,7 @@ void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
     a.sph[0].color = v3(1.0f, 1.0f, 0.0f);
     a.sph[0].type = pt::CLEARCOAT_DIFFUSE;
     a.sph[1].color = v3(1.0f, 1.0f, 1.0f);
-    a.sph[1].type = fx->prog == PT_PROG_CORNELL ? ui(fx, "uRightSphereMatType") : pt::METAL;
+    a.sph[1].type = fx->prog == PT_PROG_GLTF ? pt::METAL : ui(fx, "uRightSphereMatType");
     pt::QuadArg q[6];
     q[0] = quad(v3(0, 0, 1), v3(-W, W, W), v3(W, W, W), v3(W, -W, W), v3(-W, -W, W), white, pt::DIFFUSE);
     q[1] = quad(v3(1, 0, 0), v3(-W, -W, W), v3(-W, -W, -W), v3(-W, W, -W), v3(-W, W, W), v3(0.7f, 0.05f, 0.05f), pt::DIFFUSE);
@@ -238,6 +257,19 @@ void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
     }
     a.light = q[5];
     a.light_r2 = hdist(q[5].v0, q[5].v1) * hdist(q[5].v0, q[5].v3);
+    a.nquads = 6;
+    if (fx->prog == PT_PROG_SKY) {
+        // js/PhysicalSkyModel_FragmentShader.js:383-399: N_QUADS 4 = back, left, right walls and
+        // the floor (the Cornell ceiling and quad light are gone)
+        const pt::QuadArg floor = q[4];
+        a.qtri[6] = pt::TriArg{ floor.v0, sub(floor.v1, floor.v0), sub(floor.v2, floor.v0) };
+        a.qtri[7] = pt::TriArg{ floor.v0, sub(floor.v2, floor.v0), sub(floor.v3, floor.v0) };
+        a.qnormal[3] = floor.normal;
+        a.qcolor[3] = floor.color;
+        a.qtype[3] = floor.type;
+        a.nquads = 4;
+        sky_setup(fx, a.sky);
+    }
 }
 
 int bands_owned(const pt_ctx* c, int height)
@@ -824,6 +856,7 @@ int pt_render(pt_effect* fx, pt_texture* target)
     HIPCHK(c, hipSetDevice(c->device));
     switch (fx->prog) {
     case PT_PROG_CORNELL:
+    case PT_PROG_SKY:
     case PT_PROG_GLTF: return render_trace(fx, target);
     case PT_PROG_SCREEN_COPY: return render_copy(fx, target);
     case PT_PROG_SCREEN_OUTPUT: return render_output(fx, target);

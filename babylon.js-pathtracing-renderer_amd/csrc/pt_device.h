@@ -14,7 +14,7 @@ using namespace ptg;
 constexpr float kINF = 1000000.0f;   // #define INFINITY 1000000.0 (js/PathTracingCommon.js:329)
 constexpr float kTwoPi = 6.28318530717958648f;
 
-enum { PROG_CORNELL = 3, PROG_GLTF = 4 };
+enum { PROG_CORNELL = 3, PROG_GLTF = 4, PROG_SKY = 6 };
 // PROG_GLTF_TEX: the glTF program instantiated with its PBR / normal-map code (models with an
 // albedo or bump texture); PROG_GLTF is the same program with those branches compiled out.
 enum { PROG_GLTF_TEX = 104 };
@@ -24,6 +24,7 @@ enum { PROG_PAIRS = 1000 };
 template <int P> constexpr int kBase = P % PROG_PAIRS;
 template <int P> constexpr bool kIsGltf = kBase<P> == PROG_GLTF || kBase<P> == PROG_GLTF_TEX;
 template <int P> constexpr bool kHasTex = kBase<P> == PROG_GLTF_TEX;
+template <int P> constexpr bool kIsSky = P == PROG_SKY;
 template <int P> constexpr bool kPairs = P >= PROG_PAIRS;
 constexpr bool kIsGltfRt(int p) { return p == PROG_GLTF || p == PROG_GLTF_TEX; }
 // waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 96 -> 5; the

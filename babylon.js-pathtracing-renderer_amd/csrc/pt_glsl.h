@@ -3,30 +3,33 @@
 // (the library is built with -ffp-contract=off), correctly rounded '/' and sqrt, GLSL-spec
 // min/max/clamp/mix, and fixed range-reduction + polynomial sequences for exp2/log2/sin/cos/atan
 // built only from IEEE ops, v_floor, v_frexp_* and v_ldexp (all exact on CDNA4).
-// Everything here is __device__ code; nothing is shared with the CPU oracle except the spec.
+// These are __host__ __device__: libpt's host code evaluates the uniform-only parts of the scene
+// programs (SetupScene, the sky constants) with the very same sequences. Nothing is shared with
+// the CPU oracle except the spec.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #define PT_D __device__ __forceinline__
+#define PT_HD __host__ __device__ __forceinline__
 
 namespace ptg {
 
 constexpr float kInf = __builtin_inff();
 
-PT_D float gmin(float x, float y) { return y < x ? y : x; }
-PT_D float gmax(float x, float y) { return x < y ? y : x; }
-PT_D float gclamp(float x, float a, float b) { return gmin(gmax(x, a), b); }
-PT_D float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
-PT_D float gfract(float x) { return x - floorf(x); }
-PT_D float gmod(float x, float y) { return x - y * floorf(x / y); }
-PT_D float gsmoothstep(float e0, float e1, float x)
+PT_HD float gmin(float x, float y) { return y < x ? y : x; }
+PT_HD float gmax(float x, float y) { return x < y ? y : x; }
+PT_HD float gclamp(float x, float a, float b) { return gmin(gmax(x, a), b); }
+PT_HD float gmix(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+PT_HD float gfract(float x) { return x - floorf(x); }
+PT_HD float gmod(float x, float y) { return x - y * floorf(x / y); }
+PT_HD float gsmoothstep(float e0, float e1, float x)
 {
     float t = gclamp((x - e0) / (e1 - e0), 0.0f, 1.0f);
     return (t * t) * (3.0f - 2.0f * t);
 }
 
-PT_D float gexp2(float x)
+PT_HD float gexp2(float x)
 {
     if (x != x) return x;
     if (x >= 128.0f) return kInf;
@@ -44,7 +47,7 @@ PT_D float gexp2(float x)
     return ldexpf(p, (int)n);
 }
 
-PT_D float glog2(float x)
+PT_HD float glog2(float x)
 {
     if (x != x || x < 0.0f) return __builtin_nanf("");
     if (x == 0.0f) return -kInf;
@@ -63,11 +66,11 @@ PT_D float glog2(float x)
     return (float)e + l;
 }
 
-PT_D float gexp(float x) { return gexp2(x * 1.4426950408889634f); }
-PT_D float glog(float x) { return glog2(x) * 0.69314718055994531f; }
-PT_D float gpow(float x, float y) { return gexp2(y * glog2(x)); }
+PT_HD float gexp(float x) { return gexp2(x * 1.4426950408889634f); }
+PT_HD float glog(float x) { return glog2(x) * 0.69314718055994531f; }
+PT_HD float gpow(float x, float y) { return gexp2(y * glog2(x)); }
 
-PT_D void gsincos_reduce(float x, float& r, int& q)
+PT_HD void gsincos_reduce(float x, float& r, int& q)
 {
     float k = floorf(x * 0.63661977236758134f + 0.5f);
     float rr = x - k * 1.5703125f;
@@ -76,7 +79,7 @@ PT_D void gsincos_reduce(float x, float& r, int& q)
     r = rr;
     q = (int)(k - 4.0f * floorf(k * 0.25f));
 }
-PT_D float gsin_poly(float r)
+PT_HD float gsin_poly(float r)
 {
     float r2 = r * r;
     float p = -1.9515295891e-4f;
@@ -84,7 +87,7 @@ PT_D float gsin_poly(float r)
     p = p * r2 - 1.6666654611e-1f;
     return r + r * (r2 * p);
 }
-PT_D float gcos_poly(float r)
+PT_HD float gcos_poly(float r)
 {
     float r2 = r * r;
     float p = 2.443315711809948e-5f;
@@ -93,7 +96,7 @@ PT_D float gcos_poly(float r)
     return (1.0f - 0.5f * r2) + (r2 * r2) * p;
 }
 // sin and cos of the same angle share one reduction (the path tracer always needs both)
-PT_D void gsincos(float x, float& s, float& c)
+PT_HD void gsincos(float x, float& s, float& c)
 {
     if (!(x - x == 0.0f)) { s = c = __builtin_nanf(""); return; }
     float r; int q;
@@ -102,10 +105,10 @@ PT_D void gsincos(float x, float& s, float& c)
     s = q == 0 ? sp : q == 1 ? cp : q == 2 ? -sp : -cp;
     c = q == 0 ? cp : q == 1 ? -sp : q == 2 ? -cp : sp;
 }
-PT_D float gsin(float x) { float s, c; gsincos(x, s, c); return s; }
-PT_D float gcos(float x) { float s, c; gsincos(x, s, c); return c; }
+PT_HD float gsin(float x) { float s, c; gsincos(x, s, c); return s; }
+PT_HD float gcos(float x) { float s, c; gsincos(x, s, c); return c; }
 
-PT_D float gatan(float x)
+PT_HD float gatan(float x)
 {
     if (x != x) return x;
     float sgn = x < 0.0f ? -1.0f : 1.0f;
@@ -121,7 +124,7 @@ PT_D float gatan(float x)
     y = y + (p * z * a + a);
     return sgn * y;
 }
-PT_D float gatan2(float y, float x)
+PT_HD float gatan2(float y, float x)
 {
     if (x != x || y != y) return x + y;
     if (x == 0.0f) {
@@ -133,7 +136,7 @@ PT_D float gatan2(float y, float x)
     if (x > 0.0f) return t;
     return y < 0.0f ? t - 3.14159265358979323f : t + 3.14159265358979323f;
 }
-PT_D float gacos(float x)
+PT_HD float gacos(float x)
 {
     if (!(x >= -1.0f && x <= 1.0f)) return __builtin_nanf("");
     if (x == -1.0f) return 3.14159265358979323f;
@@ -142,32 +145,33 @@ PT_D float gacos(float x)
 
 // ------------------------------------------------------------------------------------- vec3
 struct f3 { float x, y, z; };
-PT_D f3 mk(float x, float y, float z) { return f3{ x, y, z }; }
-PT_D f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
-PT_D f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-PT_D f3 operator*(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
-PT_D f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
-PT_D f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
-PT_D float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-PT_D f3 cross(f3 a, f3 b) { return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y); }
-PT_D float length(f3 a) { return sqrtf(dot(a, a)); }
-PT_D f3 normalize(f3 a) { float inv = 1.0f / sqrtf(dot(a, a)); return a * inv; }
-PT_D float distance(f3 a, f3 b) { return length(a - b); }
-PT_D f3 reflect(f3 I, f3 N) { return I - N * (2.0f * dot(N, I)); }
-PT_D f3 refract(f3 I, f3 N, float eta)
+PT_HD f3 mk(float x, float y, float z) { return f3{ x, y, z }; }
+PT_HD f3 operator+(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+PT_HD f3 operator-(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+PT_HD f3 operator*(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+PT_HD f3 operator*(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+PT_HD f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
+PT_HD f3 operator/(f3 a, f3 b) { return mk(a.x / b.x, a.y / b.y, a.z / b.z); }
+PT_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PT_HD f3 cross(f3 a, f3 b) { return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y); }
+PT_HD float length(f3 a) { return sqrtf(dot(a, a)); }
+PT_HD f3 normalize(f3 a) { float inv = 1.0f / sqrtf(dot(a, a)); return a * inv; }
+PT_HD float distance(f3 a, f3 b) { return length(a - b); }
+PT_HD f3 reflect(f3 I, f3 N) { return I - N * (2.0f * dot(N, I)); }
+PT_HD f3 refract(f3 I, f3 N, float eta)
 {
     float d = dot(N, I);
     float k = 1.0f - eta * eta * (1.0f - d * d);
     if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
     return I * eta - N * (eta * d + sqrtf(k));
 }
-PT_D f3 mix3(f3 a, f3 b, float t) { return mk(gmix(a.x, b.x, t), gmix(a.y, b.y, t), gmix(a.z, b.z, t)); }
-PT_D f3 clamp3(f3 a, float lo, float hi) { return mk(gclamp(a.x, lo, hi), gclamp(a.y, lo, hi), gclamp(a.z, lo, hi)); }
-PT_D f3 max3s(f3 a, float s) { return mk(gmax(a.x, s), gmax(a.y, s), gmax(a.z, s)); }
+PT_HD f3 mix3(f3 a, f3 b, float t) { return mk(gmix(a.x, b.x, t), gmix(a.y, b.y, t), gmix(a.z, b.z, t)); }
+PT_HD f3 clamp3(f3 a, float lo, float hi) { return mk(gclamp(a.x, lo, hi), gclamp(a.y, lo, hi), gclamp(a.z, lo, hi)); }
+PT_HD f3 max3s(f3 a, float s) { return mk(gmax(a.x, s), gmax(a.y, s), gmax(a.z, s)); }
 
 // GLSL mat4 from Babylon Matrix.m (column-major): M * vec4(v, w)
 struct m4 { float m[16]; };
-PT_D f3 mul(const m4& M, f3 v, float w)
+PT_HD f3 mul(const m4& M, f3 v, float w)
 {
     const float* m = M.m;
     return mk(m[0] * v.x + m[4] * v.y + m[8] * v.z + m[12] * w,
@@ -175,7 +179,7 @@ PT_D f3 mul(const m4& M, f3 v, float w)
               m[2] * v.x + m[6] * v.y + m[10] * v.z + m[14] * w);
 }
 // transpose(mat3(M)) * n
-PT_D f3 mul3t(const m4& M, f3 n)
+PT_HD f3 mul3t(const m4& M, f3 n)
 {
     const float* m = M.m;
     return mk(m[0] * n.x + m[1] * n.y + m[2] * n.z,

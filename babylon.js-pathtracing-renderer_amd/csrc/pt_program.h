@@ -1,0 +1,277 @@
+// pt_program.h — the per-path part of the reference's fragment program, shared by the megakernel
+// (pt_kernels.hip: pt_trace, pt_persist) and the wavefront kernels (pt_wavefront.hip): the hit
+// record, CalculateRadiance's loop body after SceneIntersect (shadeStep), the physical sky and
+// main()'s camera ray. Everything keeps the pinned GLSL semantics of pt_glsl.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pt_args.h"
+#include "pt_device.h"
+#include "pt_glsl.h"
+
+namespace pt {
+
+// SceneIntersect's outputs (hitT, hitNormal, hitColor, hitType, hitObjectID, hit uv)
+struct Hit {
+    float t;
+    f3 normal, color;
+    float u, v;
+    int type;
+    int id;
+};
+
+struct Cnt {
+    unsigned seg, node, leaf, hit, tap, ovf;
+};
+
+// CalculateRadiance's `out` parameters objectNormal / objectColor / objectID / pixelSharpness:
+// in registers (GOut) or, for the megakernel, in LDS [field][lane] (GOutLds), which takes eight
+// live values out of the VGPR budget of the bounce loop
+struct GOut {
+    f3 nrm, col;
+    float id, sharp;
+    PT_D void clear() { nrm = mk(0, 0, 0); col = mk(0, 0, 0); id = 0.0f; sharp = 0.0f; }
+    PT_D void setNrm(f3 v) { nrm = v; }
+    PT_D void setCol(f3 v) { col = v; }
+    PT_D void setId(float v) { id = v; }
+    PT_D void setSharp(float v) { sharp = v; }
+};
+typedef __attribute__((address_space(3))) float lds_float;
+struct GOutLds {
+    lds_float* p;
+    unsigned slot;
+    PT_D void put(int f, float v) { p[f * kBlock + slot] = v; }
+    PT_D float get(int f) const { return p[f * kBlock + slot]; }
+    PT_D void clear() { for (int f = 0; f < 8; f++) put(f, 0.0f); }
+    PT_D void setNrm(f3 v) { put(0, v.x); put(1, v.y); put(2, v.z); }
+    PT_D void setCol(f3 v) { put(3, v.x); put(4, v.y); put(5, v.z); }
+    PT_D void setId(float v) { put(6, v); }
+    PT_D void setSharp(float v) { put(7, v); }
+    PT_D GOut load() const
+    {
+        GOut g;
+        g.nrm = mk(get(0), get(1), get(2)); g.col = mk(get(3), get(4), get(5)); g.id = get(6); g.sharp = get(7);
+        return g;
+    }
+};
+
+
+// CalculateRadiance: js/GLTFModelPathTracing_FragmentShader.js:351-609 and
+// js/BabylonPathTracing_FragmentShader.js:117-344 (METAL is a mirror there), as one step per
+// iteration of its `for (bounces < 6)` loop so that the persistent kernel can interleave paths.
+// The reference's per-material branches are folded so that each sampling routine has ONE call
+// site (TRANSPARENT and CLEARCOAT_DIFFUSE share the Fresnel split; CLEARCOAT's transmitted branch
+// joins DIFFUSE's "cosine bounce or light sample" tail). The sequence of rng()/blueNoise_rand()
+// draws and every IEEE op per path are exactly the GLSL's.
+struct PState {
+    f3 mask;
+    float roughness;        // metallicRoughness.g persists across bounces (:368, :496)
+    int diffuseCount, hitType, bounce;
+    bool coat, specular, sampleLight;
+};
+
+template <class G>
+PT_D void pathBegin(PState& s, G& g)
+{
+    s.mask = mk(1, 1, 1);
+    s.roughness = 0.0f;
+    s.diffuseCount = 0; s.hitType = -100; s.bounce = 0;
+    s.coat = false; s.specular = true; s.sampleLight = false;
+    g.clear();   // pinned `out` zeros
+}
+
+// Get_Sky_Color (js/PathTracingCommon.js:416-475, the three.js SkyShader Preetham model). The
+// uniform-only terms (sun intensity, extinction coefficients, sun fade, ...) come precomputed in
+// SkyArgs by the host with these same pinned sequences (pt_capi.cpp sky_setup).
+PT_D float rayleighPhase(float cosTheta) { return 0.05968310365946075f * (1.0f + (cosTheta * cosTheta)); }
+PT_HD float hgPhase(float cosTheta, float g)
+{
+    float g2 = g * g;
+    float inverse = 1.0f / gpow(gmax(0.0f, 1.0f - 2.0f * g * cosTheta + g2), 1.5f);
+    return 0.07957747154594767f * ((1.0f - g2) * inverse);
+}
+PT_D f3 pow3(f3 v, float e) { return mk(gpow(v.x, e), gpow(v.y, e), gpow(v.z, e)); }
+PT_D f3 skyColor(const SkyArgs& k, f3 rayDir)
+{
+    const f3 vd = normalize(rayDir);
+    const float cosViewSunAngle = dot(vd, k.sun);
+    const float zenithAngle = gacos(gmax(0.0f, dot(mk(0.0f, 1.0f, 0.0f), vd)));
+    const float inverse =
+        1.0f / (gcos(zenithAngle) + 0.15f * gpow(93.885f - ((zenithAngle * 180.0f) / 3.14159265358979323f), -1.253f));
+    const float rl = 8400.0f * inverse, ml = 1250.0f * inverse;
+    const f3 e = k.rayleigh * rl + k.mie * ml;
+    const f3 Fex = mk(gexp(-e.x), gexp(-e.y), gexp(-e.z));
+    const f3 betaR = k.rayleigh * rayleighPhase(cosViewSunAngle * 0.5f + 0.5f);
+    const f3 betaM = k.mie * hgPhase(cosViewSunAngle, 0.76f);
+    const f3 q = (betaR + betaM) / k.rm;
+    f3 Lin = pow3((q * k.sunE) * (mk(1.0f, 1.0f, 1.0f) - Fex), 1.5f);
+    const f3 m = pow3((q * k.sunE) * Fex, 1.0f / 2.0f);
+    Lin = Lin * mk(gmix(1.0f, m.x, k.fade), gmix(1.0f, m.y, k.fade), gmix(1.0f, m.z, k.fade));
+    f3 L0 = mk(0.1f, 0.1f, 0.1f) * Fex;
+    const float sundisk = gsmoothstep(0.9998f, 0.9998f + 0.00002f, cosViewSunAngle);
+    L0 = L0 + (Fex * k.sunE19000) * sundisk;
+    const f3 tex = (Lin + L0) * 0.04f + mk(0.0f, 0.0003f, 0.00075f);
+    return pow3(tex, k.retExp);
+}
+
+// The loop body after SceneIntersect, for the intersection `h` of the current ray. Returns false
+// when the path has ended; `accum` then holds the radiance before the final max(accum, 0).
+template <int PROG, bool COUNT, class G>
+PT_D bool shadeStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, Hit& h, Cnt& cnt)
+{
+    constexpr bool gltf = kIsGltf<PROG>;
+    constexpr bool sky = kIsSky<PROG>;
+    const int bounces = s.bounce;
+    const int prevType = s.hitType;
+    int hitType = h.type;
+    s.hitType = hitType;
+    if (h.t == kINF) {
+        if (!sky) return false;
+        // js/PhysicalSkyModel_FragmentShader.js:155-189 (with diffuseCount == 0 the path is still
+        // specular, so one of the five cases always ends it)
+        const f3 skyc = skyColor(a.sky, p.rd);
+        if (bounces == 0) { g.setSharp(1.01f); accum = skyc; }
+        else if (s.diffuseCount == 0 && s.specular) { g.setSharp(1.01f); accum = s.mask * skyc; }
+        else if (s.sampleLight) accum = s.mask * skyc;
+        else if (s.diffuseCount == 1 && prevType == TRANSPARENT && s.specular) accum = s.mask * skyc;
+        else if (s.diffuseCount > 0) accum = (s.mask * skyc) * (dot(p.rd, a.sky.sun) < 0.99f ? 1.0f : 0.0f);
+        return false;
+    }
+    f3 n = normalize(h.normal);
+    f3 nl = dot(n, p.rd) < 0.0f ? normalize(n) : normalize(-n);
+    f3 x = p.ro + p.rd * h.t;
+    if (bounces == 0) { g.setNrm(nl); g.setCol(h.color); g.setId((float)h.id); }
+    if (bounces == 1 && prevType == METAL) { g.setNrm(nl); g.setId((float)h.id); }
+
+    if (!sky && hitType == LIGHT) {   // (commented out in the sky shader)
+        if (s.diffuseCount == 0) g.setSharp(1.01f);
+        if (s.specular || s.sampleLight) accum = s.mask * h.color;
+        return false;
+    }
+    if (s.sampleLight) return false;
+
+    if (kHasTex<PROG> && hitType == PBR_MATERIAL) {
+        float tx[4];
+        texBilinear(a.albedo, h.u, h.v, tx);
+        if (COUNT) cnt.tap += 4;
+        h.color = pow22(mk(tx[0], tx[1], tx[2]));
+        f3 emission = mk(0, 0, 0);
+        if (a.uses_emissive) { texBilinear(a.emissive, h.u, h.v, tx); if (COUNT) cnt.tap += 4; emission = mk(tx[0], tx[1], tx[2]); }
+        emission = pow22(emission);
+        float maxE = gmax(emission.x, gmax(emission.y, emission.z));
+        if (s.specular && maxE > 0.01f) { g.setSharp(1.01f); accum = s.mask * emission; return false; }
+        hitType = DIFFUSE;
+        f3 mr = mk(0, 0, 0);
+        if (a.uses_metal) { texBilinear(a.metal, h.u, h.v, tx); if (COUNT) cnt.tap += 4; mr = mk(tx[0], tx[1], tx[2]); }
+        mr = pow22(mr);
+        s.roughness = mr.y;
+        if (mr.y > 0.01f) hitType = CLEARCOAT_DIFFUSE;
+        if (mr.z > 0.01f) hitType = METAL;
+        s.hitType = hitType;
+    }
+
+    const bool more = bounces + 1 < 6;
+    s.bounce = bounces + 1;
+    bool diffuseTail = hitType == DIFFUSE;
+    if (hitType == TRANSPARENT || hitType == CLEARCOAT_DIFFUSE) {
+        const bool glass = hitType == TRANSPARENT;
+        if (glass) {
+            if (s.diffuseCount == 0 && !s.coat && !a.moving) g.setSharp(1.01f);
+            else if (s.diffuseCount > 0) g.setSharp(0.0f);
+            else g.setSharp(-1.0f);
+        } else {
+            s.coat = true;
+            g.setSharp(0.0f);
+        }
+        float ratio;
+        float Re = fresnel(p.rd, glass ? n : nl, 1.0f, glass ? 1.5f : 1.4f, ratio);
+        float Tr = 1.0f - Re;
+        float P = 0.25f + (0.5f * Re);
+        float RP = Re / P, TP = Tr / (1.0f - P);
+        if (blueNoise_rand(p) < P) {            // specular reflection off the interface
+            if (!glass && s.diffuseCount == 0) g.setSharp(a.frame > 500.0f ? 1.01f : -1.0f);
+            s.mask = s.mask * RP;
+            p.rd = reflect(p.rd, nl);
+            p.ro = x + nl * a.eps;
+            return more;
+        }
+        if (glass) {                             // refraction through the dielectric
+            if (distance(n, nl) > 0.1f) {
+                const float thickness = 0.01f;
+                f3 cc = clamp3(h.color, 0.01f, 0.99f);
+                s.mask = s.mask * mk(gexp(glog(cc.x) * thickness * h.t), gexp(glog(cc.y) * thickness * h.t),
+                                     gexp(glog(cc.z) * thickness * h.t));
+            }
+            s.mask = s.mask * TP;
+            p.rd = refract(p.rd, nl, ratio);
+            p.ro = x - nl * a.eps;
+            if (s.diffuseCount == 1) s.specular = true;
+            return more;
+        }
+        s.mask = s.mask * TP;                    // clear coat transmits into its diffuse base
+        diffuseTail = true;
+    }
+    if (diffuseTail) {
+        s.diffuseCount++;
+        s.mask = s.mask * h.color;
+        s.specular = false;
+        if (s.diffuseCount == 1 && blueNoise_rand(p) < 0.5f) {
+            p.rd = cosWeightedDir(p, nl);
+        } else if (sky) {   // shadow ray into the sun's lobe (js/PhysicalSkyModel_FragmentShader.js:237-243)
+            p.rd = specularLobeDir(p, a.sky.sun, 0.1f);
+            s.mask = s.mask * (gmax(0.0f, dot(p.rd, nl)) * 0.05f);
+            if (hitType == DIFFUSE || bounces < 3) s.sampleLight = true;
+        } else {
+            float w;
+            f3 dl = sampleQuadLight(p, a, x, nl, w);
+            s.mask = s.mask * w;
+            p.rd = dl;
+            if (hitType == DIFFUSE || bounces < 3) s.sampleLight = true;
+        }
+        p.ro = x + nl * a.eps;
+        return more;
+    }
+    if (hitType == METAL) {
+        s.mask = s.mask * h.color;
+        if (gltf) p.rd = specularLobeDir(p, reflect(p.rd, nl), s.roughness);
+        else p.rd = reflect(p.rd, nl);
+        p.ro = x + nl * a.eps;
+    }
+    return more;   // any other hitType: the GLSL loop continues with the ray unchanged
+}
+
+// main()'s camera ray for pixel (px, py) (js/PathTracingCommon.js:1259-1292)
+PT_D void cameraRay(const TraceArgs& a, int px, int py, Path& p)
+{
+    const float* m = a.cam.m;
+    f3 camRight = mk(m[0], m[1], m[2]), camUp = mk(m[4], m[5], m[6]), camFwd = mk(m[8], m[9], m[10]);
+    f3 camPos = mk(m[12], m[13], m[14]);
+    float fcx = (float)px + 0.5f, fcy = (float)py + 0.5f;
+    p.s0 = (uint32_t)a.frame * (uint32_t)fcx;
+    p.s1 = (uint32_t)(a.frame + 1.0f) * (uint32_t)fcy;
+    p.counter = -1.0f;
+    int bx = (int)gmod(fcx + floorf(a.rnd[0] * 256.0f), 256.0f);
+    int by = (int)gmod(fcy + floorf(a.rnd[1] * 256.0f), 256.0f);
+    p.bn0 = 0.0f; p.bn1 = 0.0f;
+    if (bx < a.bluenoise.w && by < a.bluenoise.h) {
+        uchar4 b = a.bluenoise.p[by * a.bluenoise.w + bx];
+        p.bn0 = unorm8(b.x); p.bn1 = unorm8(b.y);
+    }
+    float ox = tentFilter(rng(p));
+    float oy = tentFilter(rng(p));
+    float ppx = ((fcx + ox) / a.res[0]) * 2.0f - 1.0f;
+    float ppy = ((fcy + oy) / a.res[1]) * 2.0f - 1.0f;
+    f3 rayDir = normalize((camRight * ppx) * a.ulen + (camUp * ppy) * a.vlen + camFwd);
+    f3 focal = rayDir * a.focus;
+    float ang = rng(p) * kTwoPi;
+    float rad = rng(p) * a.aperture;
+    float sn, cs;
+    gsincos(ang, sn, cs);
+    f3 apert = (camRight * cs + camUp * sn) * sqrtf(rad);
+    p.rd = normalize(focal - apert);
+    p.ro = camPos + apert;
+}
+
+
+} // namespace pt

@@ -28,6 +28,7 @@
 #include "pt_args.h"
 #include "pt_device.h"
 #include "pt_glsl.h"
+#include "pt_program.h"
 
 namespace pt {
 
@@ -36,16 +37,10 @@ enum Flag : unsigned {
     F_COAT = 1u << 3,        // coatTypeIntersected
     F_SPECULAR = 1u << 4,    // bounceIsSpecular
     F_SAMPLE_LIGHT = 1u << 5,
-    F_PREV_METAL = 1u << 6,  // previousIntersecType == METAL (after the PBR remap)
+    F_TYPE_SHIFT = 8,        // bits 8..15: previousIntersecType + 128 (after the PBR remap)
 };
+constexpr unsigned kTypeBias = 128u;
 
-// hit record of the current bounce, per queue slot
-struct HitRec {
-    float t;
-    int id;          // 0,1 spheres; 2..7 quads; 8 model; -1 none
-    float u, v;      // model hit uv
-    f3 n;            // hitNormal as SceneIntersect returns it
-};
 
 PT_D float u2f(unsigned u) { return __uint_as_float(u); }
 PT_D unsigned f2u(float f) { return __float_as_uint(f); }
@@ -139,7 +134,7 @@ __global__ __launch_bounds__(kBlock) void wf_raygen(TraceArgs a, WfBufs w)
     if (active) {
         w.qB[0][slot] = make_float4(p.rd.x, p.rd.y, p.rd.z, -1.0f);   // blueNoise counter starts at -1
         w.qC[0][slot] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);           // mask, roughness
-        w.qD[0][slot] = make_float4(u2f(p.s0), u2f(p.s1), u2f(F_SPECULAR), u2f(bnb));
+        w.qD[0][slot] = make_float4(u2f(p.s0), u2f(p.s1), u2f(F_SPECULAR | ((kTypeBias - 100u) << F_TYPE_SHIFT)), u2f(bnb));
     }
     if (COUNT && active) { count_add<true>(a, C_PATHS, 1); count_add<true>(a, C_RGBA8, 1); }
 }
@@ -172,7 +167,7 @@ __global__ __launch_bounds__(kBlock) void wf_extend(TraceArgs a, WfBufs w, int b
                     if (d < t) { t = d; id = s; sn = nn; }
                 }
 #pragma unroll 1
-                for (int k = 0; k < 6; k++) {
+                for (int k = 0; k < a.nquads; k++) {
                     float d = gmin(quadTriangle(a.qtri[2 * k], ro, rd), quadTriangle(a.qtri[2 * k + 1], ro, rd));
                     if (d < t) { t = d; id = 2 + k; }
                 }
@@ -292,10 +287,21 @@ __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b
 }
 
 // ============================================================================ shade (one loop iteration)
+// CalculateRadiance's G-buffer outputs go straight to the pixel's gb0 / gb1 records
+struct GOutPix {
+    float4* gb0;
+    float4* gb1;
+    unsigned pix;
+    PT_D void clear() {}
+    PT_D void setNrm(f3 v) { gb0[pix].x = v.x; gb0[pix].y = v.y; gb0[pix].z = v.z; }
+    PT_D void setCol(f3 v) { gb1[pix].x = v.x; gb1[pix].y = v.y; gb1[pix].z = v.z; }
+    PT_D void setId(float v) { gb0[pix].w = v; }
+    PT_D void setSharp(float v) { gb1[pix].w = v; }
+};
+
 template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kBlock) void wf_shade(TraceArgs a, WfBufs w, int b)
 {
-    constexpr bool gltf = kIsGltf<PROG>;
     __shared__ unsigned sh[8];
     const ShardIter it;
     const unsigned n = w.cnt[b * kShards + it.s];
@@ -315,148 +321,44 @@ __global__ __launch_bounds__(kBlock) void wf_shade(TraceArgs a, WfBufs w, int b)
             p.rd = mk(B.x, B.y, B.z);
             p.counter = B.w;
             p.s0 = f2u(D.x); p.s1 = f2u(D.y);
-            unsigned flags = f2u(D.z);
+            const unsigned flags = f2u(D.z);
             const unsigned bnb = f2u(D.w);
             p.bn0 = unorm8(bnb & 255u); p.bn1 = unorm8((bnb >> 8) & 255u);
-            f3 mask = mk(C.x, C.y, C.z);
-            float roughness = C.w;
-            int diffuseCount = (int)(flags & F_DIFFUSE_MASK);
-            bool coat = flags & F_COAT, specular = flags & F_SPECULAR, sampleLight = flags & F_SAMPLE_LIGHT;
-            const bool prevMetal = flags & F_PREV_METAL;
-            unsigned taps = 0;
-
-            const float t = H0.x;
-            const int id = (int)f2u(H0.y);
-            f3 color = mk(1.0f, 1.0f, 1.0f);
-            int hitType = -100;
-            if (id >= 0 && id < 2) { color = a.sph[id].color; hitType = a.sph[id].type; }
-            else if (id >= 2 && id < 8) { color = a.qcolor[id - 2]; hitType = a.qtype[id - 2]; }
-            else if (id == 8) hitType = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
-
-            // js/GLTFModelPathTracing_FragmentShader.js:391-602 (one iteration, `bounces` = b)
-            do {
-                if (t == kINF) break;
-                f3 nrm = normalize(mk(H1.x, H1.y, H1.z));
-                f3 nl = dot(nrm, p.rd) < 0.0f ? normalize(nrm) : normalize(-nrm);
-                f3 x = p.ro + p.rd * t;
-                if (b == 0) {
-                    w.gb0[pix] = make_float4(nl.x, nl.y, nl.z, (float)id);
-                    float4 g1 = w.gb1[pix];
-                    w.gb1[pix] = make_float4(color.x, color.y, color.z, g1.w);
-                }
-                if (b == 1 && prevMetal) w.gb0[pix] = make_float4(nl.x, nl.y, nl.z, (float)id);
-                if (hitType == LIGHT) {
-                    if (diffuseCount == 0) w.gb1[pix].w = 1.01f;
-                    if (specular || sampleLight) {
-                        f3 acc = max3s(mask * color, 0.0f);
-                        w.rad[pix] = make_float4(acc.x, acc.y, acc.z, 0.0f);
-                    }
-                    break;
-                }
-                if (sampleLight) break;
-
-                if (kHasTex<PROG> && hitType == PBR_MATERIAL) {
-                    float tx[4];
-                    texBilinear(a.albedo, H0.z, H0.w, tx);
-                    taps += 4;
-                    color = pow22(mk(tx[0], tx[1], tx[2]));
-                    f3 emission = mk(0, 0, 0);
-                    if (a.uses_emissive) { texBilinear(a.emissive, H0.z, H0.w, tx); taps += 4; emission = mk(tx[0], tx[1], tx[2]); }
-                    emission = pow22(emission);
-                    float maxE = gmax(emission.x, gmax(emission.y, emission.z));
-                    if (specular && maxE > 0.01f) {
-                        w.gb1[pix].w = 1.01f;
-                        f3 acc = max3s(mask * emission, 0.0f);
-                        w.rad[pix] = make_float4(acc.x, acc.y, acc.z, 0.0f);
-                        break;
-                    }
-                    hitType = DIFFUSE;
-                    f3 mr = mk(0, 0, 0);
-                    if (a.uses_metal) { texBilinear(a.metal, H0.z, H0.w, tx); taps += 4; mr = mk(tx[0], tx[1], tx[2]); }
-                    mr = pow22(mr);
-                    roughness = mr.y;
-                    if (mr.y > 0.01f) hitType = CLEARCOAT_DIFFUSE;
-                    if (mr.z > 0.01f) hitType = METAL;
-                }
-
-                bool diffuseTail = hitType == DIFFUSE;
-                bool next = false;
-                if (hitType == TRANSPARENT || hitType == CLEARCOAT_DIFFUSE) {
-                    const bool glass = hitType == TRANSPARENT;
-                    float sharp;
-                    if (glass) {
-                        if (diffuseCount == 0 && !coat && !a.moving) sharp = 1.01f;
-                        else if (diffuseCount > 0) sharp = 0.0f;
-                        else sharp = -1.0f;
-                    } else {
-                        coat = true;
-                        sharp = 0.0f;
-                    }
-                    float ratio;
-                    float Re = fresnel(p.rd, glass ? nrm : nl, 1.0f, glass ? 1.5f : 1.4f, ratio);
-                    float Tr = 1.0f - Re;
-                    float P = 0.25f + (0.5f * Re);
-                    float RP = Re / P, TP = Tr / (1.0f - P);
-                    if (blueNoise_rand(p) < P) {
-                        if (!glass && diffuseCount == 0) sharp = a.frame > 500.0f ? 1.01f : -1.0f;
-                        w.gb1[pix].w = sharp;
-                        mask = mask * RP;
-                        p.rd = reflect(p.rd, nl);
-                        p.ro = x + nl * a.eps;
-                        next = true;
-                    } else {
-                        w.gb1[pix].w = sharp;
-                        if (glass) {
-                            if (distance(nrm, nl) > 0.1f) {
-                                const float thickness = 0.01f;
-                                f3 cc = clamp3(color, 0.01f, 0.99f);
-                                mask = mask * mk(gexp(glog(cc.x) * thickness * t), gexp(glog(cc.y) * thickness * t),
-                                                 gexp(glog(cc.z) * thickness * t));
-                            }
-                            mask = mask * TP;
-                            p.rd = refract(p.rd, nl, ratio);
-                            p.ro = x - nl * a.eps;
-                            if (diffuseCount == 1) specular = true;
-                            next = true;
-                        } else {
-                            mask = mask * TP;
-                            diffuseTail = true;
-                        }
-                    }
-                }
-                if (!next && diffuseTail) {
-                    diffuseCount++;
-                    mask = mask * color;
-                    specular = false;
-                    if (diffuseCount == 1 && blueNoise_rand(p) < 0.5f) {
-                        p.rd = cosWeightedDir(p, nl);
-                    } else {
-                        float wgt;
-                        f3 dl = sampleQuadLight(p, a, x, nl, wgt);
-                        mask = mask * wgt;
-                        p.rd = dl;
-                        if (hitType == DIFFUSE || b < 3) sampleLight = true;
-                    }
-                    p.ro = x + nl * a.eps;
-                    next = true;
-                } else if (!next && hitType == METAL) {
-                    mask = mask * color;
-                    if (gltf) p.rd = specularLobeDir(p, reflect(p.rd, nl), roughness);
-                    else p.rd = reflect(p.rd, nl);
-                    p.ro = x + nl * a.eps;
-                    next = true;
-                }
-                // any other hitType: the GLSL loop continues with the ray unchanged
-                alive = b + 1 < 6;
-                (void)next;
-                const unsigned nf = (unsigned)diffuseCount | (coat ? F_COAT : 0u) | (specular ? F_SPECULAR : 0u) |
-                                    (sampleLight ? F_SAMPLE_LIGHT : 0u) | (hitType == METAL ? F_PREV_METAL : 0u);
+            PState s;
+            s.mask = mk(C.x, C.y, C.z);
+            s.roughness = C.w;
+            s.diffuseCount = (int)(flags & F_DIFFUSE_MASK);
+            s.hitType = (int)((flags >> F_TYPE_SHIFT) & 255u) - (int)kTypeBias;
+            s.bounce = b;
+            s.coat = flags & F_COAT; s.specular = flags & F_SPECULAR; s.sampleLight = flags & F_SAMPLE_LIGHT;
+            // the hit record SceneIntersect would have returned (wf_extend + wf_bvh)
+            Hit h;
+            h.t = H0.x;
+            h.id = (int)f2u(H0.y);
+            h.u = H0.z; h.v = H0.w;
+            h.normal = mk(H1.x, H1.y, H1.z);
+            h.color = mk(0.0f, 0.0f, 0.0f);
+            h.type = -100;
+            if (h.id >= 0 && h.id < 2) { h.color = a.sph[h.id].color; h.type = a.sph[h.id].type; }
+            else if (h.id >= 2 && h.id < 8) { h.color = a.qcolor[h.id - 2]; h.type = a.qtype[h.id - 2]; }
+            else if (h.id == 8) { h.color = mk(1.0f, 1.0f, 1.0f); h.type = a.uses_albedo ? PBR_MATERIAL : a.model_mat; }
+            GOutPix g{ w.gb0, w.gb1, pix };
+            f3 accum = mk(0, 0, 0);
+            Cnt cnt = { 0, 0, 0, 0, 0, 0 };
+            if (shadeStep<PROG, COUNT, GOutPix>(a, p, s, g, accum, h, cnt)) {
+                alive = true;
+                const unsigned nf = (unsigned)s.diffuseCount | (s.coat ? F_COAT : 0u) | (s.specular ? F_SPECULAR : 0u) |
+                                    (s.sampleLight ? F_SAMPLE_LIGHT : 0u) |
+                                    ((unsigned)(s.hitType + (int)kTypeBias) << F_TYPE_SHIFT);
                 oA = make_float4(p.ro.x, p.ro.y, p.ro.z, A.w);
                 oB = make_float4(p.rd.x, p.rd.y, p.rd.z, p.counter);
-                oC = make_float4(mask.x, mask.y, mask.z, roughness);
+                oC = make_float4(s.mask.x, s.mask.y, s.mask.z, s.roughness);
                 oD = make_float4(u2f(p.s0), u2f(p.s1), u2f(nf), D.w);
-            } while (false);
-            if (COUNT) count_add<true>(a, C_RGBA8, taps);
+            } else {
+                const f3 r = max3s(accum, 0.0f);
+                w.rad[pix] = make_float4(r.x, r.y, r.z, 0.0f);
+            }
+            if (COUNT) count_add<true>(a, C_RGBA8, cnt.tap);
         }
         const unsigned slot = shard0 + block_append(&w.cnt[(b + 1) * kShards + it.s], alive, sh);
         if (alive) {
@@ -540,6 +442,7 @@ extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceAr
     if (count) {
         switch (prog) {
         case PROG_CORNELL: WF_BOUNCE(PROG_CORNELL, true) break;
+        case PROG_SKY: WF_BOUNCE(PROG_SKY, true) break;
         case PROG_GLTF: WF_BOUNCE(PROG_GLTF, true) break;
         case PROG_GLTF_TEX: WF_BOUNCE(PROG_GLTF_TEX, true) break;
         case PROG_PAIRS + PROG_GLTF: WF_BOUNCE(PROG_PAIRS + PROG_GLTF, true) break;
@@ -549,6 +452,7 @@ extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceAr
     } else {
         switch (prog) {
         case PROG_CORNELL: WF_BOUNCE(PROG_CORNELL, false) break;
+        case PROG_SKY: WF_BOUNCE(PROG_SKY, false) break;
         case PROG_GLTF: WF_BOUNCE(PROG_GLTF, false) break;
         case PROG_GLTF_TEX: WF_BOUNCE(PROG_GLTF_TEX, false) break;
         case PROG_PAIRS + PROG_GLTF: WF_BOUNCE(PROG_PAIRS + PROG_GLTF, false) break;

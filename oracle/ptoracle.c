@@ -42,6 +42,7 @@ typedef struct {
     float counter;
     float randVec4[4];
     Quad quads[6];
+    int nquads;
     UnitSphere spheres[2];
     v3 rayOrigin, rayDirection;
     pto_counters c;
@@ -234,6 +235,19 @@ static Quad mkquad(v3 n, v3 a, v3 b, v3 c, v3 d, v3 col, int type)
 static void SetupScene(Inv* s)
 {
     const pto_frame* f = s->f;
+    if (f->scene == PTO_SCENE_SKY) {
+        /* js/PhysicalSkyModel_FragmentShader.js:383-399: N_QUADS 4 (no ceiling, no quad light) */
+        float W = 50.0f;
+        s->spheres[0].color = V3(1.0f, 1.0f, 0.0f); s->spheres[0].type = CLEARCOAT_DIFFUSE;
+        s->spheres[1].color = V3(1.0f, 1.0f, 1.0f); s->spheres[1].type = f->uRightSphereMatType;
+        s->quads[0] = mkquad(V3(0, 0, 1), V3(-W, W, W), V3(W, W, W), V3(W, -W, W), V3(-W, -W, W), V3(1.0f, 1.0f, 1.0f), DIFFUSE);
+        s->quads[1] = mkquad(V3(1, 0, 0), V3(-W, -W, W), V3(-W, -W, -W), V3(-W, W, -W), V3(-W, W, W), V3(0.7f, 0.05f, 0.05f), DIFFUSE);
+        s->quads[2] = mkquad(V3(-1, 0, 0), V3(W, -W, -W), V3(W, -W, W), V3(W, W, W), V3(W, W, -W), V3(0.05f, 0.05f, 0.7f), DIFFUSE);
+        s->quads[3] = mkquad(V3(0, 1, 0), V3(-W, -W, W), V3(W, -W, W), V3(W, -W, -W), V3(-W, -W, -W), V3(1.0f, 1.0f, 1.0f), DIFFUSE);
+        s->nquads = 4;
+        return;
+    }
+    s->nquads = 6;
     v3 light_emissionColor = v_muls(V3(1.0f, 1.0f, 1.0f), 10.0f);
     float wallRadius = 50.0f;
     float lightRadius = f->uQuadLightRadius * 0.2f;
@@ -319,7 +333,7 @@ static void SceneIntersect(Inv* s, v3 rayOrigin, v3 rayDirection, Hit* h)
         h->color = s->spheres[1].color; h->type = s->spheres[1].type; h->objectID = (float)objectCount;
     }
     objectCount++;
-    for (int i = 0; i < 6; i++) {
+    for (int i = 0; i < s->nquads; i++) {
         d = QuadIntersect(&s->quads[i], rayOrigin, rayDirection);
         if (d < h->t) {
             h->t = d;
@@ -557,6 +571,186 @@ static v3 CalculateRadiance(Inv* s, GOut* g)
     return v_maxs(accumCol, 0.0f);
 }
 
+/* ---------------------------------------------------------------- physical sky */
+/* pathtracing_physical_sky_defines / _functions, js/PathTracingCommon.js:373-477 (Preetham sky as
+ * in three.js SkyShader). Every literal is the GLSL literal rounded to f32; ops in source order. */
+#define SKY_PI 3.14159265358979323f
+#define SKY_E 2.71828182845904524f
+static float RayleighPhase(float cosTheta)
+{
+    return 0.05968310365946075f * (1.0f + (cosTheta * cosTheta));
+}
+static float hgPhase(float cosTheta, float g)
+{
+    float g2 = g * g;
+    float inverse = 1.0f / g_pow(g_max(0.0f, 1.0f - 2.0f * g * cosTheta + g2), 1.5f);
+    return 0.07957747154594767f * ((1.0f - g2) * inverse);
+}
+static v3 totalMie(void)
+{
+    float c = (0.2f * 0.5f) * 10E-18f;
+    return v_muls(V3(1.8399918514433978E14f, 2.7798023919660528E14f, 4.0790479543861094E14f), 0.434f * c);
+}
+static float SunIntensity(float zenithAngleCos)
+{
+    zenithAngleCos = g_clamp(zenithAngleCos, -1.0f, 1.0f);
+    return 200.0f * g_max(0.0f, 1.0f - g_pow(SKY_E, -((1.6110731556870734f - g_acos(zenithAngleCos)) / 1.5f)));
+}
+static v3 v_pows(v3 a, float e) { return V3(g_pow(a.x, e), g_pow(a.y, e), g_pow(a.z, e)); }
+static v3 v_exp(v3 a) { return V3(g_exp(a.x), g_exp(a.y), g_exp(a.z)); }
+static v3 v_div(v3 a, v3 b) { return V3(a.x / b.x, a.y / b.y, a.z / b.z); }
+static v3 Get_Sky_Color(const pto_frame* f, v3 rayDir)
+{
+    const v3 sun = V3(f->uSunDirection[0], f->uSunDirection[1], f->uSunDirection[2]);
+    const v3 up = V3(0.0f, 1.0f, 0.0f);
+    v3 viewDirection = v_normalize(rayDir);
+    float cosViewSunAngle = v_dot(viewDirection, sun);
+    float cosSunUpAngle = v_dot(up, sun);
+    float sunE = SunIntensity(cosSunUpAngle);
+    v3 rayleighAtX = v_muls(V3(5.804542996261093E-6f, 1.3562911419845635E-5f, 3.0265902468824876E-5f), 2.0f);
+    v3 mieAtX = v_muls(totalMie(), 0.03f);
+    float zenithAngle = g_acos(g_max(0.0f, v_dot(up, viewDirection)));
+    float inverse = 1.0f / (g_cos(zenithAngle) + 0.15f * g_pow(93.885f - ((zenithAngle * 180.0f) / SKY_PI), -1.253f));
+    float rayleighOpticalLength = 8400.0f * inverse;
+    float mieOpticalLength = 1250.0f * inverse;
+    v3 Fex = v_exp(v_neg(v_add(v_muls(rayleighAtX, rayleighOpticalLength), v_muls(mieAtX, mieOpticalLength))));
+    v3 betaRTheta = v_muls(rayleighAtX, RayleighPhase(cosViewSunAngle * 0.5f + 0.5f));
+    v3 betaMTheta = v_muls(mieAtX, hgPhase(cosViewSunAngle, 0.76f));
+    v3 ratio = v_div(v_add(betaRTheta, betaMTheta), v_add(rayleighAtX, mieAtX));
+    v3 Lin = v_pows(v_mul(v_muls(ratio, sunE), v_sub(V3(1.0f, 1.0f, 1.0f), Fex)), 1.5f);
+    v3 m = v_pows(v_mul(v_muls(ratio, sunE), Fex), 1.0f / 2.0f);
+    Lin = v_mul(Lin, v_mix(V3(1.0f, 1.0f, 1.0f), m, g_clamp(g_pow(1.0f - cosSunUpAngle, 5.0f), 0.0f, 1.0f)));
+    v3 L0 = v_mul(V3(0.1f, 0.1f, 0.1f), Fex);
+    float sundisk = g_smoothstep(0.9998f, 0.9998f + 0.00002f, cosViewSunAngle);
+    L0 = v_add(L0, v_muls(v_muls(Fex, sunE * 19000.0f), sundisk));
+    v3 texColor = v_add(v_muls(v_add(Lin, L0), 0.04f), V3(0.0f, 0.0003f, 0.00075f));
+    float sunfade = 1.0f - g_clamp(1.0f - g_exp((f->uSunDirection[1] / 450000.0f)), 0.0f, 1.0f);
+    return v_pows(texColor, 1.0f / (1.2f + (1.2f * sunfade)));
+}
+
+/* CalculateRadiance of js/PhysicalSkyModel_FragmentShader.js:119-379: misses take the sky (five
+ * cases), DIFFUSE / CLEARCOAT shadow rays go toward the sun lobe, METAL is a mirror, no quad light */
+static v3 CalculateRadianceSky(Inv* s, GOut* g)
+{
+    const pto_frame* f = s->f;
+    const v3 sun = V3(f->uSunDirection[0], f->uSunDirection[1], f->uSunDirection[2]);
+    Hit h;
+    memset(&h, 0, sizeof(h));
+    v3 accumCol = V3(0, 0, 0), mask = V3(1, 1, 1);
+    v3 x, n, nl, tdir;
+    float ratioIoR, Re, Tr, P, RP, TP, weight, thickness;
+    int diffuseCount = 0, previousIntersecType = -100, hitType = -100;
+    int coatTypeIntersected = 0, bounceIsSpecular = 1, sampleLight = 0;
+    g->objectNormal = V3(0, 0, 0); g->objectColor = V3(0, 0, 0); g->objectID = 0.0f; g->pixelSharpness = 0.0f;
+
+    for (int bounces = 0; bounces < 6; bounces++) {
+        previousIntersecType = hitType;
+        SceneIntersect(s, s->rayOrigin, s->rayDirection, &h);
+        hitType = h.type;
+        if (h.t == INFINITY_G) {
+            v3 skyColor = Get_Sky_Color(f, s->rayDirection);
+            if (bounces == 0) { g->pixelSharpness = 1.01f; accumCol = skyColor; break; }
+            else if (diffuseCount == 0 && bounceIsSpecular) { g->pixelSharpness = 1.01f; accumCol = v_mul(mask, skyColor); break; }
+            else if (sampleLight) { accumCol = v_mul(mask, skyColor); break; }
+            else if (diffuseCount == 1 && previousIntersecType == TRANSPARENT && bounceIsSpecular) { accumCol = v_mul(mask, skyColor); break; }
+            else if (diffuseCount > 0) {
+                weight = v_dot(s->rayDirection, sun) < 0.99f ? 1.0f : 0.0f;
+                accumCol = v_muls(v_mul(mask, skyColor), weight);
+                break;
+            }
+        }
+        n = v_normalize(h.normal);
+        nl = v_dot(n, s->rayDirection) < 0.0f ? v_normalize(n) : v_normalize(v_neg(n));
+        x = v_add(s->rayOrigin, v_muls(s->rayDirection, h.t));
+        if (bounces == 0) { g->objectNormal = nl; g->objectColor = h.color; g->objectID = h.objectID; }
+        if (bounces == 1 && previousIntersecType == METAL) { g->objectNormal = nl; g->objectID = h.objectID; }
+        if (sampleLight) break;
+
+        if (hitType == DIFFUSE) {
+            diffuseCount++;
+            mask = v_mul(mask, h.color);
+            bounceIsSpecular = 0;
+            if (diffuseCount == 1 && blueNoise_rand(s) < 0.5f) {
+                s->rayDirection = randomCosWeightedDirectionInHemisphere(s, nl);
+                s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
+                continue;
+            }
+            s->rayDirection = randomDirectionInSpecularLobe(s, sun, 0.1f);
+            s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
+            weight = g_max(0.0f, v_dot(s->rayDirection, nl)) * 0.05f;
+            mask = v_muls(mask, weight);
+            sampleLight = 1;
+            continue;
+        }
+        if (hitType == METAL) {
+            mask = v_mul(mask, h.color);
+            s->rayDirection = v_reflect(s->rayDirection, nl);
+            s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
+            continue;
+        }
+        if (hitType == TRANSPARENT) {
+            if (diffuseCount == 0 && !coatTypeIntersected && !f->uCameraIsMoving) g->pixelSharpness = 1.01f;
+            else if (diffuseCount > 0) g->pixelSharpness = 0.0f;
+            else g->pixelSharpness = -1.0f;
+            Re = calcFresnelReflectance(s->rayDirection, n, 1.0f, 1.5f, &ratioIoR);
+            Tr = 1.0f - Re;
+            P = 0.25f + (0.5f * Re);
+            RP = Re / P;
+            TP = Tr / (1.0f - P);
+            if (blueNoise_rand(s) < P) {
+                mask = v_muls(mask, RP);
+                s->rayDirection = v_reflect(s->rayDirection, nl);
+                s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
+                continue;
+            }
+            if (v_distance(n, nl) > 0.1f) {
+                thickness = 0.01f;
+                v3 cc = v_clamps(h.color, 0.01f, 0.99f);
+                v3 e = V3(g_exp(g_log(cc.x) * thickness * h.t), g_exp(g_log(cc.y) * thickness * h.t), g_exp(g_log(cc.z) * thickness * h.t));
+                mask = v_mul(mask, e);
+            }
+            mask = v_muls(mask, TP);
+            tdir = v_refract(s->rayDirection, nl, ratioIoR);
+            s->rayDirection = tdir;
+            s->rayOrigin = v_sub(x, v_muls(nl, f->uEPS_intersect));
+            if (diffuseCount == 1) bounceIsSpecular = 1;
+            continue;
+        }
+        if (hitType == CLEARCOAT_DIFFUSE) {
+            coatTypeIntersected = 1;
+            g->pixelSharpness = 0.0f;
+            Re = calcFresnelReflectance(s->rayDirection, nl, 1.0f, 1.4f, &ratioIoR);
+            Tr = 1.0f - Re;
+            P = 0.25f + (0.5f * Re);
+            RP = Re / P;
+            TP = Tr / (1.0f - P);
+            if (blueNoise_rand(s) < P) {
+                if (diffuseCount == 0) g->pixelSharpness = f->uFrameCounter > 500.0f ? 1.01f : -1.0f;
+                mask = v_muls(mask, RP);
+                s->rayDirection = v_reflect(s->rayDirection, nl);
+                s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
+                continue;
+            }
+            diffuseCount++;
+            mask = v_muls(mask, TP);
+            mask = v_mul(mask, h.color);
+            bounceIsSpecular = 0;
+            if (diffuseCount == 1 && blueNoise_rand(s) < 0.5f) {
+                s->rayDirection = randomCosWeightedDirectionInHemisphere(s, nl);
+                s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
+                continue;
+            }
+            s->rayDirection = randomDirectionInSpecularLobe(s, sun, 0.1f);
+            s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
+            weight = g_max(0.0f, v_dot(s->rayDirection, nl)) * 0.05f;
+            mask = v_muls(mask, weight);
+            if (bounces < 3) sampleLight = 1;
+            continue;
+        }
+    }
+    return v_maxs(accumCol, 0.0f);
+}
+
 /* ---------------------------------------------------------------- main(), part 1: per pixel */
 typedef struct { float rad[3]; float nrm[3]; float col[3]; float id; float sharp; } Shade;
 
@@ -594,7 +788,7 @@ static void shade_pixel(const pto_frame* f, int px, int py, Shade* out, pto_coun
     s.rayDirection = finalRayDir;
     SetupScene(&s);
     GOut g;
-    v3 r = CalculateRadiance(&s, &g);
+    v3 r = f->scene == PTO_SCENE_SKY ? CalculateRadianceSky(&s, &g) : CalculateRadiance(&s, &g);
     out->rad[0] = r.x; out->rad[1] = r.y; out->rad[2] = r.z;
     out->nrm[0] = g.objectNormal.x; out->nrm[1] = g.objectNormal.y; out->nrm[2] = g.objectNormal.z;
     out->col[0] = g.objectColor.x; out->col[1] = g.objectColor.y; out->col[2] = g.objectColor.z;
@@ -783,6 +977,20 @@ int pto_screen_output(int W, int H, const float* acc, float oneOverN, float expo
             }
             o[3] = 255;
         }
+    return 0;
+}
+
+/* ---------------------------------------------------------------- sky probe */
+int pto_sky_color(const float sun[3], const float* dirs, float* out, int n)
+{
+    pto_frame f;
+    memset(&f, 0, sizeof(f));
+    f.scene = PTO_SCENE_SKY;
+    f.uSunDirection[0] = sun[0]; f.uSunDirection[1] = sun[1]; f.uSunDirection[2] = sun[2];
+    for (int i = 0; i < n; i++) {
+        v3 c = Get_Sky_Color(&f, V3(dirs[3 * i], dirs[3 * i + 1], dirs[3 * i + 2]));
+        out[3 * i] = c.x; out[3 * i + 1] = c.y; out[3 * i + 2] = c.z;
+    }
     return 0;
 }
 

@@ -14,7 +14,7 @@
 extern "C" {
 #endif
 
-enum { PTO_SCENE_CORNELL = 0, PTO_SCENE_GLTF = 1 };
+enum { PTO_SCENE_CORNELL = 0, PTO_SCENE_GLTF = 1, PTO_SCENE_SKY = 2 };
 
 /* One frame's uniforms, by the names the setup scripts push (js/GLTF_Model_Path_Tracing.js:813-848,
  * js/Babylon_Path_Tracing.js:339-363). Matrices are Babylon Matrix.m (GLSL column-major). */
@@ -45,6 +45,7 @@ typedef struct pto_frame {
     const uint8_t* bump; int32_t bumpW, bumpH;
     const uint8_t* metallic; int32_t metallicW, metallicH;
     const uint8_t* emissive; int32_t emissiveW, emissiveH;
+    float uSunDirection[3];              /* sky */
 } pto_frame;
 
 typedef struct pto_counters {
@@ -65,6 +66,9 @@ int pto_path_trace(const pto_frame* f, const float* prev, float* out, int row0, 
 /* Optional G-buffer dump of the same pass (bounce-0 objectNormal/objectColor/objectID,
  * pixelSharpness and radiance), 11 floats per pixel, rows [row0,row1). */
 int pto_gbuffer(const pto_frame* f, float* gbuf, int row0, int row1, int nthreads);
+
+/* Get_Sky_Color (js/PathTracingCommon.js:416-475) for n directions (xyz triples) -> rgb triples. */
+int pto_sky_color(const float sun[3], const float* dirs, float* out, int n);
 
 /* screenOutput pass (js/PathTracingCommon.js:19-309): RGBA32F accumulation -> RGBA8 canvas. */
 int pto_screen_output(int width, int height, const float* acc, float uOneOverSampleCounter,

@@ -13,7 +13,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libptoracle.so")
 
-SCENES = {"cornell": 0, "gltf": 1}
+SCENES = {"cornell": 0, "gltf": 1, "sky": 2}
 
 c_f = ctypes.c_float
 c_i = ctypes.c_int32
@@ -41,6 +41,7 @@ class Frame(ctypes.Structure):
         ("bump", ctypes.c_void_p), ("bumpW", c_i), ("bumpH", c_i),
         ("metallic", ctypes.c_void_p), ("metallicW", c_i), ("metallicH", c_i),
         ("emissive", ctypes.c_void_p), ("emissiveW", c_i), ("emissiveH", c_i),
+        ("uSunDirection", c_f * 3),
     ]
 
 
@@ -66,6 +67,7 @@ def lib():
         L.pto_gbuffer.argtypes = [P(Frame), ctypes.c_void_p, c_i, c_i, c_i]
         L.pto_screen_output.argtypes = [c_i, c_i, ctypes.c_void_p, c_f, c_f, ctypes.c_void_p, c_i]
         L.pto_math_probe.argtypes = [c_i, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
+        L.pto_sky_color.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
         _lib = L
     return _lib
 
@@ -139,4 +141,13 @@ def math_probe(op, x, y=None):
     rc = lib().pto_math_probe(op, x.ctypes.data, None if y is None else y.ctypes.data, out.ctypes.data, x.size)
     if rc != 0:
         raise RuntimeError("bad op")
+    return out
+
+
+def sky_color(sun, dirs):
+    """Get_Sky_Color of the oracle for an (n, 3) array of ray directions."""
+    sun = np.ascontiguousarray(sun, dtype=np.float32)
+    dirs = np.ascontiguousarray(dirs, dtype=np.float32).reshape(-1, 3)
+    out = np.zeros_like(dirs)
+    lib().pto_sky_color(sun.ctypes.data, dirs.ctypes.data, out.ctypes.data, dirs.shape[0])
     return out

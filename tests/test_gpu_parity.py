@@ -119,6 +119,7 @@ def backend(request, engine):
 
 @pytest.mark.parametrize("name,frames", [
     ("cornell_256", None),
+    ("sky_256", None),
     ("gltf_teapot_320x180", None),
     ("gltf_duck_320x180", None),
     ("gltf_helmet_320x180", None),
@@ -221,7 +222,7 @@ def test_errors_are_codes_not_crashes(engine):
     import babylon_pt as bp
     with pytest.raises(bp.PtError, match="PT_ERR_SHADER"):
         bp.EffectWrapper(engine, "void main() {}", [], [], "bogus")
-    fx = bp.EffectWrapper(engine, "sky", ["uSunDirection"], ["previousBuffer"], "sky")
+    fx = bp.EffectWrapper(engine, "quadric", ["uTorusInvMatrix"], ["previousBuffer"], "quadric")
     rt = bp.RenderTargetTexture("rt", (16, 16), engine)
     with pytest.raises(bp.PtError, match="PT_ERR_UNSUPPORTED"):
         bp.EffectRenderer(engine).render(fx, rt)

@@ -30,7 +30,7 @@ def run(scene, w, h, frames, seed, model=None):
     return json.loads(out)
 
 
-@pytest.mark.parametrize("name", ["cornell_256", "gltf_teapot_320x180", "gltf_bunny_1080p", "gltf_helmet_320x180"])
+@pytest.mark.parametrize("name", ["cornell_256", "sky_256", "gltf_teapot_320x180", "gltf_bunny_1080p", "gltf_helmet_320x180"])
 def test_unmodified_setup_script_drives_the_shim(name):
     meta = H.stream(name)
     got = run(meta["scene"], meta["width"], meta["height"], len(meta["frames"]), meta["seed"], meta.get("model"))

@@ -145,3 +145,58 @@ def test_bunny_counts_plausible():
     assert cnt["paths"] == 100 * 1920
     assert 1.5 < cnt["segments"] / cnt["paths"] < 4.0
     assert cnt["node_fetches"] >= cnt["segments"]
+
+
+def _sky_f64(sun, d):
+    """Get_Sky_Color (js/PathTracingCommon.js:373-475) transcribed in float64 numpy: an independent
+    check of the oracle's f32 restatement (formula and constants), not of its rounding."""
+    sun = np.asarray(sun, np.float64)
+    d = np.asarray(d, np.float64)
+    d = d / np.linalg.norm(d, axis=1, keepdims=True)
+    up = np.array([0.0, 1.0, 0.0])
+    cos_vs = d @ sun
+    cos_su = up @ sun
+    z = np.clip(cos_su, -1.0, 1.0)
+    sunE = 200.0 * max(0.0, 1.0 - np.e ** (-((1.6110731556870734 - np.arccos(z)) / 1.5)))
+    rayleigh = np.array([5.804542996261093E-6, 1.3562911419845635E-5, 3.0265902468824876E-5]) * 2.0
+    mie = 0.434 * (0.2 * 0.5) * 10E-18 * np.array([1.8399918514433978E14, 2.7798023919660528E14, 4.0790479543861094E14]) * 0.03
+    zen = np.arccos(np.maximum(0.0, d[:, 1]))
+    inv = 1.0 / (np.cos(zen) + 0.15 * (93.885 - zen * 180.0 / np.pi) ** -1.253)
+    fex = np.exp(-(rayleigh[None] * (8400.0 * inv)[:, None] + mie[None] * (1250.0 * inv)[:, None]))
+    br = rayleigh[None] * (0.05968310365946075 * (1.0 + (cos_vs * 0.5 + 0.5) ** 2))[:, None]
+    g = 0.76
+    hg = 0.07957747154594767 * (1 - g * g) / np.maximum(0.0, 1 - 2 * g * cos_vs + g * g) ** 1.5
+    bm = mie[None] * hg[:, None]
+    q = sunE * (br + bm) / (rayleigh + mie)[None]
+    lin = (q * (1 - fex)) ** 1.5
+    t = np.clip((1.0 - cos_su) ** 5, 0, 1)
+    lin = lin * ((1 - t) + (q * fex) ** 0.5 * t)
+    x = np.clip((cos_vs - 0.9998) / 0.00002, 0, 1)
+    sundisk = x * x * (3 - 2 * x)
+    l0 = 0.1 * fex + sunE * 19000.0 * fex * sundisk[:, None]
+    tex = (lin + l0) * 0.04 + np.array([0.0, 0.0003, 0.00075])
+    sunfade = 1.0 - np.clip(1.0 - np.exp(sun[1] / 450000.0), 0, 1)
+    return tex ** (1.0 / (1.2 + 1.2 * sunfade))
+
+
+def test_sky_color_matches_float64_transcription():
+    sun = np.array(H.path_call(H.stream("sky_256")["frames"][0])["uniforms"]["uSunDirection"][1], np.float32)
+    rng = np.random.default_rng(7)
+    d = rng.normal(size=(4096, 3)).astype(np.float32)
+    d[:64] = sun + rng.normal(scale=0.004, size=(64, 3)).astype(np.float32)   # around the sun disk
+    got = po.sky_color(sun, d).astype(np.float64)
+    want = _sky_f64(sun.astype(np.float64), d.astype(np.float64))
+    assert np.all(np.isfinite(got))
+    np.testing.assert_allclose(got, want, rtol=2e-4, atol=1e-6)
+
+
+def test_sky_scene_properties():
+    """Physical-sky scene (js/PhysicalSkyModel_FragmentShader.js): rays that see the sky directly are
+    sharp (alpha 1.01) and every pixel is lit (no quad light: the sun lobe and the sky light it)."""
+    meta = H.stream("sky_256")
+    accs, cans, cnts = H.oracle_replay(meta, 1, with_output=True)
+    a = accs[0]
+    assert np.all(np.isfinite(a))
+    assert (a[..., 3] == np.float32(1.01)).mean() > 0.05
+    assert a[..., :3].min() >= 0.0 and a[..., :3].mean() > 0.1
+    assert cnts[0]["node_fetches"] == 0 and cnts[0]["segments"] > cnts[0]["paths"]
