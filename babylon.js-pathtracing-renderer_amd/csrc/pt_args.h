@@ -16,7 +16,7 @@ constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing
 #endif
 constexpr int kStackLds = PT_STACK_LDS;        // levels kept in LDS per lane; deeper levels go to a global slab
 
-enum Counter { C_PATHS, C_SEGMENTS, C_NODE, C_LEAF, C_HIT, C_RGBA8, C_OVERFLOW, C_NUM };
+enum Counter { C_PATHS, C_SEGMENTS, C_NODE, C_LEAF, C_HIT, C_RGBA8, C_OVERFLOW, C_HDR, C_NUM };
 enum ErrBits { E_STACK = 1u };
 
 // material enum of js/PathTracingCommon.js:330-350 (the subset the implemented scenes use)
@@ -41,6 +41,11 @@ struct SphereArg {          // UnitSphere + its inverse transform uniform
 
 struct Tex8 {               // RGBA8 sampler: texels row-major from row 0 (invertY applied at upload)
     const uchar4* p;
+    int w, h;
+};
+
+struct TexF {               // RGBA32F sampler (tHDRTexture), same row convention
+    const float4* p;
     int w, h;
 };
 
@@ -71,8 +76,12 @@ struct TraceArgs {
     TriArg qtri[12];
     ptg::f3 qnormal[6], qcolor[6];
     int qtype[6];
-    int nquads;             // N_QUADS: 6 (Cornell, glTF), 4 (sky: no ceiling, no quad light)
-    SkyArgs sky;
+    int nquads;             // N_QUADS: 6 (Cornell, glTF), 4 (sky, HDRI: no ceiling, no quad light)
+    SkyArgs sky;            // sky.sun is uSunDirection for the HDRI program too
+    // HDRI environment (js/HDRIEnvironmentPathTracing_FragmentShader.js:15-22)
+    TexF hdr;
+    float hdr_exposure;     // uHDRExposure
+    float sun_weight;       // uSunPower * uSunPower * 0.0000001
     QuadArg light;          // quads[5], sampled by sampleAxisAlignedQuadLight
     float light_r2;         // distance(v0,v1)*distance(v0,v3) of quads[5]
     // glTF material switches (js/GLTFModelPathTracing_FragmentShader.js:21-25)

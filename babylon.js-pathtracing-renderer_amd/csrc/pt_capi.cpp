@@ -231,7 +231,8 @@ void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
     a.sph[0].color = v3(1.0f, 1.0f, 0.0f);
     a.sph[0].type = pt::CLEARCOAT_DIFFUSE;
     a.sph[1].color = v3(1.0f, 1.0f, 1.0f);
-    a.sph[1].type = fx->prog == PT_PROG_GLTF ? pt::METAL : ui(fx, "uRightSphereMatType");
+    const bool mesh = fx->prog == PT_PROG_GLTF || fx->prog == PT_PROG_HDRI;
+    a.sph[1].type = mesh ? pt::METAL : ui(fx, "uRightSphereMatType");
     pt::QuadArg q[6];
     q[0] = quad(v3(0, 0, 1), v3(-W, W, W), v3(W, W, W), v3(W, -W, W), v3(-W, -W, W), white, pt::DIFFUSE);
     q[1] = quad(v3(1, 0, 0), v3(-W, -W, W), v3(-W, -W, -W), v3(-W, W, -W), v3(-W, W, W), v3(0.7f, 0.05f, 0.05f), pt::DIFFUSE);
@@ -258,9 +259,9 @@ void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
     a.light = q[5];
     a.light_r2 = hdist(q[5].v0, q[5].v1) * hdist(q[5].v0, q[5].v3);
     a.nquads = 6;
-    if (fx->prog == PT_PROG_SKY) {
-        // js/PhysicalSkyModel_FragmentShader.js:383-399: N_QUADS 4 = back, left, right walls and
-        // the floor (the Cornell ceiling and quad light are gone)
+    if (fx->prog == PT_PROG_SKY || fx->prog == PT_PROG_HDRI) {
+        // js/PhysicalSkyModel_FragmentShader.js:383-399, js/HDRIEnvironmentPathTracing_FragmentShader.js:529-542:
+        // N_QUADS 4 = back, left, right walls and the floor (the Cornell ceiling and quad light are gone)
         const pt::QuadArg floor = q[4];
         a.qtri[6] = pt::TriArg{ floor.v0, sub(floor.v1, floor.v0), sub(floor.v2, floor.v0) };
         a.qtri[7] = pt::TriArg{ floor.v0, sub(floor.v2, floor.v0), sub(floor.v3, floor.v0) };
@@ -268,7 +269,15 @@ void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
         a.qcolor[3] = floor.color;
         a.qtype[3] = floor.type;
         a.nquads = 4;
-        sky_setup(fx, a.sky);
+    }
+    if (fx->prog == PT_PROG_SKY) sky_setup(fx, a.sky);
+    if (fx->prog == PT_PROG_HDRI) {
+        a.sky.sun = v3(uf(fx, "uSunDirection", 0), uf(fx, "uSunDirection", 1), uf(fx, "uSunDirection", 2));
+        a.hdr_exposure = uf(fx, "uHDRExposure");
+        const float p = uf(fx, "uSunPower");
+        a.sun_weight = p * p * 0.0000001f;
+        const pt_texture* h = sampler(fx, "tHDRTexture");
+        if (h && h->kind != TEX_U8) { a.hdr.p = (const float4*)h->d; a.hdr.w = h->w; a.hdr.h = h->h; }
     }
 }
 
@@ -460,7 +469,8 @@ int render_trace(pt_effect* fx, pt_texture* target)
     a.prev = (const float4*)prev->d;
     a.out = (float4*)target->d;
     a.bluenoise = tex8(bn);
-    if (fx->prog == PT_PROG_GLTF) {
+    const bool mesh = fx->prog == PT_PROG_GLTF || fx->prog == PT_PROG_HDRI;
+    if (mesh) {
         pt_texture* bvh = sampler(fx, "tAABBTexture");
         pt_texture* tri = sampler(fx, "tTriangleTexture");
         if (!bvh || !tri || bvh->kind != TEX_F32 || tri->kind != TEX_F32)
@@ -504,10 +514,10 @@ int render_trace(pt_effect* fx, pt_texture* target)
         if (rc) return rc;
         const unsigned waves = (n_wave_tiles + c->persist_tiles - 1) / c->persist_tiles;
         const size_t lanes = (size_t)((waves + 3) / 4) * pt::kBlock;
-        if (fx->prog == PT_PROG_GLTF && (rc = spill_reserve(c, lanes))) return rc;
+        if (mesh && (rc = spill_reserve(c, lanes))) return rc;
         a.spill = c->mk_spill;
         a.spill_stride = lanes;
-    } else if (c->backend == PT_BACKEND_MEGAKERNEL && fx->prog == PT_PROG_GLTF) {
+    } else if (c->backend == PT_BACKEND_MEGAKERNEL && mesh) {
         const size_t lanes = (size_t)gx * gy * pt::kBlock;
         int rc = spill_reserve(c, lanes);
         if (rc) return rc;
@@ -857,6 +867,7 @@ int pt_render(pt_effect* fx, pt_texture* target)
     switch (fx->prog) {
     case PT_PROG_CORNELL:
     case PT_PROG_SKY:
+    case PT_PROG_HDRI:
     case PT_PROG_GLTF: return render_trace(fx, target);
     case PT_PROG_SCREEN_COPY: return render_copy(fx, target);
     case PT_PROG_SCREEN_OUTPUT: return render_output(fx, target);
@@ -964,7 +975,7 @@ int pt_set_counting(pt_ctx* c, int enable)
     return PT_OK;
 }
 
-int pt_read_counters(pt_ctx* c, uint64_t out[7])
+int pt_read_counters(pt_ctx* c, uint64_t out[PT_NUM_COUNTERS])
 {
     if (!c || !out) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));

@@ -14,19 +14,33 @@ using namespace ptg;
 constexpr float kINF = 1000000.0f;   // #define INFINITY 1000000.0 (js/PathTracingCommon.js:329)
 constexpr float kTwoPi = 6.28318530717958648f;
 
-enum { PROG_CORNELL = 3, PROG_GLTF = 4, PROG_SKY = 6 };
-// PROG_GLTF_TEX: the glTF program instantiated with its PBR / normal-map code (models with an
-// albedo or bump texture); PROG_GLTF is the same program with those branches compiled out.
-enum { PROG_GLTF_TEX = 104 };
+enum { PROG_CORNELL = 3, PROG_GLTF = 4, PROG_HDRI = 5, PROG_SKY = 6 };
+// PROG_GLTF_TEX / PROG_HDRI_TEX: the mesh programs instantiated with their PBR / normal-map code
+// (models with an albedo or bump texture); without +PROG_TEX those branches are compiled out.
+enum { PROG_TEX = 100, PROG_GLTF_TEX = 104, PROG_HDRI_TEX = 105 };
 // +PROG_PAIRS: the same programs walking the child-pair BVH records (bvhWalkPairs) instead of the
 // reference's texel pairs (bvhWalkRef); chosen per draw by the host (pt_capi.cpp ensure_pairs)
 enum { PROG_PAIRS = 1000 };
 template <int P> constexpr int kBase = P % PROG_PAIRS;
-template <int P> constexpr bool kIsGltf = kBase<P> == PROG_GLTF || kBase<P> == PROG_GLTF_TEX;
-template <int P> constexpr bool kHasTex = kBase<P> == PROG_GLTF_TEX;
+template <int P> constexpr int kScene = kBase<P> % PROG_TEX;
+// the mesh programs (BVH walk, PBR materials): glTF and HDRI
+template <int P> constexpr bool kIsGltf = kScene<P> == PROG_GLTF || kScene<P> == PROG_HDRI;
+template <int P> constexpr bool kIsHdri = kScene<P> == PROG_HDRI;
+template <int P> constexpr bool kHasTex = kBase<P> >= PROG_TEX;
 template <int P> constexpr bool kIsSky = P == PROG_SKY;
 template <int P> constexpr bool kPairs = P >= PROG_PAIRS;
-constexpr bool kIsGltfRt(int p) { return p == PROG_GLTF || p == PROG_GLTF_TEX; }
+// every instantiated program variant
+#define PT_FOR_EACH_PROG(X)                                                                           \
+    X(PROG_CORNELL) X(PROG_SKY) X(PROG_GLTF) X(PROG_GLTF_TEX) X(PROG_HDRI) X(PROG_HDRI_TEX)           \
+    X(PROG_PAIRS + PROG_GLTF) X(PROG_PAIRS + PROG_GLTF_TEX) X(PROG_PAIRS + PROG_HDRI) X(PROG_PAIRS + PROG_HDRI_TEX)
+
+// the kernel variant of a draw: the scene program, +PROG_TEX when the model carries albedo / bump
+// maps, +PROG_PAIRS when the BVH walk uses child-pair records
+__host__ __device__ inline int resolveProgram(int prog, bool textured, bool pairs)
+{
+    if (prog != PROG_GLTF && prog != PROG_HDRI) return prog;
+    return prog + (textured ? PROG_TEX : 0) + (pairs ? PROG_PAIRS : 0);
+}
 // waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 96 -> 5; the
 // textured variant keeps 2 rather than spill)
 // (measured on bunny 1080p: the child-pair walk gains 5-7% at 5 waves, the reference walk loses)
@@ -204,6 +218,23 @@ PT_D void texBilinear(const Tex8& t, float u, float v, float out[4])
     out[1] = gmix(gmix(unorm8(t00.y), unorm8(t10.y), ax), gmix(unorm8(t01.y), unorm8(t11.y), ax), by);
     out[2] = gmix(gmix(unorm8(t00.z), unorm8(t10.z), ax), gmix(unorm8(t01.z), unorm8(t11.z), ax), by);
     out[3] = gmix(gmix(unorm8(t00.w), unorm8(t10.w), ax), gmix(unorm8(t01.w), unorm8(t11.w), ax), by);
+}
+
+// texture(tHDRTexture, uv) on RGBA32F texels: LOD 0 bilinear, REPEAT (as texBilinear)
+PT_D float4 texBilinearF(const TexF& t, float u, float v)
+{
+    if (!t.p || t.w <= 0 || t.h <= 0) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float x = u * (float)t.w - 0.5f, y = v * (float)t.h - 0.5f;
+    float fx = floorf(x), fy = floorf(y);
+    float ax = x - fx, by = y - fy;
+    int x0 = wrapTexel(fx, t.w), y0 = wrapTexel(fy, t.h);
+    int x1 = x0 + 1 == t.w ? 0 : x0 + 1, y1 = y0 + 1 == t.h ? 0 : y0 + 1;
+    const float4 t00 = t.p[(size_t)y0 * t.w + x0], t10 = t.p[(size_t)y0 * t.w + x1];
+    const float4 t01 = t.p[(size_t)y1 * t.w + x0], t11 = t.p[(size_t)y1 * t.w + x1];
+    return make_float4(gmix(gmix(t00.x, t10.x, ax), gmix(t01.x, t11.x, ax), by),
+                       gmix(gmix(t00.y, t10.y, ax), gmix(t01.y, t11.y, ax), by),
+                       gmix(gmix(t00.z, t10.z, ax), gmix(t01.z, t11.z, ax), by),
+                       gmix(gmix(t00.w, t10.w, ax), gmix(t01.w, t11.w, ax), by));
 }
 
 PT_D f3 pow22(f3 c) { return mk(gpow(c.x, 2.2f), gpow(c.y, 2.2f), gpow(c.z, 2.2f)); }

@@ -175,7 +175,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
     // lanes whose whole 2x2 quad lies beyond the (even-rounded) target do no work; quad helpers
     // that only complete a quad at an odd edge are shaded like GL helper invocations
     const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1);
-    Cnt cnt = { 0, 0, 0, 0, 0, 0 };
+    Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
     GOutLds gl{ (lds_float*)lds_gout, tid };
     gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
     f3 r = mk(0, 0, 0);
@@ -212,6 +212,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
         atomicAdd(&C[C_HIT], (unsigned long long)cnt.hit);
         atomicAdd(&C[C_RGBA8], (unsigned long long)(cnt.tap + 1));
         atomicAdd(&C[C_OVERFLOW], (unsigned long long)cnt.ovf);
+        atomicAdd(&C[C_HDR], (unsigned long long)cnt.hdr);
     }
     if (px >= a.width || py >= a.height) return;   // quad helper outside the target
 
@@ -235,18 +236,11 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
     a.out[pi] = make_float4(prev.x + cr, prev.y + cg, prev.z + cb, ca);
 }
 
-template __global__ void pt_trace<PROG_CORNELL, false>(TraceArgs);
-template __global__ void pt_trace<PROG_CORNELL, true>(TraceArgs);
-template __global__ void pt_trace<PROG_SKY, false>(TraceArgs);
-template __global__ void pt_trace<PROG_SKY, true>(TraceArgs);
-template __global__ void pt_trace<PROG_GLTF, false>(TraceArgs);
-template __global__ void pt_trace<PROG_GLTF, true>(TraceArgs);
-template __global__ void pt_trace<PROG_GLTF_TEX, false>(TraceArgs);
-template __global__ void pt_trace<PROG_GLTF_TEX, true>(TraceArgs);
-template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF, false>(TraceArgs);
-template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF, true>(TraceArgs);
-template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF_TEX, false>(TraceArgs);
-template __global__ void pt_trace<PROG_PAIRS + PROG_GLTF_TEX, true>(TraceArgs);
+#define PT_TRACE_INST(P)                                     \
+    template __global__ void pt_trace<P, false>(TraceArgs); \
+    template __global__ void pt_trace<P, true>(TraceArgs);
+PT_FOR_EACH_PROG(PT_TRACE_INST)
+#undef PT_TRACE_INST
 
 // ------------------------------------------------------------------------------ persistent paths
 // pt_persist<PROG,COUNT>: the same per-pixel program with path regeneration. A wave owns a list
@@ -268,7 +262,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_persist(TraceArgs 
     unsigned next = wid * per_wave * 64u;
     const unsigned end = min(next + per_wave * 64u, n_wave_tiles * 64u);
     float2* deep = a.spill + (size_t)blockIdx.x * kBlock + tid;
-    Cnt cnt = { 0, 0, 0, 0, 0, 0 };
+    Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
     unsigned paths = 0;
     Path p;
     PState s;
@@ -324,18 +318,14 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_persist(TraceArgs 
         atomicAdd(&C[C_HIT], (unsigned long long)cnt.hit);
         atomicAdd(&C[C_RGBA8], (unsigned long long)(cnt.tap + paths));
         atomicAdd(&C[C_OVERFLOW], (unsigned long long)cnt.ovf);
+        atomicAdd(&C[C_HDR], (unsigned long long)cnt.hdr);
     }
 }
 
 #define PT_PERSIST_INST(P)                                                                          \
     template __global__ void pt_persist<P, false>(TraceArgs, WfBufs, int, unsigned, unsigned, unsigned); \
     template __global__ void pt_persist<P, true>(TraceArgs, WfBufs, int, unsigned, unsigned, unsigned);
-PT_PERSIST_INST(PROG_CORNELL)
-PT_PERSIST_INST(PROG_SKY)
-PT_PERSIST_INST(PROG_GLTF)
-PT_PERSIST_INST(PROG_GLTF_TEX)
-PT_PERSIST_INST(PROG_PAIRS + PROG_GLTF)
-PT_PERSIST_INST(PROG_PAIRS + PROG_GLTF_TEX)
+PT_FOR_EACH_PROG(PT_PERSIST_INST)
 #undef PT_PERSIST_INST
 
 // ------------------------------------------------------------------------------ screenCopy
@@ -559,49 +549,39 @@ extern "C" {
 hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s)
 {
     dim3 grid(grid_x, grid_y), block(pt::kBlock);
-    // texture-free glTF models (the bench's StanfordBunny) take the variant without PBR code
-    if (prog == pt::PROG_GLTF && (a->uses_albedo || a->uses_bump)) prog = pt::PROG_GLTF_TEX;
-    if (pt::kIsGltfRt(prog) && a->bvh_pairs) prog += pt::PROG_PAIRS;
-#define PT_LAUNCH(P)                                                                              \
-    do {                                                                                          \
-        if (count) hipLaunchKernelGGL((pt::pt_trace<P, true>), grid, block, 0, s, *a);             \
-        else hipLaunchKernelGGL((pt::pt_trace<P, false>), grid, block, 0, s, *a);                  \
-    } while (0)
+    // texture-free models (the bench's StanfordBunny) take the variant without PBR code
+    prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr);
+#define PT_CASE(P)                                                                                  \
+    case P:                                                                                          \
+        if (count) hipLaunchKernelGGL((pt::pt_trace<P, true>), grid, block, 0, s, *a);               \
+        else hipLaunchKernelGGL((pt::pt_trace<P, false>), grid, block, 0, s, *a);                    \
+        break;
+    using namespace pt;
     switch (prog) {
-    case pt::PROG_CORNELL: PT_LAUNCH(pt::PROG_CORNELL); break;
-    case pt::PROG_SKY: PT_LAUNCH(pt::PROG_SKY); break;
-    case pt::PROG_GLTF: PT_LAUNCH(pt::PROG_GLTF); break;
-    case pt::PROG_GLTF_TEX: PT_LAUNCH(pt::PROG_GLTF_TEX); break;
-    case pt::PROG_PAIRS + pt::PROG_GLTF: PT_LAUNCH(pt::PROG_PAIRS + pt::PROG_GLTF); break;
-    case pt::PROG_PAIRS + pt::PROG_GLTF_TEX: PT_LAUNCH(pt::PROG_PAIRS + pt::PROG_GLTF_TEX); break;
+        PT_FOR_EACH_PROG(PT_CASE)
     default: return hipErrorInvalidValue;
     }
-#undef PT_LAUNCH
+#undef PT_CASE
     return hipGetLastError();
 }
 
 hipError_t pt_launch_persist(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x,
                              unsigned n_wave_tiles, unsigned per_wave, unsigned refill, hipStream_t s)
 {
-    if (prog == pt::PROG_GLTF && (a->uses_albedo || a->uses_bump)) prog = pt::PROG_GLTF_TEX;
-    if (pt::kIsGltfRt(prog) && a->bvh_pairs) prog += pt::PROG_PAIRS;
+    prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr);
     const unsigned waves = (n_wave_tiles + per_wave - 1) / per_wave;
     dim3 grid((waves + 3) / 4), block(pt::kBlock);
-#define PT_LAUNCH(P)                                                                                          \
-    do {                                                                                                      \
+#define PT_CASE(P)                                                                                          \
+    case P:                                                                                                  \
         if (count) hipLaunchKernelGGL((pt::pt_persist<P, true>), grid, block, 0, s, *a, *w, tiles_x, n_wave_tiles, per_wave, refill); \
         else hipLaunchKernelGGL((pt::pt_persist<P, false>), grid, block, 0, s, *a, *w, tiles_x, n_wave_tiles, per_wave, refill); \
-    } while (0)
+        break;
+    using namespace pt;
     switch (prog) {
-    case pt::PROG_CORNELL: PT_LAUNCH(pt::PROG_CORNELL); break;
-    case pt::PROG_SKY: PT_LAUNCH(pt::PROG_SKY); break;
-    case pt::PROG_GLTF: PT_LAUNCH(pt::PROG_GLTF); break;
-    case pt::PROG_GLTF_TEX: PT_LAUNCH(pt::PROG_GLTF_TEX); break;
-    case pt::PROG_PAIRS + pt::PROG_GLTF: PT_LAUNCH(pt::PROG_PAIRS + pt::PROG_GLTF); break;
-    case pt::PROG_PAIRS + pt::PROG_GLTF_TEX: PT_LAUNCH(pt::PROG_PAIRS + pt::PROG_GLTF_TEX); break;
+        PT_FOR_EACH_PROG(PT_CASE)
     default: return hipErrorInvalidValue;
     }
-#undef PT_LAUNCH
+#undef PT_CASE
     return hipGetLastError();
 }
 

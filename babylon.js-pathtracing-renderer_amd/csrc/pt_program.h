@@ -22,7 +22,7 @@ struct Hit {
 };
 
 struct Cnt {
-    unsigned seg, node, leaf, hit, tap, ovf;
+    unsigned seg, node, leaf, hit, tap, ovf, hdr;
 };
 
 // CalculateRadiance's `out` parameters objectNormal / objectColor / objectID / pixelSharpness:
@@ -115,6 +115,17 @@ PT_D f3 skyColor(const SkyArgs& k, f3 rayDir)
     return pow3(tex, k.retExp);
 }
 
+// Get_HDR_Color (js/HDRIEnvironmentPathTracing_FragmentShader.js:236-245): equirect lookup
+template <bool COUNT>
+PT_D f3 envColor(const TraceArgs& a, f3 rd, Cnt& cnt)
+{
+    const float u = gatan2(rd.x, rd.z) * 0.15915494309f + 0.5f;   // ONE_OVER_TWO_PI as the GLSL spells it
+    const float v = gacos(-rd.y) * 0.31830988618379067f;
+    const float4 t = texBilinearF(a.hdr, u, v);
+    if (COUNT) cnt.hdr += 4;
+    return mk(t.x, t.y, t.z) * a.hdr_exposure;
+}
+
 // The loop body after SceneIntersect, for the intersection `h` of the current ray. Returns false
 // when the path has ended; `accum` then holds the radiance before the final max(accum, 0).
 template <int PROG, bool COUNT, class G>
@@ -122,11 +133,23 @@ PT_D bool shadeStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, Hit
 {
     constexpr bool gltf = kIsGltf<PROG>;
     constexpr bool sky = kIsSky<PROG>;
+    constexpr bool hdri = kIsHdri<PROG>;
     const int bounces = s.bounce;
     const int prevType = s.hitType;
     int hitType = h.type;
     s.hitType = hitType;
     if (h.t == kINF) {
+        if (hdri) {   // js/HDRIEnvironmentPathTracing_FragmentShader.js:288-323 (always ends the path)
+            const f3 env = envColor<COUNT>(a, p.rd, cnt);
+            if (bounces == 0) { g.setSharp(1.01f); accum = env; }
+            else if (s.diffuseCount == 0 && s.specular) { g.setSharp(1.01f); accum = s.mask * env; }
+            else if (s.sampleLight) accum = s.mask * env;
+            else if (s.diffuseCount == 1 && prevType == TRANSPARENT && s.specular && bounces < 3) {
+                if (dot(p.rd, a.sky.sun) > 0.99f) g.setSharp(1.01f);
+                accum = s.mask * env;
+            } else if (s.diffuseCount > 0) accum = (s.mask * env) * (dot(p.rd, a.sky.sun) < 0.99f ? 1.0f : 0.0f);
+            return false;
+        }
         if (!sky) return false;
         // js/PhysicalSkyModel_FragmentShader.js:155-189 (with diffuseCount == 0 the path is still
         // specular, so one of the five cases always ends it)
@@ -144,7 +167,7 @@ PT_D bool shadeStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, Hit
     if (bounces == 0) { g.setNrm(nl); g.setCol(h.color); g.setId((float)h.id); }
     if (bounces == 1 && prevType == METAL) { g.setNrm(nl); g.setId((float)h.id); }
 
-    if (!sky && hitType == LIGHT) {   // (commented out in the sky shader)
+    if (!sky && !hdri && hitType == LIGHT) {   // (commented out / removed in the sky and HDRI shaders)
         if (s.diffuseCount == 0) g.setSharp(1.01f);
         if (s.specular || s.sampleLight) accum = s.mask * h.color;
         return false;
@@ -216,8 +239,12 @@ PT_D bool shadeStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, Hit
         s.diffuseCount++;
         s.mask = s.mask * h.color;
         s.specular = false;
-        if (s.diffuseCount == 1 && blueNoise_rand(p) < 0.5f) {
+        if ((hdri ? s.diffuseCount <= 2 : s.diffuseCount == 1) && blueNoise_rand(p) < 0.5f) {
             p.rd = cosWeightedDir(p, nl);
+        } else if (hdri) {   // shadow ray into the sun's lobe (js/HDRIEnvironmentPathTracing_FragmentShader.js:395-400)
+            p.rd = specularLobeDir(p, a.sky.sun, 0.03f);
+            s.mask = s.mask * (gmax(0.0f, dot(p.rd, nl)) * a.sun_weight);
+            if (hitType == DIFFUSE || bounces < 3) s.sampleLight = true;
         } else if (sky) {   // shadow ray into the sun's lobe (js/PhysicalSkyModel_FragmentShader.js:237-243)
             p.rd = specularLobeDir(p, a.sky.sun, 0.1f);
             s.mask = s.mask * (gmax(0.0f, dot(p.rd, nl)) * 0.05f);

@@ -344,7 +344,7 @@ __global__ __launch_bounds__(kBlock) void wf_shade(TraceArgs a, WfBufs w, int b)
             else if (h.id == 8) { h.color = mk(1.0f, 1.0f, 1.0f); h.type = a.uses_albedo ? PBR_MATERIAL : a.model_mat; }
             GOutPix g{ w.gb0, w.gb1, pix };
             f3 accum = mk(0, 0, 0);
-            Cnt cnt = { 0, 0, 0, 0, 0, 0 };
+            Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
             if (shadeStep<PROG, COUNT, GOutPix>(a, p, s, g, accum, h, cnt)) {
                 alive = true;
                 const unsigned nf = (unsigned)s.diffuseCount | (s.coat ? F_COAT : 0u) | (s.specular ? F_SPECULAR : 0u) |
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(kBlock) void wf_shade(TraceArgs a, WfBufs w, int b)
                 const f3 r = max3s(accum, 0.0f);
                 w.rad[pix] = make_float4(r.x, r.y, r.z, 0.0f);
             }
-            if (COUNT) count_add<true>(a, C_RGBA8, cnt.tap);
+            if (COUNT) { count_add<true>(a, C_RGBA8, cnt.tap); count_add<true>(a, C_HDR, cnt.hdr); }
         }
         const unsigned slot = shard0 + block_append(&w.cnt[(b + 1) * kShards + it.s], alive, sh);
         if (alive) {
@@ -428,8 +428,7 @@ extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceAr
                                           int tiles_x, int bands, int persist_blocks, hipStream_t s)
 {
     using namespace pt;
-    if (prog == PROG_GLTF && (a->uses_albedo || a->uses_bump)) prog = PROG_GLTF_TEX;
-    if (kIsGltfRt(prog) && a->bvh_pairs) prog += PROG_PAIRS;
+    prog = resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr);
     dim3 tiles(tiles_x, bands), blk(kBlock);
     if (count) hipLaunchKernelGGL((wf_raygen<true>), tiles, blk, 0, s, *a, *w);
     else hipLaunchKernelGGL((wf_raygen<false>), tiles, blk, 0, s, *a, *w);
@@ -439,27 +438,21 @@ extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceAr
         if (kIsGltf<P>) hipLaunchKernelGGL((wf_bvh<P, C>), dim3(persist_blocks), blk, 0, s, *a, *w, b); \
         hipLaunchKernelGGL((wf_shade<P, C>), dim3(persist_blocks), blk, 0, s, *a, *w, b);          \
     }
+#define WF_CASE_T(P) case P: WF_BOUNCE(P, true) break;
+#define WF_CASE_F(P) case P: WF_BOUNCE(P, false) break;
     if (count) {
         switch (prog) {
-        case PROG_CORNELL: WF_BOUNCE(PROG_CORNELL, true) break;
-        case PROG_SKY: WF_BOUNCE(PROG_SKY, true) break;
-        case PROG_GLTF: WF_BOUNCE(PROG_GLTF, true) break;
-        case PROG_GLTF_TEX: WF_BOUNCE(PROG_GLTF_TEX, true) break;
-        case PROG_PAIRS + PROG_GLTF: WF_BOUNCE(PROG_PAIRS + PROG_GLTF, true) break;
-        case PROG_PAIRS + PROG_GLTF_TEX: WF_BOUNCE(PROG_PAIRS + PROG_GLTF_TEX, true) break;
+            PT_FOR_EACH_PROG(WF_CASE_T)
         default: return hipErrorInvalidValue;
         }
     } else {
         switch (prog) {
-        case PROG_CORNELL: WF_BOUNCE(PROG_CORNELL, false) break;
-        case PROG_SKY: WF_BOUNCE(PROG_SKY, false) break;
-        case PROG_GLTF: WF_BOUNCE(PROG_GLTF, false) break;
-        case PROG_GLTF_TEX: WF_BOUNCE(PROG_GLTF_TEX, false) break;
-        case PROG_PAIRS + PROG_GLTF: WF_BOUNCE(PROG_PAIRS + PROG_GLTF, false) break;
-        case PROG_PAIRS + PROG_GLTF_TEX: WF_BOUNCE(PROG_PAIRS + PROG_GLTF_TEX, false) break;
+            PT_FOR_EACH_PROG(WF_CASE_F)
         default: return hipErrorInvalidValue;
         }
     }
+#undef WF_CASE_T
+#undef WF_CASE_F
 #undef WF_BOUNCE
     hipLaunchKernelGGL(wf_finish, tiles, blk, 0, s, *a, *w);
     return hipGetLastError();

@@ -297,10 +297,10 @@ static napi_value SetCounting(napi_env env, napi_callback_info info)
 static napi_value ReadCounters(napi_env env, napi_callback_info info)
 {
     napi_value a[MAXARGS], r; if (args(env, info, a, 1) < 0) return NULL;
-    uint64_t c[7] = { 0 };
+    uint64_t c[PT_NUM_COUNTERS] = { 0 };
     pt_read_counters((pt_ctx*)handle(env, a[0]), c);
-    CHECK(napi_create_array_with_length(env, 7, &r));
-    for (uint32_t i = 0; i < 7; i++) napi_set_element(env, r, i, num(env, (double)c[i]));
+    CHECK(napi_create_array_with_length(env, PT_NUM_COUNTERS, &r));
+    for (uint32_t i = 0; i < PT_NUM_COUNTERS; i++) napi_set_element(env, r, i, num(env, (double)c[i]));
     return r;
 }
 static napi_value ResetCounters(napi_env env, napi_callback_info info)

@@ -172,9 +172,10 @@ class Engine:
         self.check(lib().pt_reset_counters(self.ctx))
 
     def counters(self):
-        buf = (ctypes.c_uint64 * 7)()
+        keys = ("paths", "segments", "node_fetches", "leaf_tests", "hit_lookups", "rgba8_taps", "stack_overflow",
+                "hdr_taps")
+        buf = (ctypes.c_uint64 * len(keys))()
         self.check(lib().pt_read_counters(self.ctx, buf), "pt_read_counters")
-        keys = ("paths", "segments", "node_fetches", "leaf_tests", "hit_lookups", "rgba8_taps", "stack_overflow")
         return {k: int(v) for k, v in zip(keys, buf)}
 
     def queue_stats(self):
@@ -393,7 +394,13 @@ class StreamPlayer:
         self.textures["file:BlueNoise_RGBA256.png"] = Texture(engine, bluenoise, name="blueNoise")
         if mesh is not None:
             for raw, kind in meta["textures"].items():
-                self.textures[raw] = RawTexture.CreateRGBATexture(mesh[kind], 2048, 2048, engine, name=kind)
+                if kind == "hdr":   # the environment: its own size, uploaded with invertY as the script does
+                    hd = meta["hdr"]
+                    self.textures[raw] = RawTexture.CreateRGBATexture(mesh[kind], hd["width"], hd["height"], engine,
+                                                                      invertY=hd["invertY"], samplingMode=TRILINEAR,
+                                                                      name=kind)
+                else:
+                    self.textures[raw] = RawTexture.CreateRGBATexture(mesh[kind], 2048, 2048, engine, name=kind)
         self.renderer = EffectRenderer(engine)
         self.wrappers = {}
         for call in meta["frames"][0]:

@@ -153,9 +153,10 @@ int pt_last_render_ms(pt_ctx* ctx, int program, float* ms);
 int pt_timing_begin(pt_ctx* ctx);
 int pt_timing_end(pt_ctx* ctx, int program, double* total_ms, int* launches);
 /* Algorithmic-byte counters: when enabled, path-tracing passes also accumulate
- * {paths, segments, node_fetches, leaf_tests, hit_lookups, rgba8_taps, stack_overflow}. */
+ * {paths, segments, node_fetches, leaf_tests, hit_lookups, rgba8_taps, stack_overflow, hdr_taps}. */
+#define PT_NUM_COUNTERS 8
 int pt_set_counting(pt_ctx* ctx, int enable);
-int pt_read_counters(pt_ctx* ctx, uint64_t out[7]);
+int pt_read_counters(pt_ctx* ctx, uint64_t out[PT_NUM_COUNTERS]);
 int pt_reset_counters(pt_ctx* ctx);
 /* Wavefront queue statistics of the last path-tracing draw (synchronises): out[b] = paths entering
  * bounce b (b = 0..6), out[8 + b] = rays handed to the BVH walk at bounce b (b = 0..5). */

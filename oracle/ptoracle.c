@@ -227,6 +227,22 @@ static void tex_bilinear(const uint8_t* t, int w, int h, float u, float v, float
     }
 }
 
+/* texture(sampler, uv) on an RGBA32F map (tHDRTexture): LOD 0 bilinear, REPEAT wrap */
+static void tex_bilinear_f(const float* t, int w, int h, float u, float v, float out[4])
+{
+    if (!t || w <= 0 || h <= 0) { out[0] = out[1] = out[2] = out[3] = 0.0f; return; }
+    float x = u * (float)w - 0.5f, y = v * (float)h - 0.5f;
+    float fx = floorf(x), fy = floorf(y);
+    float ax = x - fx, by = y - fy;
+    int x0 = wrap_texel(fx, w), y0 = wrap_texel(fy, h);
+    int x1 = x0 + 1 == w ? 0 : x0 + 1, y1 = y0 + 1 == h ? 0 : y0 + 1;
+    const float* t00 = t + 4 * ((size_t)y0 * w + x0);
+    const float* t10 = t + 4 * ((size_t)y0 * w + x1);
+    const float* t01 = t + 4 * ((size_t)y1 * w + x0);
+    const float* t11 = t + 4 * ((size_t)y1 * w + x1);
+    for (int k = 0; k < 4; k++) out[k] = g_mix(g_mix(t00[k], t10[k], ax), g_mix(t01[k], t11[k], ax), by);
+}
+
 /* ---------------------------------------------------------------- scene setup */
 static Quad mkquad(v3 n, v3 a, v3 b, v3 c, v3 d, v3 col, int type)
 {
@@ -235,11 +251,13 @@ static Quad mkquad(v3 n, v3 a, v3 b, v3 c, v3 d, v3 col, int type)
 static void SetupScene(Inv* s)
 {
     const pto_frame* f = s->f;
-    if (f->scene == PTO_SCENE_SKY) {
-        /* js/PhysicalSkyModel_FragmentShader.js:383-399: N_QUADS 4 (no ceiling, no quad light) */
+    if (f->scene == PTO_SCENE_SKY || f->scene == PTO_SCENE_HDRI) {
+        /* js/PhysicalSkyModel_FragmentShader.js:383-399 and
+         * js/HDRIEnvironmentPathTracing_FragmentShader.js:529-542: N_QUADS 4 (no ceiling, no quad light) */
         float W = 50.0f;
         s->spheres[0].color = V3(1.0f, 1.0f, 0.0f); s->spheres[0].type = CLEARCOAT_DIFFUSE;
-        s->spheres[1].color = V3(1.0f, 1.0f, 1.0f); s->spheres[1].type = f->uRightSphereMatType;
+        s->spheres[1].color = V3(1.0f, 1.0f, 1.0f);
+        s->spheres[1].type = f->scene == PTO_SCENE_SKY ? f->uRightSphereMatType : METAL;
         s->quads[0] = mkquad(V3(0, 0, 1), V3(-W, W, W), V3(W, W, W), V3(W, -W, W), V3(-W, -W, W), V3(1.0f, 1.0f, 1.0f), DIFFUSE);
         s->quads[1] = mkquad(V3(1, 0, 0), V3(-W, -W, W), V3(-W, -W, -W), V3(-W, W, -W), V3(-W, W, W), V3(0.7f, 0.05f, 0.05f), DIFFUSE);
         s->quads[2] = mkquad(V3(-1, 0, 0), V3(W, -W, -W), V3(W, -W, W), V3(W, W, W), V3(W, W, -W), V3(0.05f, 0.05f, 0.7f), DIFFUSE);
@@ -342,7 +360,7 @@ static void SceneIntersect(Inv* s, v3 rayOrigin, v3 rayDirection, Hit* h)
         }
         objectCount++;
     }
-    if (f->scene != PTO_SCENE_GLTF) return;
+    if (f->scene != PTO_SCENE_GLTF && f->scene != PTO_SCENE_HDRI) return;
 
     /* ---- BVH traversal, js/GLTFModelPathTracing_FragmentShader.js:201-298 */
     float stackT[STACK_LEVELS], stackId[STACK_LEVELS];
@@ -431,10 +449,28 @@ typedef struct { v3 objectNormal, objectColor; float objectID, pixelSharpness; }
 
 static v3 v_pow22(v3 a) { return V3(g_pow(a.x, 2.2f), g_pow(a.y, 2.2f), g_pow(a.z, 2.2f)); }
 
+/* Get_HDR_Color, js/HDRIEnvironmentPathTracing_FragmentShader.js:236-245 */
+static v3 Get_HDR_Color(Inv* s, v3 rayDirection)
+{
+    const pto_frame* f = s->f;
+    float u = g_atan2(rayDirection.x, rayDirection.z) * 0.15915494309f + 0.5f;
+    float v = g_acos(-rayDirection.y) * 0.31830988618379067f;
+    float tx[4];
+    tex_bilinear_f(f->hdr, f->hdrW, f->hdrH, u, v, tx);
+    s->c.hdr_taps += 4;
+    return v_muls(V3(tx[0], tx[1], tx[2]), f->uHDRExposure);
+}
+
+/* CalculateRadiance of the glTF scene (js/GLTFModelPathTracing_FragmentShader.js:351-609) and of
+ * the HDRI scene, which is the same program with an environment on misses, no quad light, shadow
+ * rays into the sun lobe and up to three cosine bounces
+ * (js/HDRIEnvironmentPathTracing_FragmentShader.js:250-520) */
 static v3 CalculateRadiance(Inv* s, GOut* g)
 {
     const pto_frame* f = s->f;
-    const int gltf = f->scene == PTO_SCENE_GLTF;
+    const int hdri = f->scene == PTO_SCENE_HDRI;
+    const int gltf = f->scene == PTO_SCENE_GLTF || hdri;
+    const v3 sun = V3(f->uSunDirection[0], f->uSunDirection[1], f->uSunDirection[2]);
     Hit h;
     memset(&h, 0, sizeof(h));
     v3 accumCol = V3(0, 0, 0), mask = V3(1, 1, 1);
@@ -450,14 +486,29 @@ static v3 CalculateRadiance(Inv* s, GOut* g)
         previousIntersecType = hitType;
         SceneIntersect(s, s->rayOrigin, s->rayDirection, &h);
         hitType = h.type;
-        if (h.t == INFINITY_G) break;
+        if (h.t == INFINITY_G) {
+            if (!hdri) break;
+            v3 environmentColor = Get_HDR_Color(s, s->rayDirection);
+            if (bounces == 0) { g->pixelSharpness = 1.01f; accumCol = environmentColor; break; }
+            else if (diffuseCount == 0 && bounceIsSpecular) { g->pixelSharpness = 1.01f; accumCol = v_mul(mask, environmentColor); break; }
+            else if (sampleLight) { accumCol = v_mul(mask, environmentColor); break; }
+            else if (diffuseCount == 1 && previousIntersecType == TRANSPARENT && bounceIsSpecular && bounces < 3) {
+                if (v_dot(s->rayDirection, sun) > 0.99f) g->pixelSharpness = 1.01f;
+                accumCol = v_mul(mask, environmentColor);
+                break;
+            } else if (diffuseCount > 0) {
+                weight = v_dot(s->rayDirection, sun) < 0.99f ? 1.0f : 0.0f;
+                accumCol = v_muls(v_mul(mask, environmentColor), weight);
+                break;
+            }
+        }
         n = v_normalize(h.normal);
         nl = v_dot(n, s->rayDirection) < 0.0f ? v_normalize(n) : v_normalize(v_neg(n));
         x = v_add(s->rayOrigin, v_muls(s->rayDirection, h.t));
         if (bounces == 0) { g->objectNormal = nl; g->objectColor = h.color; g->objectID = h.objectID; }
         if (bounces == 1 && previousIntersecType == METAL) { g->objectNormal = nl; g->objectID = h.objectID; }
 
-        if (hitType == LIGHT) {
+        if (!hdri && hitType == LIGHT) {
             if (diffuseCount == 0) g->pixelSharpness = 1.01f;
             if (bounceIsSpecular || sampleLight) accumCol = v_mul(mask, h.color);
             break;
@@ -489,9 +540,17 @@ static v3 CalculateRadiance(Inv* s, GOut* g)
             diffuseCount++;
             mask = v_mul(mask, h.color);
             bounceIsSpecular = 0;
-            if (diffuseCount == 1 && blueNoise_rand(s) < 0.5f) {
+            if ((hdri ? diffuseCount <= 2 : diffuseCount == 1) && blueNoise_rand(s) < 0.5f) {
                 s->rayDirection = randomCosWeightedDirectionInHemisphere(s, nl);
                 s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
+                continue;
+            }
+            if (hdri) {
+                s->rayDirection = randomDirectionInSpecularLobe(s, sun, 0.03f);
+                s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
+                weight = g_max(0.0f, v_dot(s->rayDirection, nl)) * (f->uSunPower * f->uSunPower * 0.0000001f);
+                mask = v_muls(mask, weight);
+                sampleLight = 1;
                 continue;
             }
             dirToLight = sampleAxisAlignedQuadLight(s, x, nl, &s->quads[5], &weight);
@@ -555,9 +614,17 @@ static v3 CalculateRadiance(Inv* s, GOut* g)
             mask = v_muls(mask, TP);
             mask = v_mul(mask, h.color);
             bounceIsSpecular = 0;
-            if (diffuseCount == 1 && blueNoise_rand(s) < 0.5f) {
+            if ((hdri ? diffuseCount <= 2 : diffuseCount == 1) && blueNoise_rand(s) < 0.5f) {
                 s->rayDirection = randomCosWeightedDirectionInHemisphere(s, nl);
                 s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
+                continue;
+            }
+            if (hdri) {
+                s->rayDirection = randomDirectionInSpecularLobe(s, sun, 0.03f);
+                s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
+                weight = g_max(0.0f, v_dot(s->rayDirection, nl)) * (f->uSunPower * f->uSunPower * 0.0000001f);
+                mask = v_muls(mask, weight);
+                if (bounces < 3) sampleLight = 1;
                 continue;
             }
             dirToLight = sampleAxisAlignedQuadLight(s, x, nl, &s->quads[5], &weight);
@@ -798,6 +865,7 @@ static void shade_pixel(const pto_frame* f, int px, int py, Shade* out, pto_coun
     cnt->paths += s.c.paths; cnt->segments += s.c.segments; cnt->node_fetches += s.c.node_fetches;
     cnt->leaf_tests += s.c.leaf_tests; cnt->hit_lookups += s.c.hit_lookups; cnt->rgba8_taps += s.c.rgba8_taps;
     cnt->stack_overflow += s.c.stack_overflow;
+    cnt->hdr_taps += s.c.hdr_taps;
 }
 
 /* ---------------------------------------------------------------- main(), part 2: quad derivatives + accumulate */
@@ -873,6 +941,7 @@ static int shade_rows(const pto_frame* f, int row0, int row1, int nthreads, Shad
             total.paths += local.paths; total.segments += local.segments; total.node_fetches += local.node_fetches;
             total.leaf_tests += local.leaf_tests; total.hit_lookups += local.hit_lookups; total.rgba8_taps += local.rgba8_taps;
             total.stack_overflow += local.stack_overflow;
+            total.hdr_taps += local.hdr_taps;
         }
     }
     if (counters) *counters = total;
@@ -883,7 +952,7 @@ static int shade_rows(const pto_frame* f, int row0, int row1, int nthreads, Shad
 int pto_path_trace(const pto_frame* f, const float* prev, float* out, int row0, int row1, int nthreads, pto_counters* counters)
 {
     if (!f || !prev || !out || row0 < 0 || row1 > f->height || row0 >= row1 || !f->blueNoise) return -1;
-    if (f->scene == PTO_SCENE_GLTF && (!f->aabb || !f->tri)) return -2;
+    if ((f->scene == PTO_SCENE_GLTF || f->scene == PTO_SCENE_HDRI) && (!f->aabb || !f->tri)) return -2;
     Shade* sh; int qy0, qy1;
     int Wq = shade_rows(f, row0, row1, nthreads, &sh, &qy0, &qy1, counters);
     if (Wq < 0) return -3;

@@ -14,7 +14,7 @@
 extern "C" {
 #endif
 
-enum { PTO_SCENE_CORNELL = 0, PTO_SCENE_GLTF = 1, PTO_SCENE_SKY = 2 };
+enum { PTO_SCENE_CORNELL = 0, PTO_SCENE_GLTF = 1, PTO_SCENE_SKY = 2, PTO_SCENE_HDRI = 3 };
 
 /* One frame's uniforms, by the names the setup scripts push (js/GLTF_Model_Path_Tracing.js:813-848,
  * js/Babylon_Path_Tracing.js:339-363). Matrices are Babylon Matrix.m (GLSL column-major). */
@@ -45,7 +45,9 @@ typedef struct pto_frame {
     const uint8_t* bump; int32_t bumpW, bumpH;
     const uint8_t* metallic; int32_t metallicW, metallicH;
     const uint8_t* emissive; int32_t emissiveW, emissiveH;
-    float uSunDirection[3];              /* sky */
+    float uSunDirection[3];              /* sky, hdri */
+    float uHDRExposure, uSunPower;       /* hdri */
+    const float* hdr; int32_t hdrW, hdrH; /* tHDRTexture: RGBA32F, GL row order (invertY applied), bilinear, REPEAT */
 } pto_frame;
 
 typedef struct pto_counters {
@@ -56,6 +58,7 @@ typedef struct pto_counters {
     uint64_t hit_lookups;    /* triangle attribute lookups: 8 texels = 128 B each */
     uint64_t rgba8_taps;     /* blue noise + PBR texel taps, 4 B each */
     uint64_t stack_overflow; /* pushes beyond stackLevels[28] (undefined in the reference) */
+    uint64_t hdr_taps;       /* tHDRTexture texel taps (RGBA32F), 16 B each */
 } pto_counters;
 
 /* Render rows [row0,row1) of one pathTracing pass: prev -> out (RGBA32F, row 0 = bottom, GL

@@ -13,7 +13,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libptoracle.so")
 
-SCENES = {"cornell": 0, "gltf": 1, "sky": 2}
+SCENES = {"cornell": 0, "gltf": 1, "sky": 2, "hdri": 3}
 
 c_f = ctypes.c_float
 c_i = ctypes.c_int32
@@ -42,12 +42,15 @@ class Frame(ctypes.Structure):
         ("metallic", ctypes.c_void_p), ("metallicW", c_i), ("metallicH", c_i),
         ("emissive", ctypes.c_void_p), ("emissiveW", c_i), ("emissiveH", c_i),
         ("uSunDirection", c_f * 3),
+        ("uHDRExposure", c_f), ("uSunPower", c_f),
+        ("hdr", ctypes.c_void_p), ("hdrW", c_i), ("hdrH", c_i),
     ]
 
 
 class Counters(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in
-                ("paths", "segments", "node_fetches", "leaf_tests", "hit_lookups", "rgba8_taps", "stack_overflow")]
+                ("paths", "segments", "node_fetches", "leaf_tests", "hit_lookups", "rgba8_taps", "stack_overflow",
+                 "hdr_taps")]
 
     def as_dict(self):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
@@ -75,8 +78,10 @@ def lib():
 class Scene:
     """Keeps the sampler arrays alive and builds Frame structs from recorded uniforms."""
 
-    def __init__(self, scene, width, height, bluenoise, bvh=None, tri=None):
+    def __init__(self, scene, width, height, bluenoise, bvh=None, tri=None, hdr=None):
+        """hdr: the tHDRTexture payload as the setup script uploads it (rows top-first, invertY)."""
         self.scene = scene
+        self.hdr = None if hdr is None else np.ascontiguousarray(np.asarray(hdr, dtype=np.float32)[::-1])
         self.width, self.height = width, height
         self.bluenoise = np.ascontiguousarray(bluenoise, dtype=np.uint8)
         self.bvh = None if bvh is None else np.ascontiguousarray(bvh, dtype=np.float32)
@@ -96,6 +101,9 @@ class Scene:
             else:
                 setattr(f, name, int(vals[0]) if kind == "i" else float(vals[0]))
         f.blueNoise = self.bluenoise.ctypes.data
+        if self.hdr is not None:
+            f.hdr = self.hdr.ctypes.data
+            f.hdrH, f.hdrW = self.hdr.shape[:2]
         if self.bvh is not None:
             f.aabb = self.bvh.ctypes.data
             f.aabbTexels = self.bvh.size // 4

@@ -94,4 +94,33 @@ function setup(REF, W, H, SEED) {
   return { REAL, BABYLON };
 }
 
-module.exports = { setup };
+// Synthetic equirect environment (the reference's .hdr files are not in the repository it ships):
+// a float RGBA image whose every value is a short dyadic rational, so the same bits come out of
+// Float32Array here and of tests/helpers.py synthetic_hdr(): a bright-top sky gradient, a dark
+// ground, 8-bit hashed noise, and a 5x5 sun whose centre texel is the unique brightest value
+// (the setup script derives uSunDirection from it, js/HDRI_Environment_Path_Tracing.js:774-815).
+const HDR_W = 2048, HDR_H = 1024, SUN_X = 1536, SUN_Y = 300;
+function hash32(i) {
+  let h = Math.imul(i, 0x9E3779B1) >>> 0;
+  h = (h ^ (h >>> 15)) >>> 0;
+  h = Math.imul(h, 0x85EBCA77) >>> 0;
+  return (h ^ (h >>> 13)) >>> 0;
+}
+function syntheticHDR() {
+  const d = new Float32Array(HDR_W * HDR_H * 4);
+  for (let y = 0; y < HDR_H; y++) {
+    for (let x = 0; x < HDR_W; x++) {
+      const i = y * HDR_W + x;
+      const n = (hash32(i) & 255) / 4096;
+      let r, g, b;
+      if (y < HDR_H / 2) { const t = (HDR_H / 2 - y) / 2048; r = 0.25 + t + n; g = 0.375 + t + n; b = 0.75 + 2 * t + n; }
+      else { r = 0.125 + n; g = 0.1875 + n; b = 0.0625 + n; }
+      const dx = x - SUN_X, dy = y - SUN_Y;
+      if (dx >= -2 && dx <= 2 && dy >= -2 && dy <= 2) { r = g = b = (dx === 0 && dy === 0) ? 4096 : 512; }
+      d[4 * i] = r; d[4 * i + 1] = g; d[4 * i + 2] = b; d[4 * i + 3] = 1;
+    }
+  }
+  return d;
+}
+
+module.exports = { setup, syntheticHDR, HDR_W, HDR_H };

@@ -10,7 +10,7 @@
 // (tests/golden/*.npz / *.json, packed by make_fixtures.py).
 //
 // usage: node make_fixtures.js <scene> <outdir> [width height frames seed model]
-//   scene: cornell | gltf | sky
+//   scene: cornell | gltf | sky | hdri
 'use strict';
 const fs = require('fs');
 const path = require('path');
@@ -24,7 +24,8 @@ const SEED = BigInt(SEED_ || '1');
 const MODEL = MODEL_ || 'Stanford Bunny';
 fs.mkdirSync(outdir, { recursive: true });
 
-const { REAL, BABYLON } = require('./browser_env.js').setup(REF, W, H, SEED);
+const ENV = require('./browser_env.js');
+const { REAL, BABYLON } = ENV.setup(REF, W, H, SEED);
 
 // ---------------------------------------------------------------- recording boundary
 let renderLoop = null;
@@ -47,11 +48,15 @@ class RecRT {
 }
 BABYLON.RenderTargetTexture = RecRT;
 class RecTexture {
-  constructor(url, scene, noMipmap, invertY, sampling) {
+  constructor(url, scene, noMipmap, invertY, sampling, onLoad) {
     this.name = 'file:' + String(url).replace(/^.*\//, '');
     this.noMipmap = noMipmap; this.invertY = invertY; this.sampling = sampling;
+    this._hdr = /\.hdr$/i.test(String(url));
+    // the .hdr environments are missing from the reference: the loader "decodes" the synthetic one
+    if (this._hdr && onLoad) setImmediate(onLoad);
   }
-  readPixels() { return Promise.resolve(new Float32Array(4)); }
+  getSize() { return this._hdr ? { width: ENV.HDR_W, height: ENV.HDR_H } : { width: 1, height: 1 }; }
+  readPixels() { return Promise.resolve(this._hdr ? ENV.syntheticHDR() : new Float32Array(4)); }
 }
 BABYLON.Texture = RecTexture;
 BABYLON.RawTexture = {
@@ -98,6 +103,7 @@ const scripts = {
   cornell: ['js/PathTracingCommon.js', 'js/BabylonPathTracing_FragmentShader.js', 'js/Babylon_Path_Tracing.js'],
   sky: ['js/PathTracingCommon.js', 'js/PhysicalSkyModel_FragmentShader.js', 'js/Physical_Sky_Model.js'],
   gltf: ['js/PathTracingCommon.js', 'js/GLTFModelPathTracing_FragmentShader.js', 'js/BVH_Fast_Builder.js', 'js/GLTF_Model_Path_Tracing.js'],
+  hdri: ['js/PathTracingCommon.js', 'js/HDRIEnvironmentPathTracing_FragmentShader.js', 'js/BVH_Fast_Builder.js', 'js/HDRI_Environment_Path_Tracing.js'],
 };
 // the setup scripts resolve models/ and textures/ relative to the page: make them absolute file URLs
 const realLoad = REAL.SceneLoader.LoadAssetContainer.bind(REAL.SceneLoader);
@@ -108,13 +114,16 @@ function frame() { frames.push([]); renderLoop(); }
 
 (async () => {
   for (const s of scripts[scene]) runScript(s);
-  if (scene === 'gltf') {
-    // wait for the initial (teapot) load, then select MODEL through the GUI exactly as a user would
-    while (rawTextures.length < 2) { frame(); await tick(); }
+  const meshTextures = () => rawTextures.filter((t) => t.h === 2048);
+  const hdrTextures = () => rawTextures.filter((t) => t.h !== 2048);
+  if (scene === 'gltf' || scene === 'hdri') {
+    // wait for the initial (teapot) load (and the environment), then select MODEL through the GUI
+    // exactly as a user would
+    while (meshTextures().length < 2 || (scene === 'hdri' && hdrTextures().length < 1)) { frame(); await tick(); }
     if (MODEL !== 'Utah Teapot') {
-      const before = rawTextures.length;
+      const before = meshTextures().length;
       vm.runInThisContext('gltfModel_SelectionController').setValue(MODEL);
-      while (rawTextures.length < before + 2) { frame(); await tick(); }
+      while (meshTextures().length < before + 2) { frame(); await tick(); }
     }
     // GUI-triggered changes (scale/rotation controllers) restart accumulation within a few frames:
     // start the recording at the last restart (uFrameCounter == 1)
@@ -130,17 +139,24 @@ function frame() { frames.push([]); renderLoop(); }
   // recorded frames: the uniform stream the setup script pushes from here on
   while (frames.length < FRAMES) frame();
   frames = frames.slice(0, FRAMES);
-  const meta = { scene, width: W, height: H, seed: Number(SEED), model: scene === 'gltf' ? MODEL : null, frames };
-  if (scene === 'gltf') {
+  const hasMesh = scene === 'gltf' || scene === 'hdri';
+  const meta = { scene, width: W, height: H, seed: Number(SEED), model: hasMesh ? MODEL : null, frames };
+  if (hasMesh) {
     const tris = vm.runInThisContext('total_number_of_triangles');
-    const n = rawTextures.length;
-    const aabb = rawTextures[n - 2], tri = rawTextures[n - 1];
+    const mt = meshTextures(), n = mt.length;
+    const aabb = mt[n - 2], tri = mt[n - 1];
     const nodes = 2 * tris - 1;
     fs.writeFileSync(path.join(outdir, 'bvh.f32'), Buffer.from(aabb.data.buffer, 0, nodes * 8 * 4));
     fs.writeFileSync(path.join(outdir, 'tri.f32'), Buffer.from(tri.data.buffer, 0, tris * 32 * 4));
     meta.triangles = tris; meta.nodes = nodes;
     meta.textures = { [aabb.name]: 'bvh', [tri.name]: 'tri' };
     meta.modelScale = vm.runInThisContext('modelInitialScale');
+  }
+  if (scene === 'hdri') {
+    const ht = hdrTextures(), env = ht[ht.length - 1];
+    meta.textures[env.name] = 'hdr';
+    meta.hdr = { width: env.w, height: env.h, invertY: env.invertY, sampling: env.sampling === undefined ? null : env.sampling,
+                 generator: 'synthetic_hdr v1', sha256: require('crypto').createHash('sha256').update(Buffer.from(env.data.buffer)).digest('hex') };
   }
   fs.writeFileSync(path.join(outdir, 'frames.json'), JSON.stringify(meta));
   process.stdout.write(`ok ${scene} ${W}x${H} frames=${FRAMES}\n`);

@@ -11,8 +11,13 @@ outputs as small fixtures:
                                    reduced to the 8-bit texels WebGL samples. Pinned convention:
                                    high byte (v16 >> 8), see DESIGN.md.
 
-usage: python tests/golden/gen/make_fixtures.py
+  The HDRI streams run HDRI_Environment_Path_Tracing.js on the synthetic environment of
+  browser_env.js syntheticHDR (== tests/helpers.py synthetic_hdr; the reference's .hdr files are
+  not in it); the stream records that texture's sha256, the payload itself is regenerated.
+
+usage: python tests/golden/gen/make_fixtures.py [stream names ...]   (default: all)
 """
+import sys
 import hashlib
 import json
 import os
@@ -35,6 +40,8 @@ STREAMS = [
     ("gltf_bunny_1080p", "gltf", 1920, 1080, 4, 1, "Stanford Bunny"),
     ("gltf_duck_320x180", "gltf", 320, 180, 3, 7, "glTF Duck"),
     ("gltf_helmet_320x180", "gltf", 320, 180, 3, 9, "Damaged Helmet"),
+    ("hdri_teapot_320x180", "hdri", 320, 180, 3, 11, "Utah Teapot"),
+    ("hdri_helmet_320x180", "hdri", 320, 180, 3, 13, "Damaged Helmet"),
 ]
 
 
@@ -47,7 +54,7 @@ def run_stream(name, scene, w, h, frames, seed, model, tmp):
     with open(os.path.join(out, "frames.json")) as f:
         meta = json.load(f)
     mesh = None
-    if scene == "gltf":
+    if scene in ("gltf", "hdri"):
         n = meta["triangles"]
         bvh = np.fromfile(os.path.join(out, "bvh.f32"), dtype="<f4").reshape(2 * n - 1, 8)
         tri = np.fromfile(os.path.join(out, "tri.f32"), dtype="<f4").reshape(n, 32)
@@ -117,13 +124,21 @@ def png_rgba16(path):
 
 
 def main():
-    manifest = {}
+    only = set(sys.argv[1:])
+    mpath = os.path.join(GOLD, "MANIFEST.json")
+    manifest = json.load(open(mpath)) if only and os.path.exists(mpath) else {}
     with tempfile.TemporaryDirectory() as tmp:
         meshes = {}
         for name, scene, w, h, frames, seed, model in STREAMS:
+            if only and name not in only:
+                continue
             meta, mesh = run_stream(name, scene, w, h, frames, seed, model, tmp)
             if mesh is not None:
                 key = model.split()[-1].lower()
+                # the HDRI scene builds its own BVH (its own model scales); share the file when equal
+                shared = manifest.get("mesh_" + key, {})
+                if scene == "hdri" and shared.get("sha256_bvh") != hashlib.sha256(mesh[0].tobytes()).hexdigest():
+                    key = "hdri_" + key
                 meta["mesh"] = "mesh_%s.npz" % key
                 meshes[key] = mesh
             with open(os.path.join(GOLD, name + ".json"), "w") as f:

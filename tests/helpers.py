@@ -24,13 +24,16 @@ def mesh(meta_or_key):
 
 
 def texture_payloads(meta, m):
-    """The two 2048x2048 RGBA32F arrays exactly as the setup script uploads them (zero tail)."""
+    """The RGBA32F arrays exactly as the setup script uploads them: the two 2048x2048 mesh textures
+    (zero tail) and, for the HDRI scene, the environment (synthetic_hdr)."""
     out = {}
     for kind in ("bvh", "tri"):
         full = np.zeros(2048 * 2048 * 4, np.float32)
         flat = m[kind].reshape(-1)
         full[:flat.size] = flat
         out[kind] = full
+    if meta["scene"] == "hdri":
+        out["hdr"] = synthetic_hdr()
     return out
 
 
@@ -45,9 +48,10 @@ def output_call(frame):
 def oracle_scene(meta, width=None, height=None, mesh_arrays=None):
     import ptoracle as po
     w, h = width or meta["width"], height or meta["height"]
-    if meta["scene"] == "gltf":
+    if meta["scene"] in ("gltf", "hdri"):
         m = mesh_arrays if mesh_arrays is not None else mesh(meta)
-        return po.Scene("gltf", w, h, bluenoise(), m["bvh"], m["tri"])
+        hdr = synthetic_hdr() if meta["scene"] == "hdri" else None
+        return po.Scene(meta["scene"], w, h, bluenoise(), m["bvh"], m["tri"], hdr)
     return po.Scene(meta["scene"], w, h, bluenoise())
 
 
@@ -78,3 +82,29 @@ def oracle_replay(meta, frames=None, width=None, height=None, nthreads=0, with_o
             exp = ou.get("uToneMappingExposure", ["f", [0.0]])[1][0]
             canvases.append(po.screen_output(acc, ou["uOneOverSampleCounter"][1][0], exp))
     return accs, canvases, counters
+
+
+HDR_W, HDR_H, SUN_X, SUN_Y = 2048, 1024, 1536, 300
+
+
+def synthetic_hdr():
+    """The synthetic equirect environment the fixture generator hands to the HDRI setup script in
+    place of its missing .hdr files (tests/golden/gen/browser_env.js syntheticHDR): (1024, 2048, 4)
+    float32 in the order the script passes it to RawTexture.CreateRGBATexture (invertY = true).
+    Every value is a short dyadic rational, so both generators produce the same bits."""
+    i = np.arange(HDR_W * HDR_H, dtype=np.uint64)
+    h = (i * np.uint64(0x9E3779B1)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(15)
+    h = (h * np.uint64(0x85EBCA77)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(13)
+    n = (h & np.uint64(255)).astype(np.float64).reshape(HDR_H, HDR_W) / 4096.0
+    y = np.arange(HDR_H, dtype=np.float64)[:, None]
+    t = (HDR_H / 2 - y) / 2048.0
+    sky = y < HDR_H / 2
+    out = np.ones((HDR_H, HDR_W, 4), np.float64)
+    out[..., 0] = np.where(sky, 0.25 + t + n, 0.125 + n)
+    out[..., 1] = np.where(sky, 0.375 + t + n, 0.1875 + n)
+    out[..., 2] = np.where(sky, 0.75 + 2 * t + n, 0.0625 + n)
+    out[SUN_Y - 2:SUN_Y + 3, SUN_X - 2:SUN_X + 3, :3] = 512.0
+    out[SUN_Y, SUN_X, :3] = 4096.0
+    return out.astype(np.float32)

@@ -79,7 +79,7 @@ def test_pinned_math_bitexact(engine, op):
 def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1):
     import babylon_pt as bp
     m = None
-    if meta["scene"] == "gltf":
+    if meta["scene"] in ("gltf", "hdri"):
         m = H.texture_payloads(meta, H.mesh(meta))
     player = bp.StreamPlayer(engine, meta, H.bluenoise(), m, width, height)
     accs, canvases = [], []
@@ -123,13 +123,15 @@ def backend(request, engine):
     ("gltf_teapot_320x180", None),
     ("gltf_duck_320x180", None),
     ("gltf_helmet_320x180", None),
+    ("hdri_teapot_320x180", None),
+    ("hdri_helmet_320x180", None),
 ])
 def test_stream_bitexact(engine, backend, name, frames):
     """Whole recorded streams (path trace -> copy -> output per frame) match the oracle exactly."""
     meta = H.stream(name)
     ref_acc, ref_can, _ = H.oracle_replay(meta, frames, with_output=True)
     got_acc, got_can, _ = _replay_gpu(engine, meta, frames)
-    if meta["scene"] == "gltf":
+    if meta["scene"] in ("gltf", "hdri"):
         assert engine.bvh_layout_used() == backend[1]
     for i, (ra, ga, rc, gc) in enumerate(zip(ref_acc, got_acc, ref_can, got_can)):
         assert _bits_equal(ra, ga), "%s frame %d accumulation: %s" % (name, i, _diff_report(ra, ga))

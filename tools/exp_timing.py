@@ -22,7 +22,7 @@ ap.add_argument("--layouts", default="pairs,reference")
 a = ap.parse_args()
 meta = H.stream(a.stream)
 e = bp.Engine(0)
-mesh = H.texture_payloads(meta, H.mesh(meta)) if meta["scene"] == "gltf" else None
+mesh = H.texture_payloads(meta, H.mesh(meta)) if meta["scene"] in ("gltf", "hdri") else None
 p = bp.StreamPlayer(e, meta, H.bluenoise(), mesh)
 prog = meta["scene"]
 import itertools  # noqa: E402

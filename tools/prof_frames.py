@@ -20,7 +20,7 @@ ap.add_argument("--height", type=int, default=0)
 a = ap.parse_args()
 meta = H.stream(a.stream)
 e = bp.Engine(0)
-mesh = H.texture_payloads(meta, H.mesh(meta)) if meta["scene"] == "gltf" else None
+mesh = H.texture_payloads(meta, H.mesh(meta)) if meta["scene"] in ("gltf", "hdri") else None
 p = bp.StreamPlayer(e, meta, H.bluenoise(), mesh, a.width or None, a.height or None)
 for k in range(a.frames):
     for call in p.synth_frame(k):
