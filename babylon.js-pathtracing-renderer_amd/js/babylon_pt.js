@@ -13,7 +13,8 @@
 //   new BABYLON.Engine(canvas)                    -> pt_ctx_create           (js/GLTF_Model_Path_Tracing.js:189)
 //   new BABYLON.RenderTargetTexture(n,{w,h},...)  -> pt_render_target_create (:762-768), .resize -> pt_render_target_resize
 //   BABYLON.RawTexture.CreateRGBATexture(...)     -> pt_texture_create_rgba32f / _rgba8 (:466-487)
-//   new BABYLON.Texture(url, ...)                 -> host PNG decode + pt_texture_create_rgba8 (:749-758)
+//   new BABYLON.Texture(url, ...)                 -> host PNG decode + pt_texture_create_rgba8 (:749-758);
+//                                                    '*.hdr' -> host RGBE decode, readPixels() (js/HDRI_Environment_Path_Tracing.js:764-823)
 //   new BABYLON.EffectWrapper({...})              -> pt_effect_create (GLSL text -> program) (:773-811)
 //   effect.setFloat/.../setMatrix/setTexture      -> pt_set_float / pt_set_int / pt_set_texture (:813-848)
 //   new BABYLON.EffectRenderer(engine).render()   -> pt_render (:1230-1235)
@@ -28,6 +29,47 @@ const TEXTURETYPE_UNSIGNED_BYTE = 0;
 
 function loadAddon() {
   return require(path.join(__dirname, '..', 'napi', 'pt_napi.node'));
+}
+
+// ---------------------------------------------------------------------------------- Radiance .hdr
+// The HDRI scene loads its environment with new BABYLON.Texture('*.hdr', ..., onLoad) and reads it
+// back with readPixels() (js/HDRI_Environment_Path_Tracing.js:764-823). RGBE -> float as Babylon's
+// HDRTools: value = mantissa * 2^(exponent - 136), exponent 0 -> 0; scanlines in file order (the
+// usual "-Y H +X W" orientation: first scanline = top row = first row of the returned data), alpha 1.
+// Both the flat layout and the adaptive run-length scanlines (2,2,hi,lo header) are read.
+function decodeHDR(buf) {
+  let pos = 0;
+  const line = () => { const e = buf.indexOf(10, pos); const l = buf.toString('latin1', pos, e); pos = e + 1; return l; };
+  const magic = line();
+  if (!magic.startsWith('#?')) throw new Error('not a Radiance HDR file');
+  let fmt = '';
+  for (let l = line(); l !== ''; l = line()) if (l.startsWith('FORMAT=')) fmt = l.slice(7);
+  if (fmt && fmt !== '32-bit_rle_rgbe') throw new Error('unsupported HDR format ' + fmt);
+  const m = /^-Y (\d+) \+X (\d+)$/.exec(line().trim());
+  if (!m) throw new Error('unsupported HDR orientation');
+  const h = parseInt(m[1], 10), w = parseInt(m[2], 10);
+  const data = new Float32Array(w * h * 4);
+  const rgbe = new Uint8Array(w * 4);
+  for (let y = 0; y < h; y++) {
+    if (w >= 8 && w < 0x8000 && buf[pos] === 2 && buf[pos + 1] === 2 && ((buf[pos + 2] << 8) | buf[pos + 3]) === w) {
+      pos += 4;
+      for (let c = 0; c < 4; c++) {
+        for (let x = 0; x < w;) {
+          let n = buf[pos++];
+          if (n > 128) { n -= 128; const v = buf[pos++]; for (let k = 0; k < n; k++) rgbe[4 * (x++) + c] = v; }
+          else for (let k = 0; k < n; k++) rgbe[4 * (x++) + c] = buf[pos++];
+        }
+      }
+    } else {
+      for (let x = 0; x < 4 * w; x++) rgbe[x] = buf[pos++];
+    }
+    for (let x = 0; x < w; x++) {
+      const e = rgbe[4 * x + 3], o = 4 * (y * w + x);
+      const f = e ? Math.pow(2, e - 136) : 0;
+      data[o] = rgbe[4 * x] * f; data[o + 1] = rgbe[4 * x + 1] * f; data[o + 2] = rgbe[4 * x + 2] * f; data[o + 3] = 1;
+    }
+  }
+  return { width: w, height: h, data };
 }
 
 // ---------------------------------------------------------------------------------- PNG (RGBA8/16)
@@ -160,20 +202,40 @@ function install(BABYLON, opts) {
   };
 
   class Texture {
-    constructor(url, scene, noMipmap, invertY, samplingMode) {
+    constructor(url, scene, noMipmap, invertY, samplingMode, onLoad) {
       this.name = url;
       this._ctx = ctxOf(scene);
       this._pt = null;
-      const file = path.isAbsolute(url) ? url : path.join(opts.baseDir, url);
+      this._size = { width: 0, height: 0 };
+      this._pixels = null;
+      // page-relative URLs resolve against baseDir, then the extra opts.assetDirs
+      const dirs = [opts.baseDir].concat(opts.assetDirs || []);
+      const file = path.isAbsolute(url) ? url
+        : (dirs.map((d) => path.join(d, url)).find((f) => fs.existsSync(f)) || path.join(opts.baseDir, url));
+      if (/\.hdr$/i.test(url)) {
+        // an environment: decoded on the host, handed back through readPixels(); the setup script
+        // re-uploads it as a RawTexture (so nothing is bound here)
+        try {
+          const img = decodeHDR(fs.readFileSync(file));
+          this._size = { width: img.width, height: img.height };
+          this._pixels = img.data;
+          if (onLoad) setImmediate(onLoad);
+        } catch (e) {
+          report('Texture(' + url + '): ' + e.message + ' (not loaded)');
+        }
+        return;
+      }
       try {
         const img = decodePNG(fs.readFileSync(file));
+        this._size = { width: img.width, height: img.height };
         const h = addon.pt_texture_create_rgba8(this._ctx, img.width, img.height, img.data, samplingMode === undefined ? 3 : samplingMode, invertY ? 1 : 0);
         if (typeof h !== 'number') this._pt = label(h, url);
       } catch (e) {
         report('Texture(' + url + '): ' + e.message + ' (left unbound)');
       }
     }
-    readPixels() { return Promise.resolve(null); }
+    getSize() { return this._size; }
+    readPixels() { return Promise.resolve(this._pixels); }
     dispose() { if (this._pt) addon.pt_texture_destroy(this._pt); this._pt = null; }
   }
 
@@ -231,7 +293,7 @@ function install(BABYLON, opts) {
   set('Texture', Texture);
   set('EffectWrapper', EffectWrapper);
   set('EffectRenderer', EffectRenderer);
-  return { addon, Engine, decodePNG };
+  return { addon, Engine, decodePNG, decodeHDR };
 }
 
-module.exports = { install, decodePNG, loadAddon };
+module.exports = { install, decodePNG, decodeHDR, loadAddon };

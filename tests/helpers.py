@@ -108,3 +108,54 @@ def synthetic_hdr():
     out[SUN_Y - 2:SUN_Y + 3, SUN_X - 2:SUN_X + 3, :3] = 512.0
     out[SUN_Y, SUN_X, :3] = 4096.0
     return out.astype(np.float32)
+
+
+def rgbe_encode(img):
+    """float RGB(A) (H, W, >=3) -> RGBE bytes (H, W, 4), Ward's float2rgbe: shared exponent of the
+    largest channel, mantissas truncated to 8 bits."""
+    rgb = np.asarray(img, np.float64)[..., :3]
+    m = rgb.max(axis=-1)
+    mant, e = np.frexp(m)
+    ok = m >= 1e-32
+    scale = np.where(ok, mant * 256.0 / np.where(ok, m, 1.0), 0.0)
+    out = np.zeros(rgb.shape[:2] + (4,), np.uint8)
+    out[..., :3] = np.floor(rgb * scale[..., None]).astype(np.uint8)
+    out[..., 3] = np.where(ok, e + 128, 0).astype(np.uint8)
+    return out
+
+
+def rgbe_decode(rgbe):
+    """RGBE bytes -> float32 RGBA, value = mantissa * 2^(e - 136) (Babylon HDRTools), alpha 1."""
+    rgbe = np.asarray(rgbe)
+    e = rgbe[..., 3].astype(np.int32)
+    f = np.where(e > 0, np.ldexp(1.0, e - 136), 0.0)
+    out = np.ones(rgbe.shape[:2] + (4,), np.float64)
+    out[..., :3] = rgbe[..., :3] * f[..., None]
+    return out.astype(np.float32)
+
+
+def write_radiance_hdr(path, rgbe):
+    """A Radiance .hdr file with adaptive run-length scanlines (what HDR tools write)."""
+    h, w = rgbe.shape[:2]
+    parts = [b"#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n", ("-Y %d +X %d\n" % (h, w)).encode()]
+    for y in range(h):
+        parts.append(bytes([2, 2, w >> 8, w & 255]))
+        for c in range(4):
+            ch = rgbe[y, :, c]
+            x = 0
+            while x < w:                       # runs of >= 3 equal bytes, else literal dumps
+                run = 1
+                while x + run < w and run < 127 and ch[x + run] == ch[x]:
+                    run += 1
+                if run >= 3:
+                    parts.append(bytes([128 + run, int(ch[x])]))
+                    x += run
+                    continue
+                start = x
+                while x < w and x - start < 128:
+                    if x + 2 < w and ch[x] == ch[x + 1] == ch[x + 2]:
+                        break
+                    x += 1
+                parts.append(bytes([x - start]) + ch[start:x].tobytes())
+    with open(path, "wb") as f:
+        f.write(b"".join(parts))

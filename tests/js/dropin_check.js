@@ -52,7 +52,8 @@ const label = (h, name) => { if (name === 'RawTexture') rawData.push(h.data); la
 const labelName = (h, name) => { h.name = name === 'RawTexture' ? 'raw' + (raw++) : (name.startsWith('./textures/') ? 'file:' + path.basename(name) : name); };
 
 const shim = require('../../babylon.js-pathtracing-renderer_amd/js/babylon_pt.js');
-shim.install(BABYLON, { addon: mock, width: W, height: H, baseDir: REF, label });
+shim.install(BABYLON, { addon: mock, width: W, height: H, baseDir: REF, label,
+                       assetDirs: process.env.PT_ASSET_DIR ? [process.env.PT_ASSET_DIR] : [] });
 
 // the setup scripts resolve models/ relative to the page
 const REAL_SL = BABYLON.SceneLoader;
@@ -64,6 +65,7 @@ const scripts = {
   cornell: ['js/PathTracingCommon.js', 'js/BabylonPathTracing_FragmentShader.js', 'js/Babylon_Path_Tracing.js'],
   sky: ['js/PathTracingCommon.js', 'js/PhysicalSkyModel_FragmentShader.js', 'js/Physical_Sky_Model.js'],
   gltf: ['js/PathTracingCommon.js', 'js/GLTFModelPathTracing_FragmentShader.js', 'js/BVH_Fast_Builder.js', 'js/GLTF_Model_Path_Tracing.js'],
+  hdri: ['js/PathTracingCommon.js', 'js/HDRIEnvironmentPathTracing_FragmentShader.js', 'js/BVH_Fast_Builder.js', 'js/HDRI_Environment_Path_Tracing.js'],
 };
 const tick = () => new Promise((r) => setImmediate(r));
 let engine = null;
@@ -74,12 +76,14 @@ const f32s = () => { let n = 0; for (const f of frames) for (const c of f) for (
 
 (async () => {
   for (const s of scripts[scene]) vm.runInThisContext(fs.readFileSync(path.join(REF, s), 'utf8'), { filename: s });
-  if (scene === 'gltf') {
-    while (raw < 2) { frame(); await tick(); }
+  const meshRaw = () => rawData.filter((d) => d.length === 2048 * 2048 * 4).length;
+  const envRaw = () => rawData.length - meshRaw();
+  if (scene === 'gltf' || scene === 'hdri') {
+    while (meshRaw() < 2 || (scene === 'hdri' && envRaw() < 1)) { frame(); await tick(); }
     if (MODEL !== 'Utah Teapot') {
-      const before = raw;
+      const before = meshRaw();
       vm.runInThisContext('gltfModel_SelectionController').setValue(MODEL);
-      while (raw < before + 2) { frame(); await tick(); }
+      while (meshRaw() < before + 2) { frame(); await tick(); }
     }
     frames = [];
     for (let i = 0; i < 6; i++) frame();

@@ -24,16 +24,31 @@ CHECK = os.path.join(H.ROOT, "tests", "js", "dropin_check.js")
 PBR_MAPS = {"tAlbedoTexture", "tBumpTexture", "tMetallicTexture", "tEmissiveTexture"}
 
 
-def run(scene, w, h, frames, seed, model=None):
+def run(scene, w, h, frames, seed, model=None, env=None):
     cmd = ["node", CHECK, scene, str(w), str(h), str(frames), str(seed)] + ([model] if model else [])
-    out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300).stdout
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=300,
+                         env=dict(os.environ, **(env or {}))).stdout
     return json.loads(out)
 
 
-@pytest.mark.parametrize("name", ["cornell_256", "sky_256", "gltf_teapot_320x180", "gltf_bunny_1080p", "gltf_helmet_320x180"])
-def test_unmodified_setup_script_drives_the_shim(name):
+@pytest.fixture(scope="module")
+def hdr_dir(tmp_path_factory):
+    """textures/noon_grass_2k.hdr (the HDRI script's default environment, absent from the
+    reference): the synthetic environment RGBE-encoded; the shim must decode it to exactly
+    rgbe_decode() of the same bytes."""
+    d = tmp_path_factory.mktemp("assets")
+    os.makedirs(d / "textures")
+    rgbe = H.rgbe_encode(H.synthetic_hdr())
+    H.write_radiance_hdr(str(d / "textures" / "noon_grass_2k.hdr"), rgbe)
+    return str(d), H.rgbe_decode(rgbe)
+
+
+@pytest.mark.parametrize("name", ["cornell_256", "sky_256", "gltf_teapot_320x180", "gltf_bunny_1080p", "gltf_helmet_320x180",
+                                  "hdri_teapot_320x180"])
+def test_unmodified_setup_script_drives_the_shim(name, hdr_dir):
     meta = H.stream(name)
-    got = run(meta["scene"], meta["width"], meta["height"], len(meta["frames"]), meta["seed"], meta.get("model"))
+    env = {"PT_ASSET_DIR": hdr_dir[0]} if meta["scene"] == "hdri" else None
+    got = run(meta["scene"], meta["width"], meta["height"], len(meta["frames"]), meta["seed"], meta.get("model"), env)
     assert len(got["frames"]) == len(meta["frames"])
     for i, (fa, fb) in enumerate(zip(got["frames"], meta["frames"])):
         assert len(fa) == len(fb) == 3
@@ -44,7 +59,10 @@ def test_unmodified_setup_script_drives_the_shim(name):
             # host yet, so the shim binds them as unloaded textures
             want = {s: (None if s in PBR_MAPS else t) for s, t in cb["samplers"].items()}
             assert ca["samplers"] == want, "frame %d %s samplers" % (i, cb["effect"])
-    if meta["scene"] == "gltf":
+    if meta["scene"] in ("gltf", "hdri"):
         payload = H.texture_payloads(meta, H.mesh(meta))
-        want = [hashlib.sha256(payload[k].tobytes()).hexdigest() for k in ("bvh", "tri")]
-        assert got["raw_sha256"][-2:] == want
+        want = {hashlib.sha256(payload[k].tobytes()).hexdigest() for k in ("bvh", "tri")}
+        assert want <= set(got["raw_sha256"])
+    if meta["scene"] == "hdri":
+        # the environment reached the boundary exactly as decoded from the RGBE file
+        assert hashlib.sha256(hdr_dir[1].tobytes()).hexdigest() in got["raw_sha256"]
