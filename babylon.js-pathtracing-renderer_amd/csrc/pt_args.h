@@ -76,7 +76,12 @@ struct TraceArgs {
     TriArg qtri[12];
     ptg::f3 qnormal[6], qcolor[6];
     int qtype[6];
-    int nquads;             // N_QUADS: 6 (Cornell, glTF), 4 (sky, HDRI: no ceiling, no quad light)
+    int nquads;             // N_QUADS: 6 (Cornell, glTF, quadric), 4 (sky, HDRI: no ceiling, no quad light)
+    // transformed-quadric program (js/TransformedQuadricGeometry_FragmentShader.js:9-24): the twelve
+    // unit shapes' inverse matrices in SceneIntersect order, uShapeK, uAllShapesMatType
+    ptg::m4 shape_inv[12];
+    float shape_k;
+    int shape_mat;
     SkyArgs sky;            // sky.sun is uSunDirection for the HDRI program too
     // HDRI environment (js/HDRIEnvironmentPathTracing_FragmentShader.js:15-22)
     TexF hdr;

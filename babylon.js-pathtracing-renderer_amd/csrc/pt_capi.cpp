@@ -271,6 +271,15 @@ void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
         a.nquads = 4;
     }
     if (fx->prog == PT_PROG_SKY) sky_setup(fx, a.sky);
+    if (fx->prog == PT_PROG_QUADRIC) {   // js/TransformedQuadricGeometry_FragmentShader.js:9-24
+        static const char* const kShapes[12] = {
+            "uSphereInvMatrix", "uCylinderInvMatrix", "uConeInvMatrix", "uParaboloidInvMatrix",
+            "uHyperboloidInvMatrix", "uCapsuleInvMatrix", "uFlattenedRingInvMatrix", "uBoxInvMatrix",
+            "uPyramidFrustumInvMatrix", "uDiskInvMatrix", "uRectangleInvMatrix", "uTorusInvMatrix" };
+        for (int k = 0; k < 12; k++) um4(fx, kShapes[k], a.shape_inv[k]);
+        a.shape_k = uf(fx, "uShapeK");
+        a.shape_mat = ui(fx, "uAllShapesMatType");
+    }
     if (fx->prog == PT_PROG_HDRI) {
         a.sky.sun = v3(uf(fx, "uSunDirection", 0), uf(fx, "uSunDirection", 1), uf(fx, "uSunDirection", 2));
         a.hdr_exposure = uf(fx, "uHDRExposure");
@@ -866,6 +875,7 @@ int pt_render(pt_effect* fx, pt_texture* target)
     HIPCHK(c, hipSetDevice(c->device));
     switch (fx->prog) {
     case PT_PROG_CORNELL:
+    case PT_PROG_QUADRIC:
     case PT_PROG_SKY:
     case PT_PROG_HDRI:
     case PT_PROG_GLTF: return render_trace(fx, target);

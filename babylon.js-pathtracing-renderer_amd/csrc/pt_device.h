@@ -14,7 +14,7 @@ using namespace ptg;
 constexpr float kINF = 1000000.0f;   // #define INFINITY 1000000.0 (js/PathTracingCommon.js:329)
 constexpr float kTwoPi = 6.28318530717958648f;
 
-enum { PROG_CORNELL = 3, PROG_GLTF = 4, PROG_HDRI = 5, PROG_SKY = 6 };
+enum { PROG_CORNELL = 3, PROG_GLTF = 4, PROG_HDRI = 5, PROG_SKY = 6, PROG_QUADRIC = 7 };
 // PROG_GLTF_TEX / PROG_HDRI_TEX: the mesh programs instantiated with their PBR / normal-map code
 // (models with an albedo or bump texture); without +PROG_TEX those branches are compiled out.
 enum { PROG_TEX = 100, PROG_GLTF_TEX = 104, PROG_HDRI_TEX = 105 };
@@ -28,10 +28,13 @@ template <int P> constexpr bool kIsGltf = kScene<P> == PROG_GLTF || kScene<P> ==
 template <int P> constexpr bool kIsHdri = kScene<P> == PROG_HDRI;
 template <int P> constexpr bool kHasTex = kBase<P> >= PROG_TEX;
 template <int P> constexpr bool kIsSky = P == PROG_SKY;
+template <int P> constexpr bool kIsQuadric = P == PROG_QUADRIC;
+// hitObjectID layout: spheres 0-1 (quadric: shapes 0-11), then the quads; the mesh is 8
+template <int P> constexpr int kQuadId0 = kIsQuadric<P> ? 12 : 2;
 template <int P> constexpr bool kPairs = P >= PROG_PAIRS;
 // every instantiated program variant
 #define PT_FOR_EACH_PROG(X)                                                                           \
-    X(PROG_CORNELL) X(PROG_SKY) X(PROG_GLTF) X(PROG_GLTF_TEX) X(PROG_HDRI) X(PROG_HDRI_TEX)           \
+    X(PROG_CORNELL) X(PROG_SKY) X(PROG_QUADRIC) X(PROG_GLTF) X(PROG_GLTF_TEX) X(PROG_HDRI) X(PROG_HDRI_TEX)           \
     X(PROG_PAIRS + PROG_GLTF) X(PROG_PAIRS + PROG_GLTF_TEX) X(PROG_PAIRS + PROG_HDRI) X(PROG_PAIRS + PROG_HDRI_TEX)
 
 // the kernel variant of a draw: the scene program, +PROG_TEX when the model carries albedo / bump

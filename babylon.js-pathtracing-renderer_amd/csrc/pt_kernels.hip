@@ -55,42 +55,15 @@ struct MegaStack {
     }
 };
 
-// SceneIntersect: js/BabylonPathTracing_FragmentShader.js:47-112 (Cornell) and
-// js/GLTFModelPathTracing_FragmentShader.js:116-346 (glTF, with the BVH walk). The object loops
-// stay rolled (#pragma unroll 1): each iteration re-reads its sphere / triangle from the kernarg
-// segment through the scalar cache, which keeps ~130 wave-uniform floats out of VGPRs and the
-// code small enough for the instruction cache.
+// SceneIntersect: js/BabylonPathTracing_FragmentShader.js:47-112 (Cornell),
+// js/TransformedQuadricGeometry_FragmentShader.js:77-317 (quadrics) and
+// js/GLTFModelPathTracing_FragmentShader.js:116-346 (glTF, with the BVH walk)
 template <int PROG, bool COUNT>
 PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* lds, unsigned lane_slot,
                          float2* deep, Cnt& cnt)
 {
     if (COUNT) cnt.seg++;
-    h.t = kINF;
-    h.type = -100;
-    h.id = -1;
-    f3 sn = mk(0, 0, 0);
-#pragma unroll 1
-    for (int s = 0; s < 2; s++) {
-        const SphereArg& S = a.sph[s];
-        f3 n;
-        float d = unitSphere(mul(S.inv, rayO, 1.0f), mul(S.inv, rayD, 0.0f), n);
-        if (d < h.t) { h.t = d; h.id = s; sn = n; }
-    }
-#pragma unroll 1
-    for (int i = 0; i < a.nquads; i++) {
-        float d = gmin(quadTriangle(a.qtri[2 * i], rayO, rayD), quadTriangle(a.qtri[2 * i + 1], rayO, rayD));
-        if (d < h.t) { h.t = d; h.id = 2 + i; }
-    }
-    // resolve the closest analytic hit's attributes once (the GLSL writes them at every closer hit;
-    // only the last write survives)
-    if (h.id >= 0 && h.id < 2) {
-        const SphereArg& S = a.sph[h.id];
-        h.normal = normalize(mul3t(S.inv, normalize(sn)));
-        h.color = S.color; h.type = S.type;
-    } else if (h.id >= 2) {
-        h.normal = normalize(a.qnormal[h.id - 2]);
-        h.color = a.qcolor[h.id - 2]; h.type = a.qtype[h.id - 2];
-    }
+    analyticIntersect<PROG>(a, rayO, rayD, h);
     if (!kIsGltf<PROG>) return;
 
     // ---- BVH walk (js/GLTFModelPathTracing_FragmentShader.js:201-298), pt_device.h

@@ -9,6 +9,7 @@
 #include "pt_args.h"
 #include "pt_device.h"
 #include "pt_glsl.h"
+#include "pt_quadric.h"
 
 namespace pt {
 
@@ -113,6 +114,72 @@ PT_D f3 skyColor(const SkyArgs& k, f3 rayDir)
     L0 = L0 + (Fex * k.sunE19000) * sundisk;
     const f3 tex = (Lin + L0) * 0.04f + mk(0.0f, 0.0003f, 0.00075f);
     return pow3(tex, k.retExp);
+}
+
+// hitColor / hitType of analytic object `id` (the values SceneIntersect writes with it)
+template <int PROG>
+PT_D void objectMaterial(const TraceArgs& a, int id, f3& color, int& type)
+{
+    constexpr int q0 = kQuadId0<PROG>;
+    if (kIsQuadric<PROG> && id >= 0 && id < q0) {
+        // js/TransformedQuadricGeometry_FragmentShader.js:103-293
+        const float cr[12] = { 1.0f, 0.0f, 1.0f, 1.0f, 1.0f, 0.5f, 0.0f, 0.0f, 0.2f, 0.0f, 1.0f, 0.5f };
+        const float cg[12] = { 0.0f, 1.0f, 1.0f, 0.0f, 0.1f, 1.0f, 0.4f, 0.0f, 0.0f, 1.0f, 0.3f, 0.0f };
+        const float cb[12] = { 0.0f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 1.0f, 1.0f, 1.0f, 0.5f, 0.0f, 1.0f };
+        color = mk(cr[id], cg[id], cb[id]);
+        type = a.shape_mat;
+    } else if (!kIsQuadric<PROG> && id >= 0 && id < 2) {
+        color = a.sph[id].color; type = a.sph[id].type;
+    } else if (id >= q0 && id < q0 + a.nquads) {
+        color = a.qcolor[id - q0]; type = a.qtype[id - q0];
+    } else if (id == 8 && kIsGltf<PROG>) {
+        color = mk(1.0f, 1.0f, 1.0f); type = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
+    }
+}
+
+// SceneIntersect's analytic objects (spheres or the twelve quadric shapes, then the quads), with
+// the closest hit's attributes resolved once (the GLSL writes them at every closer hit; only the
+// last write survives). The object loops stay rolled (#pragma unroll 1): each iteration re-reads
+// its object from the kernarg segment through the scalar cache, which keeps ~130 wave-uniform
+// floats out of VGPRs and the code small enough for the instruction cache.
+template <int PROG>
+PT_D void analyticIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h)
+{
+    constexpr int q0 = kQuadId0<PROG>;
+    h.t = kINF;
+    h.type = -100;
+    h.id = -1;
+    f3 sn = mk(0, 0, 0);
+    if (kIsQuadric<PROG>) {
+#pragma unroll 1
+        for (int s = 0; s < 12; s++) {
+            f3 n = mk(0, 0, 0);
+            float d = quadricShape(s, mul(a.shape_inv[s], rayO, 1.0f), mul(a.shape_inv[s], rayD, 0.0f), a.shape_k, n);
+            if (d < h.t) { h.t = d; h.id = s; sn = n; }
+        }
+    } else {
+#pragma unroll 1
+        for (int s = 0; s < 2; s++) {
+            const SphereArg& S = a.sph[s];
+            f3 n;
+            float d = unitSphere(mul(S.inv, rayO, 1.0f), mul(S.inv, rayD, 0.0f), n);
+            if (d < h.t) { h.t = d; h.id = s; sn = n; }
+        }
+    }
+#pragma unroll 1
+    for (int i = 0; i < a.nquads; i++) {
+        float d = gmin(quadTriangle(a.qtri[2 * i], rayO, rayD), quadTriangle(a.qtri[2 * i + 1], rayO, rayD));
+        if (d < h.t) { h.t = d; h.id = q0 + i; }
+    }
+    if (h.id >= 0 && h.id < q0) {
+        const m4& M = kIsQuadric<PROG> ? a.shape_inv[h.id] : a.sph[h.id].inv;
+        // disk and rectangle: hitNormal = vec3(0,-1,0), not normalized before the transform
+        const f3 n0 = (kIsQuadric<PROG> && (h.id == 9 || h.id == 10)) ? mk(0.0f, -1.0f, 0.0f) : normalize(sn);
+        h.normal = normalize(mul3t(M, n0));
+    } else if (h.id >= q0) {
+        h.normal = normalize(a.qnormal[h.id - q0]);
+    }
+    if (h.id >= 0) objectMaterial<PROG>(a, h.id, h.color, h.type);
 }
 
 // Get_HDR_Color (js/HDRIEnvironmentPathTracing_FragmentShader.js:236-245): equirect lookup
@@ -220,13 +287,18 @@ PT_D bool shadeStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, Hit
             return more;
         }
         if (glass) {                             // refraction through the dielectric
-            if (distance(n, nl) > 0.1f) {
-                const float thickness = 0.01f;
-                f3 cc = clamp3(h.color, 0.01f, 0.99f);
-                s.mask = s.mask * mk(gexp(glog(cc.x) * thickness * h.t), gexp(glog(cc.y) * thickness * h.t),
-                                     gexp(glog(cc.z) * thickness * h.t));
+            if (kIsQuadric<PROG>) {              // no absorption, a colour filter (:470-471)
+                s.mask = s.mask * TP;
+                s.mask = s.mask * h.color;
+            } else {
+                if (distance(n, nl) > 0.1f) {
+                    const float thickness = 0.01f;
+                    f3 cc = clamp3(h.color, 0.01f, 0.99f);
+                    s.mask = s.mask * mk(gexp(glog(cc.x) * thickness * h.t), gexp(glog(cc.y) * thickness * h.t),
+                                         gexp(glog(cc.z) * thickness * h.t));
+                }
+                s.mask = s.mask * TP;
             }
-            s.mask = s.mask * TP;
             p.rd = refract(p.rd, nl, ratio);
             p.ro = x - nl * a.eps;
             if (s.diffuseCount == 1) s.specular = true;

@@ -156,24 +156,11 @@ __global__ __launch_bounds__(kBlock) void wf_extend(TraceArgs a, WfBufs w, int b
             if (f2u(A.w) != kHole) {
                 float4 B = w.qB[q][i];
                 f3 ro = mk(A.x, A.y, A.z), rd = mk(B.x, B.y, B.z);
-                float t = kINF;
-                int id = -1;
-                f3 sn = mk(0, 0, 0);
-#pragma unroll 1
-                for (int s = 0; s < 2; s++) {
-                    const SphereArg& S = a.sph[s];
-                    f3 nn;
-                    float d = unitSphere(mul(S.inv, ro, 1.0f), mul(S.inv, rd, 0.0f), nn);
-                    if (d < t) { t = d; id = s; sn = nn; }
-                }
-#pragma unroll 1
-                for (int k = 0; k < a.nquads; k++) {
-                    float d = gmin(quadTriangle(a.qtri[2 * k], ro, rd), quadTriangle(a.qtri[2 * k + 1], ro, rd));
-                    if (d < t) { t = d; id = 2 + k; }
-                }
-                f3 hn = mk(0, 0, 0);
-                if (id >= 0 && id < 2) hn = normalize(mul3t(a.sph[id].inv, normalize(sn)));
-                else if (id >= 2) hn = normalize(a.qnormal[id - 2]);
+                Hit h;
+                analyticIntersect<PROG>(a, ro, rd, h);
+                const float t = h.t;
+                const int id = h.id;
+                const f3 hn = id >= 0 ? h.normal : mk(0, 0, 0);
                 if (COUNT) count_add<true>(a, C_SEGMENTS, 1);
                 if (kIsGltf<PROG>) {
                     f3 O = mul(a.model, ro, 1.0f), D = mul(a.model, rd, 0.0f);
@@ -339,9 +326,7 @@ __global__ __launch_bounds__(kBlock) void wf_shade(TraceArgs a, WfBufs w, int b)
             h.normal = mk(H1.x, H1.y, H1.z);
             h.color = mk(0.0f, 0.0f, 0.0f);
             h.type = -100;
-            if (h.id >= 0 && h.id < 2) { h.color = a.sph[h.id].color; h.type = a.sph[h.id].type; }
-            else if (h.id >= 2 && h.id < 8) { h.color = a.qcolor[h.id - 2]; h.type = a.qtype[h.id - 2]; }
-            else if (h.id == 8) { h.color = mk(1.0f, 1.0f, 1.0f); h.type = a.uses_albedo ? PBR_MATERIAL : a.model_mat; }
+            objectMaterial<PROG>(a, h.id, h.color, h.type);
             GOutPix g{ w.gb0, w.gb1, pix };
             f3 accum = mk(0, 0, 0);
             Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };

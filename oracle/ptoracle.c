@@ -195,6 +195,260 @@ static float BVH_TriangleIntersect(v3 v0, v3 v1, v3 v2, v3 ro, v3 rd, float* u, 
     return (det < 0.0f || *u < 0.0f || *u > 1.0f || *v < 0.0f || *u + *v > 1.0f || t <= 0.0f) ? INFINITY_G : t;
 }
 
+/* ---------------------------------------------------------------- transformed quadrics */
+/* js/PathTracingCommon.js:690-1163: unit shapes in object space (the scene transforms the ray by
+ * each shape's inverse matrix). Expression order follows the GLSL exactly. */
+static v3 qhit(v3 ro, v3 rd, float t) { return v_add(ro, v_muls(rd, t)); }
+static float g_sign(float x) { return x > 0.0f ? 1.0f : x < 0.0f ? -1.0f : 0.0f; }
+static float g_step(float edge, float x) { return x < edge ? 0.0f : 1.0f; }
+
+static float UnitCylinderIntersect(v3 ro, v3 rd, v3* n)
+{
+    float t0, t1;
+    float a = (rd.x * rd.x + rd.z * rd.z);
+    float b = 2.0f * (rd.x * ro.x + rd.z * ro.z);
+    float c = (ro.x * ro.x + ro.z * ro.z) - 1.0f;
+    solveQuadratic(a, b, c, &t0, &t1);
+    v3 hit = qhit(ro, rd, t0);
+    if (t0 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x, 0.0f, 2.0f * hit.z); return t0; }
+    hit = qhit(ro, rd, t1);
+    if (t1 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x, 0.0f, 2.0f * hit.z); return t1; }
+    return INFINITY_G;
+}
+static float UnitConeIntersect(v3 ro, v3 rd, float k, v3* n)
+{
+    float t0, t1;
+    k = g_clamp(k, 0.01f, 1.0f);
+    float j = 1.0f / k;
+    float h = j * 2.0f - 1.0f;
+    float a = j * rd.x * rd.x + j * rd.z * rd.z - (k * 0.25f) * rd.y * rd.y;
+    float b = 2.0f * (j * rd.x * ro.x + j * rd.z * ro.z - (k * 0.25f) * rd.y * (ro.y - h));
+    float c = j * ro.x * ro.x + j * ro.z * ro.z - (k * 0.25f) * (ro.y - h) * (ro.y - h);
+    solveQuadratic(a, b, c, &t0, &t1);
+    v3 hit = qhit(ro, rd, t0);
+    if (t0 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x * j, 2.0f * (h - hit.y) * (k * 0.25f), 2.0f * hit.z * j); return t0; }
+    hit = qhit(ro, rd, t1);
+    if (t1 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x * j, 2.0f * (h - hit.y) * (k * 0.25f), 2.0f * hit.z * j); return t1; }
+    return INFINITY_G;
+}
+static float UnitParaboloidIntersect(v3 ro, v3 rd, v3* n)
+{
+    float t0, t1;
+    float k = 0.5f;
+    float a = rd.x * rd.x + rd.z * rd.z;
+    float b = 2.0f * (rd.x * ro.x + rd.z * ro.z) + k * rd.y;
+    float c = ro.x * ro.x + ro.z * ro.z + k * (ro.y - 1.0f);
+    solveQuadratic(a, b, c, &t0, &t1);
+    v3 hit = qhit(ro, rd, t0);
+    if (t0 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x, 0.5f, 2.0f * hit.z); return t0; }
+    hit = qhit(ro, rd, t1);
+    if (t1 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x, 0.5f, 2.0f * hit.z); return t1; }
+    return INFINITY_G;
+}
+static float UnitHyperboloidIntersect(v3 ro, v3 rd, float k, v3* n)
+{
+    float t0, t1;
+    k = k * k * k * k + 0.0012f;
+    k *= 1000.0f;
+    float j = k - 1.0f;
+    float a = k * rd.x * rd.x + k * rd.z * rd.z - j * rd.y * rd.y;
+    float b = 2.0f * (k * rd.x * ro.x + k * rd.z * ro.z - j * rd.y * ro.y);
+    float c = (k * ro.x * ro.x + k * ro.z * ro.z - j * ro.y * ro.y) - 1.0f;
+    solveQuadratic(a, b, c, &t0, &t1);
+    v3 hit = qhit(ro, rd, t0);
+    if (t0 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x * k, 2.0f * -hit.y * j, 2.0f * hit.z * k); return t0; }
+    hit = qhit(ro, rd, t1);
+    if (t1 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x * k, 2.0f * -hit.y * j, 2.0f * hit.z * k); return t1; }
+    return INFINITY_G;
+}
+static float UnitCapsuleIntersect(v3 ro, v3 rd, float k, v3* n)
+{
+    k += 0.25f;
+    float t0, t1, s0t0, s0t1, s1t0, s1t1;
+    v3 L = v_sub(ro, V3(0.0f, k, 0.0f));
+    float a = v_dot(rd, rd);
+    float b = 2.0f * v_dot(rd, L);
+    float c = v_dot(L, L) - 1.0f;
+    solveQuadratic(a, b, c, &s0t0, &s0t1);
+    v3 hit = qhit(ro, rd, s0t0);
+    if (s0t0 > 0.0f && hit.y >= k) { *n = V3(2.0f * hit.x, 2.0f * (hit.y - k), 2.0f * hit.z); return s0t0; }
+    L = v_sub(ro, V3(0.0f, -k, 0.0f));
+    a = v_dot(rd, rd);
+    b = 2.0f * v_dot(rd, L);
+    c = v_dot(L, L) - 1.0f;
+    solveQuadratic(a, b, c, &s1t0, &s1t1);
+    hit = qhit(ro, rd, s1t0);
+    if (s1t0 > 0.0f && hit.y <= -k) { *n = V3(2.0f * hit.x, 2.0f * (hit.y + k), 2.0f * hit.z); return s1t0; }
+    a = (rd.x * rd.x + rd.z * rd.z);
+    b = 2.0f * (rd.x * ro.x + rd.z * ro.z);
+    c = (ro.x * ro.x + ro.z * ro.z) - 1.0f;
+    solveQuadratic(a, b, c, &t0, &t1);
+    hit = qhit(ro, rd, t0);
+    if (t0 > 0.0f && fabsf(hit.y) <= k) { *n = V3(2.0f * hit.x, 0.0f, 2.0f * hit.z); return t0; }
+    hit = qhit(ro, rd, s0t1);
+    if (s0t1 > 0.0f && hit.y >= k) { *n = V3(2.0f * hit.x, 2.0f * (hit.y - k), 2.0f * hit.z); return s0t1; }
+    hit = qhit(ro, rd, s1t1);
+    if (s1t1 > 0.0f && hit.y <= -k) { *n = V3(2.0f * hit.x, 2.0f * (hit.y + k), 2.0f * hit.z); return s1t1; }
+    hit = qhit(ro, rd, t1);
+    if (t1 > 0.0f && fabsf(hit.y) <= k) { *n = V3(2.0f * hit.x, 0.0f, 2.0f * hit.z); return t1; }
+    return INFINITY_G;
+}
+static float UnitFlattenedRingIntersect(v3 ro, v3 rd, float k, v3* n)
+{
+    k -= 0.01f;
+    float t0, t1, c0, c1;
+    float a = (rd.x * rd.x + rd.z * rd.z);
+    float b = 2.0f * (rd.x * ro.x + rd.z * ro.z);
+    float c = (ro.x * ro.x + ro.z * ro.z) - 1.0f;
+    solveQuadratic(a, b, c, &t0, &t1);
+    v3 hit = qhit(ro, rd, t0);
+    if (t0 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x, 0.0f, 2.0f * hit.z); return t0; }
+    float d0 = (ro.y - 1.0f) / -rd.y;
+    hit = qhit(ro, rd, d0);
+    float x2z2 = hit.x * hit.x + hit.z * hit.z;
+    if (rd.y < 0.0f && d0 > 0.0f && x2z2 <= 1.0f && x2z2 > k) { *n = V3(0.0f, 1.0f, 0.0f); return d0; }
+    float d1 = (ro.y + 1.0f) / -rd.y;
+    hit = qhit(ro, rd, d1);
+    x2z2 = hit.x * hit.x + hit.z * hit.z;
+    if (rd.y > 0.0f && d1 > 0.0f && x2z2 <= 1.0f && x2z2 > k) { *n = V3(0.0f, -1.0f, 0.0f); return d1; }
+    c = (ro.x * ro.x + ro.z * ro.z) - k;
+    solveQuadratic(a, b, c, &c0, &c1);
+    hit = qhit(ro, rd, c0);
+    if (c0 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x, 0.0f, 2.0f * hit.z); return c0; }
+    hit = qhit(ro, rd, c1);
+    if (c1 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x, 0.0f, 2.0f * hit.z); return c1; }
+    hit = qhit(ro, rd, t1);
+    if (t1 > 0.0f && fabsf(hit.y) <= 1.0f) { *n = V3(2.0f * hit.x, 0.0f, 2.0f * hit.z); return t1; }
+    hit = qhit(ro, rd, d0);
+    x2z2 = hit.x * hit.x + hit.z * hit.z;
+    if (rd.y > 0.0f && d0 > 0.0f && x2z2 <= 1.0f && x2z2 > k) { *n = V3(0.0f, 1.0f, 0.0f); return d0; }
+    hit = qhit(ro, rd, d1);
+    x2z2 = hit.x * hit.x + hit.z * hit.z;
+    if (rd.y < 0.0f && d1 > 0.0f && x2z2 <= 1.0f && x2z2 > k) { *n = V3(0.0f, -1.0f, 0.0f); return d1; }
+    return INFINITY_G;
+}
+static float UnitBoxIntersect(v3 ro, v3 rd, v3* n)
+{
+    v3 invDir = V3(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
+    v3 nr = v_mul(v_sub(V3(-1.0f, -1.0f, -1.0f), ro), invDir);
+    v3 fr = v_mul(v_sub(V3(1.0f, 1.0f, 1.0f), ro), invDir);
+    v3 tmin = V3(g_min(nr.x, fr.x), g_min(nr.y, fr.y), g_min(nr.z, fr.z));
+    v3 tmax = V3(g_max(nr.x, fr.x), g_max(nr.y, fr.y), g_max(nr.z, fr.z));
+    float t0 = g_max(g_max(tmin.x, tmin.y), tmin.z);
+    float t1 = g_min(g_min(tmax.x, tmax.y), tmax.z);
+    if (t0 < t1) {
+        if (t0 > 0.0f) {   /* -sign(rd) * step(tmin.yzx, tmin) * step(tmin.zxy, tmin) */
+            *n = V3(-g_sign(rd.x) * g_step(tmin.y, tmin.x) * g_step(tmin.z, tmin.x),
+                    -g_sign(rd.y) * g_step(tmin.z, tmin.y) * g_step(tmin.x, tmin.y),
+                    -g_sign(rd.z) * g_step(tmin.x, tmin.z) * g_step(tmin.y, tmin.z));
+            return t0;
+        }
+        if (t1 > 0.0f) {   /* -sign(rd) * step(tmax, tmax.yzx) * step(tmax, tmax.zxy) */
+            *n = V3(-g_sign(rd.x) * g_step(tmax.x, tmax.y) * g_step(tmax.x, tmax.z),
+                    -g_sign(rd.y) * g_step(tmax.y, tmax.z) * g_step(tmax.y, tmax.x),
+                    -g_sign(rd.z) * g_step(tmax.z, tmax.x) * g_step(tmax.z, tmax.y));
+            return t1;
+        }
+    }
+    return INFINITY_G;
+}
+static float PyramidFrustumIntersect(v3 ro, v3 rd, float k, v3* n)
+{
+    float xt0, xt1, zt0, zt1;
+    float xt = INFINITY_G, zt = INFINITY_G;
+    v3 hit0, hit1, xn = V3(0, 0, 0), zn = V3(0, 0, 0);
+    k = g_clamp(k, 0.01f, 1.0f);
+    float j = 1.0f / k;
+    float h = j * 2.0f - 1.0f;
+    float a = j * rd.x * rd.x - (k * 0.25f) * rd.y * rd.y;
+    float b = 2.0f * (j * rd.x * ro.x - (k * 0.25f) * rd.y * (ro.y - h));
+    float c = j * ro.x * ro.x - (k * 0.25f) * (ro.y - h) * (ro.y - h);
+    solveQuadratic(a, b, c, &xt0, &xt1);
+    hit0 = qhit(ro, rd, xt0);
+    hit1 = qhit(ro, rd, xt1);
+    if (xt0 > 0.0f && fabsf(hit0.x) <= 1.0f && fabsf(hit0.z) <= 1.0f && hit0.y <= 1.0f &&
+        (j * hit0.z * hit0.z - k * 0.25f * (hit0.y - h) * (hit0.y - h)) <= 0.0f) {
+        xt = xt0;
+        xn = V3(2.0f * hit0.x * j, 2.0f * (hit0.y - h) * -(k * 0.25f), 0.0f);
+    } else if (xt1 > 0.0f && fabsf(hit1.x) <= 1.0f && fabsf(hit1.z) <= 1.0f && hit1.y <= 1.0f &&
+               (j * hit1.z * hit1.z - k * 0.25f * (hit1.y - h) * (hit1.y - h)) <= 0.0f) {
+        xt = xt1;
+        xn = V3(2.0f * hit1.x * j, 2.0f * (hit1.y - h) * -(k * 0.25f), 0.0f);
+    }
+    a = j * rd.z * rd.z - (k * 0.25f) * rd.y * rd.y;
+    b = 2.0f * (j * rd.z * ro.z - (k * 0.25f) * rd.y * (ro.y - h));
+    c = j * ro.z * ro.z - (k * 0.25f) * (ro.y - h) * (ro.y - h);
+    solveQuadratic(a, b, c, &zt0, &zt1);
+    hit0 = qhit(ro, rd, zt0);
+    hit1 = qhit(ro, rd, zt1);
+    if (zt0 > 0.0f && fabsf(hit0.x) <= 1.0f && fabsf(hit0.z) <= 1.0f && hit0.y <= 1.0f &&
+        (j * hit0.x * hit0.x - k * 0.25f * (hit0.y - h) * (hit0.y - h)) <= 0.0f) {
+        zt = zt0;
+        zn = V3(0.0f, 2.0f * (hit0.y - h) * -(k * 0.25f), 2.0f * hit0.z * j);
+    } else if (zt1 > 0.0f && fabsf(hit1.x) <= 1.0f && fabsf(hit1.z) <= 1.0f && hit1.y <= 1.0f &&
+               (j * hit1.x * hit1.x - k * 0.25f * (hit1.y - h) * (hit1.y - h)) <= 0.0f) {
+        zt = zt1;
+        zn = V3(0.0f, 2.0f * (hit1.y - h) * -(k * 0.25f), 2.0f * hit1.z * j);
+    }
+    if (xt <= zt) { *n = xn; return xt; }
+    *n = zn;
+    return zt;
+}
+static float UnitDiskIntersect(v3 ro, v3 rd)
+{
+    float t0 = (ro.y + 0.0f) / -rd.y;
+    v3 hit = qhit(ro, rd, t0);
+    return (t0 > 0.0f && hit.x * hit.x + hit.z * hit.z <= 1.0f) ? t0 : INFINITY_G;
+}
+static float UnitRectangleIntersect(v3 ro, v3 rd)
+{
+    float t0 = (ro.y + 0.0f) / -rd.y;
+    v3 hit = qhit(ro, rd, t0);
+    return (t0 > 0.0f && fabsf(hit.x) <= 1.0f && fabsf(hit.z) <= 1.0f) ? t0 : INFINITY_G;
+}
+static float map_Torus(v3 pos, float k)
+{
+    float a = sqrtf(pos.x * pos.x + pos.z * pos.z) - (1.0f - k);
+    return sqrtf(a * a + pos.y * pos.y) - k;
+}
+static float UnitTorusIntersect(v3 ro, v3 rd, float k, v3* n)
+{
+    k = 1.0f - g_clamp(k, 0.01f, 0.99f);
+    float d = INFINITY_G;
+    float tc, t0, t1;
+    float a = (rd.x * rd.x + rd.z * rd.z);
+    float b = 2.0f * (rd.x * ro.x + rd.z * ro.z);
+    float c = (ro.x * ro.x + ro.z * ro.z) - 1.0f;
+    solveQuadratic(a, b, c, &t0, &t1);
+    v3 hit0 = qhit(ro, rd, t0), hit1 = qhit(ro, rd, t1);
+    tc = (t0 > 0.0f && fabsf(hit0.y) <= k) ? t0 : (t1 > 0.0f && fabsf(hit1.y) <= k) ? t1 : INFINITY_G;
+    float d0 = (ro.y + k) / -rd.y;
+    v3 hit = qhit(ro, rd, d0);
+    d0 = (d0 > 0.0f && hit.x * hit.x + hit.z * hit.z <= 1.0f) ? d0 : INFINITY_G;
+    float d1 = (ro.y - k) / -rd.y;
+    hit = qhit(ro, rd, d1);
+    d1 = (d1 > 0.0f && hit.x * hit.x + hit.z * hit.z <= 1.0f) ? d1 : INFINITY_G;
+    if (tc == INFINITY_G && d0 == INFINITY_G && d1 == INFINITY_G) return INFINITY_G;
+    v3 pos = V3(0, 0, 0);
+    float t = g_min(g_min(d0, d1), tc);
+    for (int i = 0; i < 500; i++) {
+        pos = qhit(ro, rd, t);
+        d = map_Torus(pos, k);
+        if (fabsf(d) < 0.01f) break;
+        t += d;
+    }
+    if (fabsf(d) < 0.01f) {
+        float ex = (1.0f * 0.5773f) * 0.0002f, ey = (-1.0f * 0.5773f) * 0.0002f;
+        v3 s = v_muls(V3(ex, ey, ey), map_Torus(v_add(pos, V3(ex, ey, ey)), k));
+        s = v_add(s, v_muls(V3(ey, ey, ex), map_Torus(v_add(pos, V3(ey, ey, ex)), k)));
+        s = v_add(s, v_muls(V3(ey, ex, ey), map_Torus(v_add(pos, V3(ey, ex, ey)), k)));
+        s = v_add(s, v_muls(V3(ex, ex, ex), map_Torus(v_add(pos, V3(ex, ex, ex)), k)));
+        *n = v_normalize(s);
+        return t;
+    }
+    return INFINITY_G;
+}
+
 /* ---------------------------------------------------------------- textures */
 static const float* texel32(const float* base, int64_t n, float idx)
 {
@@ -330,6 +584,52 @@ static void SceneIntersect(Inv* s, v3 rayOrigin, v3 rayDirection, Hit* h)
     h->t = INFINITY_G;
     h->type = -100;
     h->objectID = -INFINITY_G;
+    if (f->scene == PTO_SCENE_QUADRIC) {
+        /* js/TransformedQuadricGeometry_FragmentShader.js:77-317: twelve unit shapes, each behind its
+         * inverse matrix, all of material uAllShapesMatType, then the Cornell quads */
+        static const float col[12][3] = { { 1.0f, 0.0f, 0.0f }, { 0.0f, 1.0f, 0.0f }, { 1.0f, 1.0f, 0.0f }, { 1.0f, 0.0f, 1.0f },
+                                          { 1.0f, 0.1f, 0.0f }, { 0.5f, 1.0f, 0.0f }, { 0.0f, 0.4f, 1.0f }, { 0.0f, 0.0f, 1.0f },
+                                          { 0.2f, 0.0f, 1.0f }, { 0.0f, 1.0f, 0.5f }, { 1.0f, 0.3f, 0.0f }, { 0.5f, 0.0f, 1.0f } };
+        for (int k = 0; k < 12; k++) {
+            const float* M = f->uShapeInvMatrix[k];
+            v3 ro = m4_mul(M, rayOrigin, 1.0f), rd = m4_mul(M, rayDirection, 0.0f);
+            n = V3(0, 0, 0);
+            switch (k) {
+            case 0: d = UnitSphereIntersect(ro, rd, &n); break;
+            case 1: d = UnitCylinderIntersect(ro, rd, &n); break;
+            case 2: d = UnitConeIntersect(ro, rd, f->uShapeK, &n); break;
+            case 3: d = UnitParaboloidIntersect(ro, rd, &n); break;
+            case 4: d = UnitHyperboloidIntersect(ro, rd, f->uShapeK, &n); break;
+            case 5: d = UnitCapsuleIntersect(ro, rd, f->uShapeK, &n); break;
+            case 6: d = UnitFlattenedRingIntersect(ro, rd, f->uShapeK, &n); break;
+            case 7: d = UnitBoxIntersect(ro, rd, &n); break;
+            case 8: d = PyramidFrustumIntersect(ro, rd, f->uShapeK, &n); break;
+            case 9: d = UnitDiskIntersect(ro, rd); break;
+            case 10: d = UnitRectangleIntersect(ro, rd); break;
+            default: d = UnitTorusIntersect(ro, rd, f->uShapeK, &n); break;
+            }
+            if (d < h->t) {
+                h->t = d;
+                /* disk and rectangle: hitNormal = vec3(0,-1,0), not normalized before the transform */
+                h->normal = (k == 9 || k == 10) ? V3(0.0f, -1.0f, 0.0f) : v_normalize(n);
+                h->normal = v_normalize(m3t_mul(M, h->normal));
+                h->color = V3(col[k][0], col[k][1], col[k][2]);
+                h->type = f->uAllShapesMatType;
+                h->objectID = (float)objectCount;
+            }
+            objectCount++;
+        }
+        for (int i = 0; i < s->nquads; i++) {
+            d = QuadIntersect(&s->quads[i], rayOrigin, rayDirection);
+            if (d < h->t) {
+                h->t = d;
+                h->normal = v_normalize(s->quads[i].normal);
+                h->color = s->quads[i].color; h->type = s->quads[i].type; h->objectID = (float)objectCount;
+            }
+            objectCount++;
+        }
+        return;
+    }
 
     v3 ro = m4_mul(f->uLeftSphereInvMatrix, rayOrigin, 1.0f);
     v3 rd = m4_mul(f->uLeftSphereInvMatrix, rayDirection, 0.0f);
@@ -469,6 +769,7 @@ static v3 CalculateRadiance(Inv* s, GOut* g)
 {
     const pto_frame* f = s->f;
     const int hdri = f->scene == PTO_SCENE_HDRI;
+    const int quadric = f->scene == PTO_SCENE_QUADRIC;
     const int gltf = f->scene == PTO_SCENE_GLTF || hdri;
     const v3 sun = V3(f->uSunDirection[0], f->uSunDirection[1], f->uSunDirection[2]);
     Hit h;
@@ -582,13 +883,18 @@ static v3 CalculateRadiance(Inv* s, GOut* g)
                 s->rayOrigin = v_add(x, v_muls(nl, f->uEPS_intersect));
                 continue;
             }
-            if (v_distance(n, nl) > 0.1f) {
-                thickness = 0.01f;
-                v3 cc = v_clamps(h.color, 0.01f, 0.99f);
-                v3 e = V3(g_exp(g_log(cc.x) * thickness * h.t), g_exp(g_log(cc.y) * thickness * h.t), g_exp(g_log(cc.z) * thickness * h.t));
-                mask = v_mul(mask, e);
+            if (quadric) {   /* js/TransformedQuadricGeometry_FragmentShader.js:470-471: no absorption */
+                mask = v_muls(mask, TP);
+                mask = v_mul(mask, h.color);
+            } else {
+                if (v_distance(n, nl) > 0.1f) {
+                    thickness = 0.01f;
+                    v3 cc = v_clamps(h.color, 0.01f, 0.99f);
+                    v3 e = V3(g_exp(g_log(cc.x) * thickness * h.t), g_exp(g_log(cc.y) * thickness * h.t), g_exp(g_log(cc.z) * thickness * h.t));
+                    mask = v_mul(mask, e);
+                }
+                mask = v_muls(mask, TP);
             }
-            mask = v_muls(mask, TP);
             tdir = v_refract(s->rayDirection, nl, ratioIoR);
             s->rayDirection = tdir;
             s->rayOrigin = v_sub(x, v_muls(nl, f->uEPS_intersect));
@@ -1046,6 +1352,34 @@ int pto_screen_output(int W, int H, const float* acc, float oneOverN, float expo
             }
             o[3] = 255;
         }
+    return 0;
+}
+
+/* ---------------------------------------------------------------- quadric probe */
+int pto_quadric_probe(int shape, float k, const float* ro, const float* rd, float* t, float* nrm, int n)
+{
+    for (int i = 0; i < n; i++) {
+        v3 o = V3(ro[3 * i], ro[3 * i + 1], ro[3 * i + 2]), d = V3(rd[3 * i], rd[3 * i + 1], rd[3 * i + 2]);
+        v3 nn = V3(0, 1, 0);
+        float r;
+        switch (shape) {
+        case 0: r = UnitSphereIntersect(o, d, &nn); break;
+        case 1: r = UnitCylinderIntersect(o, d, &nn); break;
+        case 2: r = UnitConeIntersect(o, d, k, &nn); break;
+        case 3: r = UnitParaboloidIntersect(o, d, &nn); break;
+        case 4: r = UnitHyperboloidIntersect(o, d, k, &nn); break;
+        case 5: r = UnitCapsuleIntersect(o, d, k, &nn); break;
+        case 6: r = UnitFlattenedRingIntersect(o, d, k, &nn); break;
+        case 7: r = UnitBoxIntersect(o, d, &nn); break;
+        case 8: r = PyramidFrustumIntersect(o, d, k, &nn); break;
+        case 9: r = UnitDiskIntersect(o, d); break;
+        case 10: r = UnitRectangleIntersect(o, d); break;
+        case 11: r = UnitTorusIntersect(o, d, k, &nn); break;
+        default: return -1;
+        }
+        t[i] = r;
+        nrm[3 * i] = nn.x; nrm[3 * i + 1] = nn.y; nrm[3 * i + 2] = nn.z;
+    }
     return 0;
 }
 

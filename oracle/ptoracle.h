@@ -14,7 +14,7 @@
 extern "C" {
 #endif
 
-enum { PTO_SCENE_CORNELL = 0, PTO_SCENE_GLTF = 1, PTO_SCENE_SKY = 2, PTO_SCENE_HDRI = 3 };
+enum { PTO_SCENE_CORNELL = 0, PTO_SCENE_GLTF = 1, PTO_SCENE_SKY = 2, PTO_SCENE_HDRI = 3, PTO_SCENE_QUADRIC = 4 };
 
 /* One frame's uniforms, by the names the setup scripts push (js/GLTF_Model_Path_Tracing.js:813-848,
  * js/Babylon_Path_Tracing.js:339-363). Matrices are Babylon Matrix.m (GLSL column-major). */
@@ -48,6 +48,11 @@ typedef struct pto_frame {
     float uSunDirection[3];              /* sky, hdri */
     float uHDRExposure, uSunPower;       /* hdri */
     const float* hdr; int32_t hdrW, hdrH; /* tHDRTexture: RGBA32F, GL row order (invertY applied), bilinear, REPEAT */
+    /* quadric: uSphere/Cylinder/Cone/Paraboloid/Hyperboloid/Capsule/FlattenedRing/Box/
+     * PyramidFrustum/Disk/Rectangle/TorusInvMatrix, in SceneIntersect order */
+    float uShapeInvMatrix[12][16];
+    float uShapeK;
+    int32_t uAllShapesMatType;
 } pto_frame;
 
 typedef struct pto_counters {
@@ -72,6 +77,10 @@ int pto_gbuffer(const pto_frame* f, float* gbuf, int row0, int row1, int nthread
 
 /* Get_Sky_Color (js/PathTracingCommon.js:416-475) for n directions (xyz triples) -> rgb triples. */
 int pto_sky_color(const float sun[3], const float* dirs, float* out, int n);
+
+/* One transformed-quadric intersector (shape = SceneIntersect order 0..11) on n object-space rays:
+ * t (INFINITY = 1e6 on a miss) and the unnormalised object-space normal. */
+int pto_quadric_probe(int shape, float k, const float* ro, const float* rd, float* t, float* nrm, int n);
 
 /* screenOutput pass (js/PathTracingCommon.js:19-309): RGBA32F accumulation -> RGBA8 canvas. */
 int pto_screen_output(int width, int height, const float* acc, float uOneOverSampleCounter,

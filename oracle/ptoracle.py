@@ -13,7 +13,10 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libptoracle.so")
 
-SCENES = {"cornell": 0, "gltf": 1, "sky": 2, "hdri": 3}
+SCENES = {"cornell": 0, "gltf": 1, "sky": 2, "hdri": 3, "quadric": 4}
+SHAPES = ("uSphereInvMatrix", "uCylinderInvMatrix", "uConeInvMatrix", "uParaboloidInvMatrix", "uHyperboloidInvMatrix",
+          "uCapsuleInvMatrix", "uFlattenedRingInvMatrix", "uBoxInvMatrix", "uPyramidFrustumInvMatrix", "uDiskInvMatrix",
+          "uRectangleInvMatrix", "uTorusInvMatrix")
 
 c_f = ctypes.c_float
 c_i = ctypes.c_int32
@@ -44,6 +47,7 @@ class Frame(ctypes.Structure):
         ("uSunDirection", c_f * 3),
         ("uHDRExposure", c_f), ("uSunPower", c_f),
         ("hdr", ctypes.c_void_p), ("hdrW", c_i), ("hdrH", c_i),
+        ("uShapeInvMatrix", (c_f * 16) * 12), ("uShapeK", c_f), ("uAllShapesMatType", c_i),
     ]
 
 
@@ -71,6 +75,7 @@ def lib():
         L.pto_screen_output.argtypes = [c_i, c_i, ctypes.c_void_p, c_f, c_f, ctypes.c_void_p, c_i]
         L.pto_math_probe.argtypes = [c_i, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
         L.pto_sky_color.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
+        L.pto_quadric_probe.argtypes = [c_i, c_f, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
         _lib = L
     return _lib
 
@@ -92,6 +97,10 @@ class Scene:
         f.scene = SCENES[self.scene]
         f.width, f.height = self.width, self.height
         for name, (kind, vals) in uniforms.items():
+            if name in SHAPES:
+                for i, v in enumerate(vals):
+                    f.uShapeInvMatrix[SHAPES.index(name)][i] = v
+                continue
             if not hasattr(f, name):
                 continue
             cur = getattr(f, name)
@@ -159,3 +168,14 @@ def sky_color(sun, dirs):
     out = np.zeros_like(dirs)
     lib().pto_sky_color(sun.ctypes.data, dirs.ctypes.data, out.ctypes.data, dirs.shape[0])
     return out
+
+
+def quadric_probe(shape, k, ro, rd):
+    """The oracle's unit-shape intersector `shape` (0..11, SceneIntersect order) on object-space rays."""
+    ro = np.ascontiguousarray(ro, dtype=np.float32).reshape(-1, 3)
+    rd = np.ascontiguousarray(rd, dtype=np.float32).reshape(-1, 3)
+    t = np.zeros(ro.shape[0], np.float32)
+    n = np.zeros_like(ro)
+    if lib().pto_quadric_probe(shape, k, ro.ctypes.data, rd.ctypes.data, t.ctypes.data, n.ctypes.data, ro.shape[0]) != 0:
+        raise ValueError("bad shape")
+    return t, n

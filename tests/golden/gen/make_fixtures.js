@@ -10,7 +10,7 @@
 // (tests/golden/*.npz / *.json, packed by make_fixtures.py).
 //
 // usage: node make_fixtures.js <scene> <outdir> [width height frames seed model]
-//   scene: cornell | gltf | sky | hdri
+//   scene: cornell | gltf | sky | hdri | quadric
 'use strict';
 const fs = require('fs');
 const path = require('path');
@@ -104,6 +104,7 @@ const scripts = {
   sky: ['js/PathTracingCommon.js', 'js/PhysicalSkyModel_FragmentShader.js', 'js/Physical_Sky_Model.js'],
   gltf: ['js/PathTracingCommon.js', 'js/GLTFModelPathTracing_FragmentShader.js', 'js/BVH_Fast_Builder.js', 'js/GLTF_Model_Path_Tracing.js'],
   hdri: ['js/PathTracingCommon.js', 'js/HDRIEnvironmentPathTracing_FragmentShader.js', 'js/BVH_Fast_Builder.js', 'js/HDRI_Environment_Path_Tracing.js'],
+  quadric: ['js/PathTracingCommon.js', 'js/TransformedQuadricGeometry_FragmentShader.js', 'js/Transformed_Quadric_Geometry.js'],
 };
 // the setup scripts resolve models/ and textures/ relative to the page: make them absolute file URLs
 const realLoad = REAL.SceneLoader.LoadAssetContainer.bind(REAL.SceneLoader);

@@ -42,6 +42,7 @@ STREAMS = [
     ("gltf_helmet_320x180", "gltf", 320, 180, 3, 9, "Damaged Helmet"),
     ("hdri_teapot_320x180", "hdri", 320, 180, 3, 11, "Utah Teapot"),
     ("hdri_helmet_320x180", "hdri", 320, 180, 3, 13, "Damaged Helmet"),
+    ("quadric_256", "quadric", 256, 256, 3, 17, None),
 ]
 
 

@@ -66,6 +66,7 @@ const scripts = {
   sky: ['js/PathTracingCommon.js', 'js/PhysicalSkyModel_FragmentShader.js', 'js/Physical_Sky_Model.js'],
   gltf: ['js/PathTracingCommon.js', 'js/GLTFModelPathTracing_FragmentShader.js', 'js/BVH_Fast_Builder.js', 'js/GLTF_Model_Path_Tracing.js'],
   hdri: ['js/PathTracingCommon.js', 'js/HDRIEnvironmentPathTracing_FragmentShader.js', 'js/BVH_Fast_Builder.js', 'js/HDRI_Environment_Path_Tracing.js'],
+  quadric: ['js/PathTracingCommon.js', 'js/TransformedQuadricGeometry_FragmentShader.js', 'js/Transformed_Quadric_Geometry.js'],
 };
 const tick = () => new Promise((r) => setImmediate(r));
 let engine = null;

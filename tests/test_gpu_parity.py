@@ -125,6 +125,7 @@ def backend(request, engine):
     ("gltf_helmet_320x180", None),
     ("hdri_teapot_320x180", None),
     ("hdri_helmet_320x180", None),
+    ("quadric_256", None),
 ])
 def test_stream_bitexact(engine, backend, name, frames):
     """Whole recorded streams (path trace -> copy -> output per frame) match the oracle exactly."""
@@ -136,6 +137,37 @@ def test_stream_bitexact(engine, backend, name, frames):
     for i, (ra, ga, rc, gc) in enumerate(zip(ref_acc, got_acc, ref_can, got_can)):
         assert _bits_equal(ra, ga), "%s frame %d accumulation: %s" % (name, i, _diff_report(ra, ga))
         assert _bits_equal(rc, gc), "%s frame %d canvas: %s" % (name, i, _diff_report(rc, gc))
+
+
+def _quadric_variant(mat, k, rotate):
+    """The recorded quadric stream with every shape switched to material `mat`, uShapeK = k and,
+    optionally, each shape's inverse matrix rotated (what the GUI controls change)."""
+    import copy
+    meta = copy.deepcopy(H.stream("quadric_256"))
+    th = 0.7
+    rx = np.array([[1, 0, 0, 0], [0, np.cos(th), -np.sin(th), 0], [0, np.sin(th), np.cos(th), 0], [0, 0, 0, 1]])
+    rz = np.array([[np.cos(th), -np.sin(th), 0, 0], [np.sin(th), np.cos(th), 0, 0], [0, 0, 1, 0], [0, 0, 0, 1]])
+    for f in meta["frames"]:
+        u = H.path_call(f)["uniforms"]
+        u["uAllShapesMatType"] = ["i", [mat]]
+        u["uShapeK"] = ["f", [k]]
+        if rotate:
+            for name in list(u):
+                if name.endswith("InvMatrix") and name != "uCameraMatrix":
+                    m = np.array(u[name][1], np.float64).reshape(4, 4)
+                    u[name] = ["f", [float(v) for v in np.float32(m @ rx @ rz).reshape(-1)]]
+    return meta
+
+
+@pytest.mark.parametrize("mat,k,rotate", [(1, 0.5, False), (2, 0.8, True), (3, 0.3, True), (4, 1.0, True)])
+def test_quadric_materials_and_transforms_bitexact(engine, backend, mat, k, rotate):
+    """All twelve unit shapes under each material, a non-default uShapeK and rotated transforms."""
+    meta = _quadric_variant(mat, k, rotate)
+    ref_acc, ref_can, _ = H.oracle_replay(meta, 2, with_output=True)
+    got_acc, got_can, _ = _replay_gpu(engine, meta, 2)
+    for ra, ga, rc, gc in zip(ref_acc, got_acc, ref_can, got_can):
+        assert _bits_equal(ra, ga), _diff_report(ra, ga)
+        assert _bits_equal(rc, gc), _diff_report(rc, gc)
 
 
 def test_bunny_1080p_bitexact_and_counters(engine, backend):
@@ -224,10 +256,7 @@ def test_errors_are_codes_not_crashes(engine):
     import babylon_pt as bp
     with pytest.raises(bp.PtError, match="PT_ERR_SHADER"):
         bp.EffectWrapper(engine, "void main() {}", [], [], "bogus")
-    fx = bp.EffectWrapper(engine, "quadric", ["uTorusInvMatrix"], ["previousBuffer"], "quadric")
     rt = bp.RenderTargetTexture("rt", (16, 16), engine)
-    with pytest.raises(bp.PtError, match="PT_ERR_UNSUPPORTED"):
-        bp.EffectRenderer(engine).render(fx, rt)
     pt = bp.EffectWrapper(engine, "cornell", ["uResolution"], ["previousBuffer", "blueNoiseTexture"], "pt")
     with pytest.raises(bp.PtError, match="PT_ERR_STATE"):
         bp.EffectRenderer(engine).render(pt, rt)      # samplers unbound

@@ -44,7 +44,7 @@ def hdr_dir(tmp_path_factory):
 
 
 @pytest.mark.parametrize("name", ["cornell_256", "sky_256", "gltf_teapot_320x180", "gltf_bunny_1080p", "gltf_helmet_320x180",
-                                  "hdri_teapot_320x180"])
+                                  "hdri_teapot_320x180", "quadric_256"])
 def test_unmodified_setup_script_drives_the_shim(name, hdr_dir):
     meta = H.stream(name)
     env = {"PT_ASSET_DIR": hdr_dir[0]} if meta["scene"] == "hdri" else None

@@ -200,3 +200,58 @@ def test_sky_scene_properties():
     assert (a[..., 3] == np.float32(1.01)).mean() > 0.05
     assert a[..., :3].min() >= 0.0 and a[..., :3].mean() > 0.1
     assert cnts[0]["node_fetches"] == 0 and cnts[0]["segments"] > cnts[0]["paths"]
+
+
+def _implicit(shape, k, p):
+    """Residual of each unit shape's surface at p (js/PathTracingCommon.js:690-1163), float64."""
+    x, y, z = p[:, 0], p[:, 1], p[:, 2]
+    r2 = x * x + z * z
+    if shape == 0:
+        return np.abs(x * x + y * y + z * z - 1)
+    if shape == 1:
+        return np.abs(r2 - 1)
+    if shape in (2, 8):
+        kk = min(max(k, 0.01), 1.0)
+        j, h = 1 / kk, 2 / kk - 1
+        if shape == 2:
+            return np.abs(j * r2 - kk * 0.25 * (y - h) ** 2)
+        fx = np.abs(j * x * x - kk * 0.25 * (y - h) ** 2)
+        fz = np.abs(j * z * z - kk * 0.25 * (y - h) ** 2)
+        return np.minimum(fx, fz)
+    if shape == 3:
+        return np.abs(r2 + 0.5 * (y - 1))
+    if shape == 4:
+        K = (k ** 4 + 0.0012) * 1000
+        return np.abs(K * r2 - (K - 1) * y * y - 1) / K
+    if shape == 5:
+        kk = k + 0.25
+        cyl = np.abs(r2 - 1)
+        cap = np.minimum(np.abs(r2 + (y - kk) ** 2 - 1), np.abs(r2 + (y + kk) ** 2 - 1))
+        return np.where(np.abs(y) <= kk, cyl, cap)
+    if shape == 6:
+        kk = k - 0.01
+        return np.minimum.reduce([np.abs(r2 - 1), np.abs(r2 - kk), np.abs(np.abs(y) - 1)])
+    if shape == 7:
+        return np.abs(np.maximum.reduce([np.abs(x), np.abs(y), np.abs(z)]) - 1)
+    if shape in (9, 10):
+        return np.abs(y)
+    kk = 1 - min(max(k, 0.01), 0.99)
+    return np.abs(np.hypot(np.sqrt(r2) - (1 - kk), y) - kk)
+
+
+@pytest.mark.parametrize("shape", range(12))
+def test_quadric_intersectors_hit_their_surfaces(shape):
+    """Each restated intersector returns points on its shape's implicit surface (a transcription
+    check independent of rounding: sign or term errors would move the hits off the surface)."""
+    rng = np.random.default_rng(shape)
+    n = 4000
+    target = rng.uniform(-0.9, 0.9, (n, 3))
+    ro = target + rng.normal(size=(n, 3)) * 4.0
+    rd = target - ro
+    k = 0.6
+    t, _ = po.quadric_probe(shape, k, ro, rd)
+    hit = t < 1e6
+    assert hit.mean() > 0.05
+    p = ro[hit].astype(np.float64) + rd[hit].astype(np.float64) * t[hit, None].astype(np.float64)
+    tol = 0.02 if shape == 11 else 2e-3   # the torus is ray-marched to |d| < 0.01
+    assert np.quantile(_implicit(shape, k, p), 0.99) < tol
