@@ -314,6 +314,18 @@ static napi_value QueueStats(napi_env env, napi_callback_info info)
     for (uint32_t i = 0; i < 16; i++) napi_set_element(env, r, i, num(env, q[i]));
     return r;
 }
+/* pt_bvh_build(aabbIn: Float32Array (9 per triangle), work: Uint32Array, out: Float32Array) -> node count */
+static napi_value BvhBuild(napi_env env, napi_callback_info info)
+{
+    napi_value a[MAXARGS]; if (args(env, info, a, 3) < 0) return NULL;
+    size_t la, lw, lo;
+    const float* aabb = (const float*)bytes_of(env, a[0], &la);
+    const uint32_t* work = (const uint32_t*)bytes_of(env, a[1], &lw);
+    float* out = (float*)bytes_of(env, a[2], &lo);
+    int n = (int)(lw / 4);
+    if (!aabb || !work || !out || la < (size_t)n * 36) return num(env, PT_ERR_ARG);
+    return num(env, pt_bvh_build(aabb, work, n, out, (int)(lo / 32)));
+}
 static napi_value Version(napi_env env, napi_callback_info info)
 {
     napi_value r; (void)info;
@@ -337,7 +349,7 @@ static napi_value Init(napi_env env, napi_value exports)
         { "pt_bvh_layout_used", BvhLayoutUsed }, { "pt_set_stream", SetStream }, { "pt_texture_device_ptr", TexDevicePtr },
         { "pt_last_render_ms", LastRenderMs }, { "pt_timing_begin", TimingBegin }, { "pt_timing_end", TimingEnd },
         { "pt_set_counting", SetCounting }, { "pt_read_counters", ReadCounters }, { "pt_reset_counters", ResetCounters }, { "pt_queue_stats", QueueStats },
-        { "pt_version", Version },
+        { "pt_bvh_build", BvhBuild }, { "pt_version", Version },
     };
     for (size_t i = 0; i < sizeof(F) / sizeof(F[0]); i++) {
         napi_value fn;

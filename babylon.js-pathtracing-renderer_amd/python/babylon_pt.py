@@ -39,7 +39,7 @@ SYMBOLS = [
     "pt_render_target_resize", "pt_texture_size", "pt_texture_destroy",
     "pt_render", "pt_read_pixels", "pt_write_pixels",
     "pt_set_row_partition", "pt_set_backend", "pt_set_bvh_layout", "pt_bvh_layout_used", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
-    "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_version",
+    "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_bvh_build", "pt_version",
 ]
 
 _lib = None
@@ -74,6 +74,7 @@ def lib():
         "pt_set_row_partition": ([vp, i32, i32], i32), "pt_texture_device_ptr": ([vp], vp),
         "pt_set_backend": ([vp, i32], i32), "pt_set_stream": ([vp, vp], i32),
         "pt_set_bvh_layout": ([vp, i32], i32), "pt_bvh_layout_used": ([vp], i32),
+        "pt_bvh_build": ([vp, vp, i32, vp, i32], i32),
         "pt_last_render_ms": ([vp, i32, f32p], i32), "pt_set_counting": ([vp, i32], i32),
         "pt_timing_begin": ([vp], i32),
         "pt_timing_end": ([vp, i32, ctypes.POINTER(ctypes.c_double), ip], i32),
@@ -357,6 +358,19 @@ class EffectRenderer:
 
 SHADER_PROG = {"pathTracingFragmentShader": None, "screenCopyFragmentShader": "screenCopy",
                "screenOutputFragmentShader": "screenOutput"}
+
+
+def bvh_build(aabb_in, work=None):
+    """BVH_Build_Iterative (js/BVH_Fast_Builder.js) in libpt: (n, 9) per-triangle AABBs ->
+    (2n-1, 8) float32 nodes in the tAABBTexture layout."""
+    aabb_in = np.ascontiguousarray(aabb_in, dtype=np.float32).reshape(-1, 9)
+    n = aabb_in.shape[0]
+    work = np.arange(n, dtype=np.uint32) if work is None else np.ascontiguousarray(work, dtype=np.uint32)
+    out = np.zeros((2 * len(work), 8), np.float32)
+    rc = lib().pt_bvh_build(aabb_in.ctypes.data, work.ctypes.data, len(work), out.ctypes.data, out.shape[0])
+    if rc < 0:
+        raise PtError("pt_bvh_build: %s" % ERRORS.get(rc, rc))
+    return out[:rc]
 
 
 def splitmix64_uniforms(seed, n):

@@ -163,6 +163,13 @@ int pt_reset_counters(pt_ctx* ctx);
 int pt_queue_stats(pt_ctx* ctx, uint32_t out[16]);
 /* Device self-test of the pinned GLSL built-ins (ops as the oracle's pto_math_probe). */
 int pt_math_probe(pt_ctx* ctx, int op, const float* x, const float* y, float* out, int n);
+/* BVH_Build_Iterative(workList, aabb_array) (js/BVH_Fast_Builder.js:320-406) as native host code:
+ * aabb_in = the per-triangle AABBs the setup script fills (9 floats: min.xyz, max.xyz,
+ * centroid.xyz; js/GLTF_Model_Path_Tracing.js:421-454), work = the triangle ids to build over
+ * (n of them). Writes 8 floats per node, depth-first, exactly the reference's tAABBTexture layout
+ * and bits, and returns the node count (2n-1), or a negative pt_status (max_nodes too small). No
+ * context or device needed. */
+int pt_bvh_build(const float* aabb_in, const uint32_t* work, int n, float* nodes_out, int max_nodes);
 /* Library identity: "libpt <version> gfx950" */
 const char* pt_version(void);
 

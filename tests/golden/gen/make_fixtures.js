@@ -113,8 +113,19 @@ BABYLON.SceneLoader = Object.assign(Object.create(REAL.SceneLoader), { LoadAsset
 const tick = () => new Promise((r) => setImmediate(r));
 function frame() { frames.push([]); renderLoop(); }
 
+// the BVH builder's own input (per-triangle AABB min/max/centroid, js/GLTF_Model_Path_Tracing.js:
+// 421-454), captured as BVH_Build_Iterative receives it: the native builder is pinned against it
+let builderInput = null;
+function wrapBuilder() {
+  const real = vm.runInThisContext('BVH_Build_Iterative');
+  globalThis.BVH_Build_Iterative = function (workList, aabb) {
+    builderInput = { work: Uint32Array.from(workList), aabb: Float32Array.from(aabb.subarray(0, 9 * workList.length)) };
+    return real(workList, aabb);
+  };
+}
+
 (async () => {
-  for (const s of scripts[scene]) runScript(s);
+  for (const s of scripts[scene]) { runScript(s); if (s.endsWith('BVH_Fast_Builder.js')) wrapBuilder(); }
   const meshTextures = () => rawTextures.filter((t) => t.h === 2048);
   const hdrTextures = () => rawTextures.filter((t) => t.h !== 2048);
   if (scene === 'gltf' || scene === 'hdri') {
@@ -149,6 +160,9 @@ function frame() { frames.push([]); renderLoop(); }
     const nodes = 2 * tris - 1;
     fs.writeFileSync(path.join(outdir, 'bvh.f32'), Buffer.from(aabb.data.buffer, 0, nodes * 8 * 4));
     fs.writeFileSync(path.join(outdir, 'tri.f32'), Buffer.from(tri.data.buffer, 0, tris * 32 * 4));
+    if (!builderInput || builderInput.work.length !== tris) throw new Error('builder input not captured');
+    for (let i = 0; i < tris; i++) if (builderInput.work[i] !== i) throw new Error('unexpected work list');
+    fs.writeFileSync(path.join(outdir, 'aabb_in.f32'), Buffer.from(builderInput.aabb.buffer));
     meta.triangles = tris; meta.nodes = nodes;
     meta.textures = { [aabb.name]: 'bvh', [tri.name]: 'tri' };
     meta.modelScale = vm.runInThisContext('modelInitialScale');

@@ -59,7 +59,8 @@ def run_stream(name, scene, w, h, frames, seed, model, tmp):
         n = meta["triangles"]
         bvh = np.fromfile(os.path.join(out, "bvh.f32"), dtype="<f4").reshape(2 * n - 1, 8)
         tri = np.fromfile(os.path.join(out, "tri.f32"), dtype="<f4").reshape(n, 32)
-        mesh = (bvh, tri)
+        aabb_in = np.fromfile(os.path.join(out, "aabb_in.f32"), dtype="<f4").reshape(n, 9)
+        mesh = (bvh, tri, aabb_in)
     return meta, mesh
 
 
@@ -145,8 +146,9 @@ def main():
             with open(os.path.join(GOLD, name + ".json"), "w") as f:
                 json.dump(meta, f, indent=0)
             manifest[name] = {"scene": scene, "width": w, "height": h, "frames": frames, "seed": seed, "model": model}
-        for key, (bvh, tri) in meshes.items():
-            np.savez_compressed(os.path.join(GOLD, "mesh_%s.npz" % key), bvh=bvh, tri=tri)
+        for key, (bvh, tri, aabb_in) in meshes.items():
+            # aabb_in: BVH_Build_Iterative's input (js/BVH_Fast_Builder.js:320), work list = 0..N-1
+            np.savez_compressed(os.path.join(GOLD, "mesh_%s.npz" % key), bvh=bvh, tri=tri, aabb_in=aabb_in)
             manifest["mesh_" + key] = {
                 "triangles": int(tri.shape[0]), "nodes": int(bvh.shape[0]), "depth": tree_depth(bvh),
                 "sha256_bvh": hashlib.sha256(bvh.tobytes()).hexdigest(),

@@ -76,7 +76,13 @@ const frame = () => { frames.push([]); engine.stepFrame(); };
 const f32s = () => { let n = 0; for (const f of frames) for (const c of f) for (const k in c.samplers) if (String(c.samplers[k]).startsWith('raw')) n++; return n; };
 
 (async () => {
-  for (const s of scripts[scene]) vm.runInThisContext(fs.readFileSync(path.join(REF, s), 'utf8'), { filename: s });
+  for (const s of scripts[scene]) {
+    vm.runInThisContext(fs.readFileSync(path.join(REF, s), 'utf8'), { filename: s });
+    // PT_NATIVE_BVH=1: the page's builder replaced by libpt's (only pt_bvh_build of the real
+    // addon runs: host code, no device)
+    if (s.endsWith('BVH_Fast_Builder.js') && process.env.PT_NATIVE_BVH === '1')
+      globalThis.BVH_Build_Iterative = shim.nativeBVH(shim.loadAddon());
+  }
   const meshRaw = () => rawData.filter((d) => d.length === 2048 * 2048 * 4).length;
   const envRaw = () => rawData.length - meshRaw();
   if (scene === 'gltf' || scene === 'hdri') {
