@@ -176,6 +176,19 @@ PT_D float box(f3 mn, f3 mx, f3 ro, f3 inv)
     float t1 = gmin(gmin(gmax(nr.x, fr.x), gmax(nr.y, fr.y)), gmax(nr.z, fr.z));
     return gmax(t0, 0.0f) > t1 ? kINF : t0;
 }
+// box() for a ray whose model-space origin and inverse direction are finite and nonzero and a box
+// without NaN: then no slab product is NaN, and IEEE min/max (v_min3 / v_max3) pick the same values
+// as the GLSL's y<x?y:x forms up to the sign of a zero, which only ever feeds comparisons
+PT_D float boxFast(f3 mn, f3 mx, f3 ro, f3 inv)
+{
+    f3 nr = (mn - ro) * inv;
+    f3 fr = (mx - ro) * inv;
+    float t0 = fmaxf(fmaxf(fminf(nr.x, fr.x), fminf(nr.y, fr.y)), fminf(nr.z, fr.z));
+    float t1 = fminf(fminf(fmaxf(nr.x, fr.x), fmaxf(nr.y, fr.y)), fmaxf(nr.z, fr.z));
+    return fmaxf(t0, 0.0f) > t1 ? kINF : t0;
+}
+PT_D bool finite3(f3 v) { return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z); }
+
 PT_D float bvhTriangle(f3 v0, f3 v1, f3 v2, f3 ro, f3 rd, float& u, float& v, bool dbl)
 {
     f3 e1 = v1 - v0, e2 = v2 - v0;
@@ -333,6 +346,8 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     const float4* R = a.bvh_pairs;
     const float4* LR = a.bvh_leaves;
     float code = a.bvh_root_code;
+    // records are NaN-free (checked at build); see boxFast
+    const bool fast = finite3(O) && finite3(inv) && inv.x != 0.0f && inv.y != 0.0f && inv.z != 0.0f;
     int sp = 0;
     bool skip = curT < hitT;
     for (;;) {
@@ -349,8 +364,14 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
             const float4* rec = R + 4u * (unsigned)code;
             const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
             r.nodes += 2;
-            float tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
-            float tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+            float tA, tB;
+            if (fast) {
+                tA = boxFast(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
+                tB = boxFast(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+            } else {
+                tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
+                tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+            }
             float cA = r3.x, cB = r3.y;
             if (tB < tA) {
                 float tt = tB; tB = tA; tA = tt;

@@ -396,6 +396,8 @@ __global__ __launch_bounds__(256) void pt_pairs_kinds(const float4* aabb, long l
     const float4 c0 = fetch32(aabb, texels, fn * 2.0f), c1 = fetch32(aabb, texels, fn * 2.0f + 1.0f);
     const bool in = c0.x < 0.0f;
     inner[n] = in ? 1 : 0;
+    // boxFast needs NaN-free boxes
+    if (c0.y != c0.y || c0.z != c0.z || c0.w != c0.w || c1.y != c1.y || c1.z != c1.z || c1.w != c1.w) atomicOr(bad, 1u);
     if (n == 0 && !in) leafref[0] = 1;
     if (!in) return;
     const float idA = fn + 1.0f, idB = c1.x;
