@@ -156,13 +156,19 @@ PT_D float unitSphere(f3 ro, f3 rd, f3& n)
     return t;
 }
 // TriangleIntersect, single-sided (QuadIntersect passes isDoubleSided = false), edges precomputed
+// 1/x < 0 without the division: x negative and finite (1/x of a finite float never underflows to
+// zero), or x = -0 (1/-0 = -inf); -inf (1/-inf = -0) and NaN are not
+PT_D bool recipNegative(float x) { return (x < 0.0f && x != -__builtin_inff()) || (x == 0.0f && __builtin_signbit(x)); }
+
 PT_D float quadTriangle(const TriArg& T, f3 ro, f3 rd)
 {
     f3 pv = cross(rd, T.e2);
-    float det = 1.0f / dot(T.e1, pv);
-    if (det < 0.0f) return kINF;
+    const float dd = dot(T.e1, pv);
+    if (recipNegative(dd)) return kINF;   // det < 0: back face, decided before the division
+    float det = 1.0f / dd;
     f3 tv = ro - T.v0;
     float u = dot(tv, pv) * det;
+    if (u < 0.0f || u > 1.0f) return kINF;   // the miss is an OR: its first terms decide early
     f3 qv = cross(tv, T.e1);
     float v = dot(rd, qv) * det;
     float t = dot(T.e2, qv) * det;
@@ -193,9 +199,12 @@ PT_D float bvhTriangle(f3 v0, f3 v1, f3 v2, f3 ro, f3 rd, float& u, float& v, bo
 {
     f3 e1 = v1 - v0, e2 = v2 - v0;
     f3 pv = cross(rd, e2);
-    float det = 1.0f / dot(e1, pv);
+    const float dd = dot(e1, pv);
+    if (!dbl && recipNegative(dd)) return kINF;   // (u, v are only read for a hit)
+    float det = 1.0f / dd;
     f3 tv = ro - v0;
     u = dot(tv, pv) * det;
+    if (u < 0.0f || u > 1.0f) return kINF;
     f3 qv = cross(tv, e1);
     v = dot(rd, qv) * det;
     float t = dot(e2, qv) * det;
@@ -272,7 +281,14 @@ template <class Stk>
 PT_D void stackPush(const TraceArgs& a, Stk& st, int si, float2 e, unsigned& ovf)
 {
     if (si < kStackLevels) st.put(si, e);
-    else { ovf++; atomicOr(a.err, (unsigned)E_STACK); }   // GLSL would write out of bounds
+    else { ovf++; atomicOr(a.err, (unsigned)E_STACK); }   // GLSL would write out of bounds: dropped
+}
+// a pop past stackLevels[27] (undefined in the GLSL) yields `sentinel`, whose tNear = INFINITY the
+// walk culls at once (pinned with the oracle; nothing is read out of bounds)
+template <class Stk>
+PT_D float2 stackPop(const Stk& st, int si, float2 sentinel)
+{
+    return si < kStackLevels ? st.get(si) : sentinel;
 }
 
 // The reference layout: a pushed entry is (node id, tNear); a pop re-fetches the node's two texels.
@@ -287,7 +303,7 @@ PT_D void bvhWalkRef(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float4 c0
         if (!skip) {
             stackptr = stackptr - 1.0f;
             if (stackptr < 0.0f) break;
-            float2 e = st.get((int)stackptr);
+            float2 e = stackPop(st, (int)stackptr, make_float2(0.0f, kINF));
             curId = e.x; curT = e.y;
             if (curT >= hitT) continue;
             c0 = fetch32(a.aabb, a.aabb_texels, curId * 2.0f);
@@ -354,7 +370,7 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
         if (!skip) {
             sp--;
             if (sp < 0) break;
-            float2 e = st.get(sp);
+            float2 e = stackPop(st, sp, make_float2(kINF, 0.0f));
             if (e.x >= hitT) continue;
             code = e.y;
             r.nodes++;

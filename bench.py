@@ -45,13 +45,13 @@ def algorithmic_bytes(cnt):
     return sum(cnt[k] * b for k, b in BYTES.items()) + PIXEL_IO * cnt["paths"]
 
 
-def cpu_baseline(meta, width, height, budget_s):
+def cpu_baseline(meta, width, height, budget_s, mesh=None):
     """The CPU oracle (C restatement of the reference GLSL, OpenMP over rows) on this host,
     timing whole 1920x1080 frames of the same stream until ~budget_s of wall time is spent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import helpers as H
     cores = min(16, os.cpu_count() or 1)
-    sc = H.oracle_scene(meta, width, height)
+    sc = H.oracle_scene(meta, width, height, mesh)
     acc = np.zeros((height, width, 4), np.float32)
     frames, t0 = 0, time.perf_counter()
     while True:
@@ -64,7 +64,7 @@ def cpu_baseline(meta, width, height, budget_s):
             break
     return {"value": round(frames * width * height / dt / 1e6, 3), "unit": "Mpaths/s", "cores": cores,
             "kind": "port",
-            "sample": "%d full %dx%d frames of the bunny stream, CPU oracle (C restatement, OpenMP %d threads), %.1f s"
+            "sample": "%d full %dx%d frames of the bench stream, CPU oracle (C restatement, OpenMP %d threads), %.1f s"
                       % (frames, width, height, cores, dt)}
 
 
@@ -83,6 +83,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-oracle baseline (0 = skip)")
     ap.add_argument("--no-output", action="store_true", help="time pathTracing+copy only (no screenOutput/gather)")
+    ap.add_argument("--workload", choices=("bunny", "dragon"), default="bunny",
+                    help="bunny: BASELINE configs[1] (the reference's StanfordBunny through its own builder); "
+                         "dragon: the 524,288-triangle StanfordDragon stand-in (helpers.synthetic_dragon)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,7 +105,8 @@ def main():
     meta = H.stream("gltf_bunny_1080p")
     W, Hh = frame_size(world)
     engine = bp.Engine(local)
-    mesh = H.texture_payloads(meta, H.mesh(meta))
+    mesh_arrays = H.synthetic_dragon() if args.workload == "dragon" else H.mesh(meta)
+    mesh = H.texture_payloads(meta, mesh_arrays)
 
     rt_ptrs, acc_t, full_t = None, None, None
     pad_bands = bp.padded_bands(Hh, world)
@@ -203,11 +207,12 @@ def main():
     value = paths / elapsed / 1e6
     avg_launch_ms = pt_ms / max(1, pt_n)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
-    workload = "gltf_bunny_%dx%d" % (W, Hh)
+    workload = "gltf_%s_%dx%d" % ("bunny" if args.workload == "bunny" else "dragon_standin", W, Hh)
     pmc = load_pmc(workload)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     line = {
-        "metric": "Mpaths/s (StanfordBunny glTF scene, 1 spp per frame, full pathTracing+screenCopy+screenOutput frame)",
+        "metric": "Mpaths/s (%s glTF scene, 1 spp per frame, full pathTracing+screenCopy+screenOutput frame)"
+                  % ("StanfordBunny" if args.workload == "bunny" else "StanfordDragon stand-in"),
         "value": round(value, 2),
         "unit": "Mpaths/s",
         "n_gpus": world,
@@ -218,9 +223,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: the reference setup script's recorded StanfordBunny uniform stream, continued with fresh uRandomVec2 per frame; mesh textures = the reference BVH_Fast_Builder output",
+        "data": ("synthetic: the reference setup script's recorded StanfordBunny uniform stream, continued with fresh "
+                 "uRandomVec2 per frame; mesh textures = " +
+                 ("the reference BVH_Fast_Builder output" if args.workload == "bunny" else
+                  "a 524,288-triangle procedural stand-in for the missing StanfordDragon.glb, built by the native builder")),
         "config": {"workload": workload, "width": W, "height": Hh, "spp_per_frame": 1, "max_bounces": 6,
-                   "triangles": int(meta.get("triangles", 0)), "parallelism": "row-bands x%d" % world,
+                   "triangles": int(mesh_arrays["tri"].shape[0]), "parallelism": "row-bands x%d" % world,
                    "gather": "rccl gather of RGBA32F bands to rank 0 per frame" if world > 1 else None},
         "pathtrace_mpaths_per_s": round(W * Hh / world / (avg_launch_ms * 1e-3) / 1e6 * world, 2),
         "kernel_ms": {"pathtrace": round(avg_launch_ms, 4), "screen_copy": round(cp_ms / max(1, pt_n), 4),
@@ -232,7 +240,7 @@ def main():
                      "counts_per_launch": {k: v / nc for k, v in cnt.items()}},
     }
     if args.cpu_budget > 0:
-        line["cpu_baseline"] = cpu_baseline(meta, 1920, 1080, args.cpu_budget) if world == 1 else None
+        line["cpu_baseline"] = cpu_baseline(meta, 1920, 1080, args.cpu_budget, mesh_arrays) if world == 1 else None
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

@@ -684,7 +684,10 @@ static void SceneIntersect(Inv* s, v3 rayOrigin, v3 rayDirection, Hit* h)
             stackptr = stackptr - 1.0f;
             if (stackptr < 0.0f) break;
             int si = (int)stackptr;
-            curId = stackId[si]; curT = stackT[si];
+            /* pinned: stackLevels[28] out of bounds (the GLSL is undefined there): a push past
+             * level 27 is dropped, a pop past it yields (0, INFINITY), which the cull below skips */
+            if (si < STACK_LEVELS) { curId = stackId[si]; curT = stackT[si]; }
+            else { curId = 0.0f; curT = INFINITY_G; }
             if (curT >= h->t) continue;
             NODE(curId, c0, c1);
         }

@@ -159,3 +159,64 @@ def write_radiance_hdr(path, rgbe):
                 parts.append(bytes([x - start]) + ch[start:x].tobytes())
     with open(path, "wb") as f:
         f.write(b"".join(parts))
+
+
+def synthetic_dragon(nu=512, nv=512, knot=(1, 1), tube=9.0):
+    """A deterministic stand-in for StanfordDragon.glb (not in the reference, SURVEY.md §8d config
+    4): a bumpy (p, q) torus-knot tube (default (1, 1): a bumpy torus, BVH depth 29, no stack
+    overflow; (2, 3) nests deeper than stackLevels[28]) of nu x nv x 2 triangles (524,288 at the default, the most the
+    2048x2048 triangle texture holds), packed exactly as Prepare_Model_For_PathTracing packs a
+    model (js/GLTF_Model_Path_Tracing.js:296-454: float64 vertex math, float32 storage, UVs -1,
+    per-triangle AABBs) and built by the native builder (bit-identical to BVH_Fast_Builder.js).
+    Returns {"bvh": (2N-1, 8), "tri": (N, 32), "aabb_in": (N, 9)}."""
+    import babylon_pt as bp
+    t = np.arange(nu) * (2 * np.pi / nu)
+    v = np.arange(nv) * (2 * np.pi / nv)
+
+    p, q = knot
+
+    def curve(tt):
+        r = 2.0 + np.cos(q * tt)
+        return np.stack([r * np.cos(p * tt), r * np.sin(q * tt) * 0.6, r * np.sin(p * tt)], -1) * 9.0 + [0, -10, 0]
+
+    c = curve(t)
+    tan = curve(t + 1e-4) - curve(t - 1e-4)
+    tan /= np.linalg.norm(tan, axis=1, keepdims=True)
+    # rotation-minimising frame by parallel transport from an arbitrary start
+    nrm = np.zeros_like(c)
+    n0 = np.cross(tan[0], [0.0, 0.0, 1.0])
+    nrm[0] = n0 / np.linalg.norm(n0)
+    for i in range(1, nu):
+        n1 = nrm[i - 1] - tan[i] * np.dot(nrm[i - 1], tan[i])
+        nrm[i] = n1 / np.linalg.norm(n1)
+    bin_ = np.cross(tan, nrm)
+    rad = tube * (1.0 + 0.18 * np.sin(17 * t)[:, None] * np.sin(5 * v)[None, :] + 0.07 * np.sin(41 * t)[:, None])
+    ring = np.cos(v)[None, :, None] * nrm[:, None, :] + np.sin(v)[None, :, None] * bin_[:, None, :]
+    P = c[:, None, :] + rad[..., None] * ring                               # (nu, nv, 3) float64
+    du = np.roll(P, -1, 0) - np.roll(P, 1, 0)
+    dv = np.roll(P, -1, 1) - np.roll(P, 1, 1)
+    N = np.cross(du, dv)
+    N *= np.sign(np.sum(N * ring, -1))[..., None]                           # outward
+    N /= np.linalg.norm(N, axis=-1, keepdims=True)
+    i0, j0 = np.meshgrid(np.arange(nu), np.arange(nv), indexing="ij")
+    i1, j1 = (i0 + 1) % nu, (j0 + 1) % nv
+    a = np.stack([i0, j0], -1).reshape(-1, 2)
+    b = np.stack([i1, j0], -1).reshape(-1, 2)
+    cc = np.stack([i1, j1], -1).reshape(-1, 2)
+    d = np.stack([i0, j1], -1).reshape(-1, 2)
+    tris = np.stack([np.stack([a, b, cc], 1), np.stack([a, cc, d], 1)], 1).reshape(-1, 3, 2)
+    pos = P[tris[..., 0], tris[..., 1]]                                     # (N, 3, 3)
+    nor = N[tris[..., 0], tris[..., 1]]
+    # front faces outward: cross(e1, e2) along the outward normal (single-sided BVH test)
+    face = np.cross(pos[:, 1] - pos[:, 0], pos[:, 2] - pos[:, 0])
+    flip = np.sum(face * nor.sum(1), -1) < 0
+    pos[flip] = pos[flip][:, ::-1]
+    nor[flip] = nor[flip][:, ::-1]
+    n = pos.shape[0]
+    tri = np.zeros((n, 32), np.float32)
+    tri[:, 0:9] = pos.reshape(n, 9)
+    tri[:, 9:18] = nor.reshape(n, 9)
+    tri[:, 18:24] = -1.0
+    lo, hi = pos.min(1), pos.max(1)
+    aabb_in = np.concatenate([lo, hi, (lo + hi) * 0.5], 1).astype(np.float32)
+    return {"bvh": bp.bvh_build(aabb_in), "tri": tri, "aabb_in": aabb_in}

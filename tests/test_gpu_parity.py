@@ -188,6 +188,51 @@ def test_bunny_1080p_bitexact_and_counters(engine, backend):
     assert cnt == ref_total
 
 
+def test_dragon_standin_1080p_bitexact_and_counters(engine, backend):
+    """A 524,288-triangle mesh (the texture's capacity; helpers.synthetic_dragon, BVH by the native
+    builder) under the bunny stream's camera at 1920x1080: BASELINE config 4's geometry scale."""
+    meta = H.stream("gltf_bunny_1080p")
+    mesh = H.synthetic_dragon()
+    ref_acc, ref_can, ref_cnt = H.oracle_replay(meta, 2, with_output=True, mesh=mesh)
+    import babylon_pt as bp
+    engine.set_counting(True)
+    engine.reset_counters()
+    try:
+        player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, mesh))
+        got_acc, got_can = [], []
+        for i in range(2):
+            player.play_frame(i)
+            engine.sync()
+            got_acc.append(player.textures["pathTracingRenderTarget"].read())
+            got_can.append(engine.read_canvas(meta["width"], meta["height"]))
+        cnt = engine.counters()
+    finally:
+        engine.set_counting(False)
+    assert engine.bvh_layout_used() == backend[1]
+    for ra, ga, rc, gc in zip(ref_acc, got_acc, ref_can, got_can):
+        assert _bits_equal(ra, ga), _diff_report(ra, ga)
+        assert _bits_equal(rc, gc), _diff_report(rc, gc)
+    assert cnt == {k: sum(c[k] for c in ref_cnt) for k in ref_cnt[0]}
+
+
+def test_stack_overflow_is_defined_and_reported(engine, backend):
+    """A tree whose walks nest deeper than stackLevels[28] (out of bounds in the GLSL): pushes past
+    level 27 are dropped and such pops are culled, identically to the oracle, nothing is read out
+    of bounds, and the draw reports PT_ERR_DATA."""
+    import babylon_pt as bp
+    meta = H.stream("gltf_bunny_1080p")
+    mesh = H.synthetic_dragon(128, 128, knot=(2, 3), tube=3.2)
+    ref_acc, _, ref_cnt = H.oracle_replay(meta, 1, width=480, height=270, mesh=mesh)
+    assert ref_cnt[0]["stack_overflow"] > 0
+    player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, mesh), 480, 270)
+    engine.resize_canvas(480, 270)
+    player.play_call(meta["frames"][0][0])
+    with pytest.raises(bp.PtError, match="PT_ERR_DATA"):
+        engine.sync()
+    engine.sync()   # the error is reported once
+    assert _bits_equal(ref_acc[0], player.textures["pathTracingRenderTarget"].read())
+
+
 @pytest.mark.parametrize("parts", [2, 3, 8])
 def test_row_partition_is_exact(engine, backend, parts):
     """Band sharding (the multi-GPU split) reproduces the full-frame result bit for bit."""
