@@ -199,12 +199,9 @@ PT_D float bvhTriangle(f3 v0, f3 v1, f3 v2, f3 ro, f3 rd, float& u, float& v, bo
 {
     f3 e1 = v1 - v0, e2 = v2 - v0;
     f3 pv = cross(rd, e2);
-    const float dd = dot(e1, pv);
-    if (!dbl && recipNegative(dd)) return kINF;   // (u, v are only read for a hit)
-    float det = 1.0f / dd;
+    float det = 1.0f / dot(e1, pv);
     f3 tv = ro - v0;
     u = dot(tv, pv) * det;
-    if (u < 0.0f || u > 1.0f) return kINF;
     f3 qv = cross(tv, e1);
     v = dot(rd, qv) * det;
     float t = dot(e2, qv) * det;

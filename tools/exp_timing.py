@@ -19,10 +19,13 @@ ap.add_argument("--stream", default="gltf_bunny_1080p")
 ap.add_argument("--frames", type=int, default=20)
 ap.add_argument("--backends", default="megakernel,wavefront")
 ap.add_argument("--layouts", default="pairs,reference")
+ap.add_argument("--dragon", action="store_true", help="the StanfordDragon stand-in mesh instead of the stream's")
 a = ap.parse_args()
 meta = H.stream(a.stream)
 e = bp.Engine(0)
-mesh = H.texture_payloads(meta, H.mesh(meta)) if meta["scene"] in ("gltf", "hdri") else None
+mesh = None
+if meta["scene"] in ("gltf", "hdri"):
+    mesh = H.texture_payloads(meta, H.synthetic_dragon() if a.dragon else H.mesh(meta))
 p = bp.StreamPlayer(e, meta, H.bluenoise(), mesh)
 prog = meta["scene"]
 import itertools  # noqa: E402
