@@ -12,7 +12,7 @@ constexpr int kBlock = 256;          // 4 waves; a block shades a 16x16 pixel ti
 constexpr int kTile = 16;            // tile edge == row-band height used for sharding
 constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing_FragmentShader.js:95
 #ifndef PT_STACK_LDS
-#define PT_STACK_LDS 10
+#define PT_STACK_LDS 8
 #endif
 constexpr int kStackLds = PT_STACK_LDS;        // levels kept in LDS per lane; deeper levels go to a global slab
 

@@ -44,11 +44,13 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, bool pair
     if (prog != PROG_GLTF && prog != PROG_HDRI) return prog;
     return prog + (textured ? PROG_TEX : 0) + (pairs ? PROG_PAIRS : 0);
 }
-// waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 96 -> 5; the
+// waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 80 -> 6; the
 // textured variant keeps 2 rather than spill)
-// (measured on bunny 1080p: the child-pair walk gains 5-7% at 5 waves, the reference walk loses)
+// (measured with 8 LDS stack levels: the child-pair walk gains 2 % on the bunny and 7 % on the
+// dragon stand-in at 6 waves over 5, although the shading code then spills 64 B; 7-8 waves and
+// more LDS levels lose; the reference walk loses above 4)
 #ifndef PT_MINWAVES_PAIRS
-#define PT_MINWAVES_PAIRS 5
+#define PT_MINWAVES_PAIRS 6
 #endif
 template <int P> constexpr int kMinWaves = kHasTex<P> ? 2 : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
 
@@ -352,58 +354,83 @@ PT_D void bvhWalkRef(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float4 c0
 // no fetch (the stack entry (tNear, code) already says what the node is), and a leaf's vertices
 // sit in a dense 48-byte record instead of the first third of a 128-byte triangle texel group:
 // both arrays together are about 3.4 MB for StanfordBunny, within one XCD's L2.
+// The walk as a resumable state machine (a step is one pop, culled or not, and/or one record):
+// `pop` = the next step pops the stack (the reference loop's !skip). `fast` = the ray qualifies
+// for boxFast (records are NaN-free, checked at build). A schedule that interleaved walk steps
+// with other lanes' shading on top of it measured slower.
+struct PairWalk {
+    float code, hitT;        // node to process, closest hit so far
+    float triID, triU, triV; // the hit triangle (lookup), its barycentrics
+    int sp;                  // stack pointer
+    bool pop, lookup;
+};
+PT_D void pairWalkBegin(PairWalk& w, float rootCode, float rootT, float hitT)
+{
+    w.code = rootCode; w.hitT = hitT; w.sp = 0;
+    w.pop = !(rootT < hitT);
+    w.lookup = false;
+    w.triID = 0.0f; w.triU = 0.0f; w.triV = 0.0f;
+}
+PT_D bool pairWalkFast(f3 O, f3 inv)
+{
+    return finite3(O) && finite3(inv) && inv.x != 0.0f && inv.y != 0.0f && inv.z != 0.0f;
+}
+// one step; false once the stack has run empty (the walk is over)
+template <class Stk>
+PT_D bool pairWalkStep(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, bool fast, Stk& st, PairWalk& w,
+                       BvhResult& r)
+{
+    if (w.pop) {
+        w.sp--;
+        if (w.sp < 0) return false;
+        const float2 e = stackPop(st, w.sp, make_float2(kINF, 0.0f));
+        if (e.x >= w.hitT) return true;
+        w.code = e.y;
+        r.nodes++;
+    }
+    w.pop = true;
+    if (w.code >= 0.0f) {
+        const float4* rec = a.bvh_pairs + 4u * (unsigned)w.code;
+        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+        r.nodes += 2;
+        float tA, tB;
+        if (fast) {
+            tA = boxFast(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
+            tB = boxFast(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+        } else {
+            tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
+            tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+        }
+        float cA = r3.x, cB = r3.y;
+        if (tB < tA) {
+            float tt = tB; tB = tA; tA = tt;
+            float tc = cB; cB = cA; cA = tc;
+        }
+        if (tB < w.hitT) { w.code = cB; w.pop = false; }
+        if (tA < w.hitT) {
+            if (!w.pop) { stackPush(a, st, w.sp, make_float2(tB, cB), r.ovf); w.sp++; }
+            w.code = cA; w.pop = false;
+        }
+        return true;
+    }
+    const float4* lf = a.bvh_leaves + 3u * (unsigned)(-1.0f - w.code);
+    const float4 t0 = lf[0], t1 = lf[1], t2 = lf[2];
+    r.leaves++;
+    float tu, tv;
+    const float d = bvhTriangle(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
+    if (d < w.hitT) { w.hitT = d; w.triID = 8.0f * t2.y; w.triU = tu; w.triV = tv; w.lookup = true; }
+    return true;
+}
 template <class Stk>
 PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float curT, float& hitT, Stk& st,
                        BvhResult& r)
 {
-    const float4* R = a.bvh_pairs;
-    const float4* LR = a.bvh_leaves;
-    float code = a.bvh_root_code;
-    // records are NaN-free (checked at build); see boxFast
-    const bool fast = finite3(O) && finite3(inv) && inv.x != 0.0f && inv.y != 0.0f && inv.z != 0.0f;
-    int sp = 0;
-    bool skip = curT < hitT;
-    for (;;) {
-        if (!skip) {
-            sp--;
-            if (sp < 0) break;
-            float2 e = stackPop(st, sp, make_float2(kINF, 0.0f));
-            if (e.x >= hitT) continue;
-            code = e.y;
-            r.nodes++;
-        }
-        skip = false;
-        if (code >= 0.0f) {
-            const float4* rec = R + 4u * (unsigned)code;
-            const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
-            r.nodes += 2;
-            float tA, tB;
-            if (fast) {
-                tA = boxFast(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
-                tB = boxFast(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
-            } else {
-                tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
-                tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
-            }
-            float cA = r3.x, cB = r3.y;
-            if (tB < tA) {
-                float tt = tB; tB = tA; tA = tt;
-                float tc = cB; cB = cA; cA = tc;
-            }
-            if (tB < hitT) { code = cB; skip = true; }
-            if (tA < hitT) {
-                if (skip) { stackPush(a, st, sp, make_float2(tB, cB), r.ovf); sp++; }
-                code = cA; skip = true;
-            }
-            continue;
-        }
-        const float4* lf = LR + 3u * (unsigned)(-1.0f - code);
-        const float4 t0 = lf[0], t1 = lf[1], t2 = lf[2];
-        r.leaves++;
-        float tu, tv;
-        float d = bvhTriangle(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
-        if (d < hitT) { hitT = d; r.triID = 8.0f * t2.y; r.triU = tu; r.triV = tv; r.lookup = true; }
-    }
+    PairWalk w;
+    pairWalkBegin(w, a.bvh_root_code, curT, hitT);
+    const bool fast = pairWalkFast(O, inv);
+    while (pairWalkStep(a, O, D, inv, dbl, fast, st, w, r)) {}
+    hitT = w.hitT;
+    if (w.lookup) { r.triID = w.triID; r.triU = w.triU; r.triV = w.triV; r.lookup = true; }
 }
 
 } // namespace pt

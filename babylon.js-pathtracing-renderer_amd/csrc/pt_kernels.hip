@@ -55,6 +55,36 @@ struct MegaStack {
     }
 };
 
+// the mesh hit's attributes (js/GLTFModelPathTracing_FragmentShader.js:300-346): interpolated
+// normal and uv from the triangle texels 2-5, optional bump map, model transform
+template <int PROG, bool COUNT>
+PT_D void meshHit(const TraceArgs& a, float triID, float triU, float triV, Hit& h, Cnt& cnt)
+{
+    float4 v2 = fetch32(a.tri, a.tri_texels, triID + 2.0f), v3 = fetch32(a.tri, a.tri_texels, triID + 3.0f),
+           v4 = fetch32(a.tri, a.tri_texels, triID + 4.0f), v5 = fetch32(a.tri, a.tri_texels, triID + 5.0f);
+    if (COUNT) cnt.hit++;
+    float triW = 1.0f - triU - triV;
+    f3 nn = normalize(mk(v2.y, v2.z, v2.w) * triW + mk(v3.x, v3.y, v3.z) * triU + mk(v3.w, v4.x, v4.y) * triV);
+    h.u = triW * v4.z + triU * v5.x + triV * v5.z;
+    h.v = triW * v4.w + triU * v5.y + triV * v5.w;
+    if (kHasTex<PROG> && a.uses_bump) {   // perturbNormal(n, vec2(1), uv), js/GLTFModelPathTracing_FragmentShader.js:72-92
+        f3 S = onb_u(nn);
+        f3 T = cross(nn, S);
+        f3 N = normalize(nn);
+        if (dot(cross(S, T), N) < 0.0f) { S = S * -1.0f; T = T * -1.0f; }
+        float tx[4];
+        texBilinear(a.bump, h.u, h.v, tx);
+        if (COUNT) cnt.tap += 4;
+        f3 mN = normalize(mk(tx[0] * 2.0f - 1.0f, tx[1] * 2.0f - 1.0f, tx[2] * 2.0f - 1.0f));
+        mN.x *= 1.0f; mN.y *= 1.0f;
+        nn = normalize(S * mN.x + T * mN.y + N * mN.z);
+    }
+    h.normal = normalize(mul3t(a.model, nn));
+    h.type = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
+    h.color = mk(1.0f, 1.0f, 1.0f);
+    h.id = 8;
+}
+
 // SceneIntersect: js/BabylonPathTracing_FragmentShader.js:47-112 (Cornell),
 // js/TransformedQuadricGeometry_FragmentShader.js:77-317 (quadrics) and
 // js/GLTFModelPathTracing_FragmentShader.js:116-346 (glTF, with the BVH walk)
@@ -77,33 +107,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
     else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, h.t, st, br);
     if (COUNT) { cnt.node += br.nodes; cnt.leaf += br.leaves; cnt.ovf += br.ovf; }
-    const bool lookup = br.lookup;
-    const float triID = br.triID, triU = br.triU, triV = br.triV;
-    if (lookup) {
-        float4 v2 = fetch32(a.tri, a.tri_texels, triID + 2.0f), v3 = fetch32(a.tri, a.tri_texels, triID + 3.0f),
-               v4 = fetch32(a.tri, a.tri_texels, triID + 4.0f), v5 = fetch32(a.tri, a.tri_texels, triID + 5.0f);
-        if (COUNT) cnt.hit++;
-        float triW = 1.0f - triU - triV;
-        f3 nn = normalize(mk(v2.y, v2.z, v2.w) * triW + mk(v3.x, v3.y, v3.z) * triU + mk(v3.w, v4.x, v4.y) * triV);
-        h.u = triW * v4.z + triU * v5.x + triV * v5.z;
-        h.v = triW * v4.w + triU * v5.y + triV * v5.w;
-        if (kHasTex<PROG> && a.uses_bump) {   // perturbNormal(n, vec2(1), uv), js/GLTFModelPathTracing_FragmentShader.js:72-92
-            f3 S = onb_u(nn);
-            f3 T = cross(nn, S);
-            f3 N = normalize(nn);
-            if (dot(cross(S, T), N) < 0.0f) { S = S * -1.0f; T = T * -1.0f; }
-            float tx[4];
-            texBilinear(a.bump, h.u, h.v, tx);
-            if (COUNT) cnt.tap += 4;
-            f3 mN = normalize(mk(tx[0] * 2.0f - 1.0f, tx[1] * 2.0f - 1.0f, tx[2] * 2.0f - 1.0f));
-            mN.x *= 1.0f; mN.y *= 1.0f;
-            nn = normalize(S * mN.x + T * mN.y + N * mN.z);
-        }
-        h.normal = normalize(mul3t(a.model, nn));
-        h.type = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
-        h.color = mk(1.0f, 1.0f, 1.0f);
-        h.id = 8;
-    }
+    if (br.lookup) meshHit<PROG, COUNT>(a, br.triID, br.triU, br.triV, h, cnt);
 }
 
 // One iteration of CalculateRadiance's loop: SceneIntersect, then the shading step

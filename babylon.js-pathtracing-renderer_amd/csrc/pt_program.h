@@ -143,13 +143,13 @@ PT_D void objectMaterial(const TraceArgs& a, int id, f3& color, int& type)
 // its object from the kernarg segment through the scalar cache, which keeps ~130 wave-uniform
 // floats out of VGPRs and the code small enough for the instruction cache.
 template <int PROG>
-PT_D void analyticIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h)
+PT_D void analyticNearest(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, f3& sn)
 {
     constexpr int q0 = kQuadId0<PROG>;
     h.t = kINF;
     h.type = -100;
     h.id = -1;
-    f3 sn = mk(0, 0, 0);
+    sn = mk(0, 0, 0);
     if (kIsQuadric<PROG>) {
 #pragma unroll 1
         for (int s = 0; s < 12; s++) {
@@ -171,6 +171,12 @@ PT_D void analyticIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h)
         float d = gmin(quadTriangle(a.qtri[2 * i], rayO, rayD), quadTriangle(a.qtri[2 * i + 1], rayO, rayD));
         if (d < h.t) { h.t = d; h.id = q0 + i; }
     }
+}
+// the winner's attributes; `sn` = its object-space normal (spheres / quadric shapes)
+template <int PROG>
+PT_D void analyticAttributes(const TraceArgs& a, Hit& h, f3 sn)
+{
+    constexpr int q0 = kQuadId0<PROG>;
     if (h.id >= 0 && h.id < q0) {
         const m4& M = kIsQuadric<PROG> ? a.shape_inv[h.id] : a.sph[h.id].inv;
         // disk and rectangle: hitNormal = vec3(0,-1,0), not normalized before the transform
@@ -181,7 +187,13 @@ PT_D void analyticIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h)
     }
     if (h.id >= 0) objectMaterial<PROG>(a, h.id, h.color, h.type);
 }
-
+template <int PROG>
+PT_D void analyticIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h)
+{
+    f3 sn;
+    analyticNearest<PROG>(a, rayO, rayD, h, sn);
+    analyticAttributes<PROG>(a, h, sn);
+}
 // Get_HDR_Color (js/HDRIEnvironmentPathTracing_FragmentShader.js:236-245): equirect lookup
 template <bool COUNT>
 PT_D f3 envColor(const TraceArgs& a, f3 rd, Cnt& cnt)

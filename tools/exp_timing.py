@@ -32,7 +32,8 @@ import itertools  # noqa: E402
 for backend, layout in itertools.product(a.backends.split(","), a.layouts.split(",")):
     e.set_backend(backend)
     e.set_bvh_layout(layout)
-    for variant in ("mesh", "no_mesh"):
+    call_pt = [c for c in p.meta["frames"][-1] if c["effect"] == "pathTracingEffectWrapper"][0]
+    for variant in ("mesh", "no_mesh") if "uGLTF_Model_InvMatrix" in call_pt["uniforms"] else ("mesh",):
         over = None
         if variant == "no_mesh":
             call0 = [c for c in p.meta["frames"][-1] if c["effect"] == "pathTracingEffectWrapper"][0]

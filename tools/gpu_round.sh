@@ -12,4 +12,6 @@ timeout -k 10 300 python bench.py --steps 50 --warmup 5 --cpu-budget 10 > gpurun
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 2 --cpu-budget 0 > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1 || exit $?
 echo "prof rc=0" >> "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log"
-cd "$GRAFT_REPO_ROOT" && bash tools/gpu_pmc.sh $TAG
+cd "$GRAFT_REPO_ROOT" && bash tools/gpu_pmc.sh $TAG || exit $?
+timeout -k 10 300 python bench.py --workload dragon --steps 20 --warmup 3 --cpu-budget 10 > gpurun_out/bench_${TAG}_dragon.json 2> gpurun_out/bench_${TAG}_dragon.err || exit $?
+bash tools/gpu_pmc.sh ${TAG}_dragon --dragon

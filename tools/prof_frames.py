@@ -17,10 +17,11 @@ ap.add_argument("--stream", default="gltf_bunny_1080p")
 ap.add_argument("--frames", type=int, default=10)
 ap.add_argument("--width", type=int, default=0)
 ap.add_argument("--height", type=int, default=0)
+ap.add_argument("--dragon", action="store_true", help="the StanfordDragon stand-in mesh instead of the stream's")
 a = ap.parse_args()
 meta = H.stream(a.stream)
 e = bp.Engine(0)
-mesh = H.texture_payloads(meta, H.mesh(meta)) if meta["scene"] in ("gltf", "hdri") else None
+mesh = H.texture_payloads(meta, H.synthetic_dragon() if a.dragon else H.mesh(meta)) if meta["scene"] in ("gltf", "hdri") else None
 p = bp.StreamPlayer(e, meta, H.bluenoise(), mesh, a.width or None, a.height or None)
 for k in range(a.frames):
     for call in p.synth_frame(k):
