@@ -103,7 +103,7 @@ struct TraceArgs {
     const float4* bvh_leaves;  // ... and its leaf records
     float bvh_root_code;       // code of node 0
     float2* spill;             // megakernel BVH stack levels >= kStackLds: [level][grid lane]
-    unsigned long long spill_stride;
+    unsigned spill_stride;
     Tex8 albedo, bump, metal, emissive;
     // diagnostics
     unsigned long long* counters;   // C_NUM entries, only with counting builds

@@ -523,11 +523,15 @@ int render_trace(pt_effect* fx, pt_texture* target)
         if (rc) return rc;
         const unsigned waves = (n_wave_tiles + c->persist_tiles - 1) / c->persist_tiles;
         const size_t lanes = (size_t)((waves + 3) / 4) * pt::kBlock;
+        if (lanes * (pt::kStackLevels - pt::kStackLds) > 0xffffffffull)   // 32-bit slab index
+            return fail(c, PT_ERR_ARG, "render target too large for the BVH stack slab");
         if (mesh && (rc = spill_reserve(c, lanes))) return rc;
         a.spill = c->mk_spill;
         a.spill_stride = lanes;
     } else if (c->backend == PT_BACKEND_MEGAKERNEL && mesh) {
         const size_t lanes = (size_t)gx * gy * pt::kBlock;
+        if (lanes * (pt::kStackLevels - pt::kStackLds) > 0xffffffffull)   // 32-bit slab index
+            return fail(c, PT_ERR_ARG, "render target too large for the BVH stack slab");
         int rc = spill_reserve(c, lanes);
         if (rc) return rc;
         a.spill = c->mk_spill;

@@ -38,20 +38,21 @@ typedef __attribute__((address_space(1))) vf2 glb_float2;
 struct MegaStack {
     lds_float2* lds;
     unsigned slot;
-    glb_float2* deep;     // this lane's level kStackLds in the spill slab, levels `stride` apart
-    unsigned long long stride;
+    glb_float2* slab;     // the spill slab (wave-uniform base) ...
+    unsigned deep;        // ... and this lane's index in it: level kStackLds, levels `stride` apart
+    unsigned stride;      //     (32-bit: a 64-bit per-lane pointer costs two VGPRs for the whole path)
     PT_D float2 get(int si) const
     {
         vf2 e;
         if (si < kStackLds) e = lds[si * kBlock + slot];
-        else e = deep[(si - kStackLds) * stride];
+        else e = slab[(unsigned)(si - kStackLds) * stride + deep];
         return make_float2(e.x, e.y);
     }
     PT_D void put(int si, float2 e)
     {
         const vf2 v = { e.x, e.y };
         if (si < kStackLds) lds[si * kBlock + slot] = v;
-        else deep[(si - kStackLds) * stride] = v;
+        else slab[(unsigned)(si - kStackLds) * stride + deep] = v;
     }
 };
 
@@ -90,7 +91,7 @@ PT_D void meshHit(const TraceArgs& a, float triID, float triU, float triV, Hit& 
 // js/GLTFModelPathTracing_FragmentShader.js:116-346 (glTF, with the BVH walk)
 template <int PROG, bool COUNT>
 PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* lds, unsigned lane_slot,
-                         float2* deep, Cnt& cnt)
+                         unsigned deep, Cnt& cnt)
 {
     if (COUNT) cnt.seg++;
     analyticIntersect<PROG>(a, rayO, rayD, h);
@@ -103,7 +104,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
     float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
     BvhResult br = { 0.0f, 0.0f, 0.0f, false, 1u, 0u, 0u };
-    MegaStack st{ (lds_float2*)lds, lane_slot, (glb_float2*)deep, a.spill_stride };
+    MegaStack st{ (lds_float2*)lds, lane_slot, (glb_float2*)a.spill, deep, a.spill_stride };
     if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
     else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, h.t, st, br);
     if (COUNT) { cnt.node += br.nodes; cnt.leaf += br.leaves; cnt.ovf += br.ovf; }
@@ -113,7 +114,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
 // One iteration of CalculateRadiance's loop: SceneIntersect, then the shading step
 template <int PROG, bool COUNT, class G>
 PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, float2* lds, unsigned lane_slot,
-                     float2* deep, Cnt& cnt)
+                     unsigned deep, Cnt& cnt)
 {
     Hit h;
     sceneIntersect<PROG, COUNT>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt);
@@ -121,7 +122,7 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, fl
 }
 
 template <int PROG, bool COUNT, class G>
-PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_slot, float2* deep, Cnt& cnt)
+PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_slot, unsigned deep, Cnt& cnt)
 {
     PState s;
     pathBegin(s, g);
@@ -147,7 +148,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
     const int py = band * kTile + (wave >> 1) * 8 + ly;
     // stack levels >= kStackLds: a global slab [level][lane of the grid] (a private array would be
     // scratch, which the runtime reserves for every resident wave)
-    float2* deep = a.spill + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + tid;
+    const unsigned deep = (blockIdx.y * gridDim.x + blockIdx.x) * kBlock + tid;
 
     // lanes whose whole 2x2 quad lies beyond the (even-rounded) target do no work; quad helpers
     // that only complete a quad at an odd edge are shaded like GL helper invocations
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_persist(TraceArgs 
     const unsigned wid = blockIdx.x * (kBlock / 64) + wave;
     unsigned next = wid * per_wave * 64u;
     const unsigned end = min(next + per_wave * 64u, n_wave_tiles * 64u);
-    float2* deep = a.spill + (size_t)blockIdx.x * kBlock + tid;
+    const unsigned deep = blockIdx.x * kBlock + tid;
     Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
     unsigned paths = 0;
     Path p;
