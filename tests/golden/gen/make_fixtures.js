@@ -11,6 +11,7 @@
 //
 // usage: node make_fixtures.js <scene> <outdir> [width height frames seed model]
 //   scene: cornell | gltf | sky | hdri | quadric
+//   model: a menu name, or file:<model file>:<modelInitialScale>:<rh 0|1> (mesh payloads only)
 'use strict';
 const fs = require('fs');
 const path = require('path');
@@ -132,7 +133,15 @@ function wrapBuilder() {
     // wait for the initial (teapot) load (and the environment), then select MODEL through the GUI
     // exactly as a user would
     while (meshTextures().length < 2 || (scene === 'hdri' && hdrTextures().length < 1)) { frame(); await tick(); }
-    if (MODEL !== 'Utah Teapot') {
+    if (MODEL.startsWith('file:')) {
+      // a model file outside the menu (file:<name>:<modelInitialScale>:<rh 0|1>): set what the
+      // menu handler sets and call the script's own loadModel()
+      const [, file, scale, rh] = MODEL.split(':');
+      const before = meshTextures().length;
+      vm.runInThisContext(`modelNameAndExtension = ${JSON.stringify(file)}; modelWasDefinedInRHCoordSystem = ${rh === '1'};` +
+                          ` modelInitialScale = ${Number(scale)}; loadModel();`);
+      while (meshTextures().length < before + 2) { frame(); await tick(); }
+    } else if (MODEL !== 'Utah Teapot') {
       const before = meshTextures().length;
       vm.runInThisContext('gltfModel_SelectionController').setValue(MODEL);
       while (meshTextures().length < before + 2) { frame(); await tick(); }

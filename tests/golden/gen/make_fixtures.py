@@ -15,7 +15,7 @@ outputs as small fixtures:
   browser_env.js syntheticHDR (== tests/helpers.py synthetic_hdr; the reference's .hdr files are
   not in it); the stream records that texture's sha256, the payload itself is regenerated.
 
-usage: python tests/golden/gen/make_fixtures.py [stream names ...]   (default: all)
+usage: python tests/golden/gen/make_fixtures.py [stream names | mesh_<model fixture> ...]   (default: all)
 """
 import sys
 import hashlib
@@ -43,6 +43,13 @@ STREAMS = [
     ("hdri_teapot_320x180", "hdri", 320, 180, 3, 11, "Utah Teapot"),
     ("hdri_helmet_320x180", "hdri", 320, 180, 3, 13, "Damaged Helmet"),
     ("quadric_256", "quadric", 256, 256, 3, 17, None),
+]
+# models of the reference's models/ outside the setup script's menu, loaded through the script's
+# own loadModel(): only their mesh payloads are kept (they pin the asset-pipeline restatement,
+# python/pt_assets.py, on multi-mesh merges and mixed vertex-attribute sets)
+MODEL_FIXTURES = [
+    ("bookcase", "file:testBookCase.gltf:8:0"),
+    ("twoparts", "file:twoParts-opaque.gltf:25:0"),
 ]
 
 
@@ -146,6 +153,11 @@ def main():
             with open(os.path.join(GOLD, name + ".json"), "w") as f:
                 json.dump(meta, f, indent=0)
             manifest[name] = {"scene": scene, "width": w, "height": h, "frames": frames, "seed": seed, "model": model}
+        for key, model in MODEL_FIXTURES:
+            if only and "mesh_" + key not in only:
+                continue
+            meta, mesh = run_stream("model_" + key, "gltf", 64, 64, 1, 1, model, tmp)
+            meshes[key] = mesh
         for key, (bvh, tri, aabb_in) in meshes.items():
             # aabb_in: BVH_Build_Iterative's input (js/BVH_Fast_Builder.js:320), work list = 0..N-1
             np.savez_compressed(os.path.join(GOLD, "mesh_%s.npz" % key), bvh=bvh, tri=tri, aabb_in=aabb_in)
@@ -154,6 +166,9 @@ def main():
                 "sha256_bvh": hashlib.sha256(bvh.tobytes()).hexdigest(),
                 "sha256_tri": hashlib.sha256(tri.tobytes()).hexdigest(),
             }
+            src = dict(MODEL_FIXTURES).get(key)
+            if src:
+                manifest["mesh_" + key]["model"] = src
     v16 = png_rgba16(os.path.join(REF, "textures/BlueNoise_RGBA256.png"))
     np.save(os.path.join(GOLD, "bluenoise_rgba8.npy"), (v16 >> 8).astype(np.uint8))
     manifest["bluenoise"] = {"sha256_rgba16": hashlib.sha256(v16.astype("<u2").tobytes()).hexdigest(),
