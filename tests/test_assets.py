@@ -144,3 +144,28 @@ def test_texture_arrays_layout():
     ref = H.texture_payloads({"scene": "gltf"}, {"bvh": gold["bvh"], "tri": gold["tri"]})
     for k in ("bvh", "tri"):
         assert t[k].shape == (4 * 2048 * 2048,) and np.array_equal(_bits(t[k]), _bits(ref[k]))
+
+
+# ------------------------------------------------------------------------------ HDR environment
+@pytest.mark.parametrize("w,h", [(64, 16), (5, 3)])   # RLE scanlines, flat scanlines (w < 8)
+def test_decode_hdr_matches_rgbe(tmp_path, w, h):
+    rng = np.random.default_rng(w)
+    img = rng.exponential(2.0, (h, w, 3)) * (rng.random((h, w, 1)) < 0.8)
+    img[0, :4] = 7.0   # runs
+    rgbe = H.rgbe_encode(img)
+    p = tmp_path / "e.hdr"
+    if w >= 8:
+        H.write_radiance_hdr(str(p), rgbe)
+    else:
+        p.write_bytes(b"#?RADIANCE\nFORMAT=32-bit_rle_rgbe\n\n" + ("-Y %d +X %d\n" % (h, w)).encode() + rgbe.tobytes())
+    got = A.decode_hdr(p.read_bytes())
+    assert np.array_equal(_bits(got), _bits(H.rgbe_decode(rgbe)))
+
+
+def test_hdr_sun_direction_matches_the_script():
+    """The HDRI setup script derived uSunDirection from synthetic_hdr() when the fixture streams
+    were recorded; the uniform (float32) must be reproduced exactly."""
+    d = A.hdr_sun_direction(H.synthetic_hdr())
+    for name in ("hdri_teapot_320x180", "hdri_helmet_320x180"):
+        u = H.path_call(H.stream(name)["frames"][0])["uniforms"]["uSunDirection"][1]
+        assert np.array_equal(np.float32(u), np.float32(d)), (u, d)
