@@ -12,9 +12,18 @@ constexpr int kBlock = 256;          // 4 waves; a block shades a 16x16 pixel ti
 constexpr int kTile = 16;            // tile edge == row-band height used for sharding
 constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing_FragmentShader.js:95
 #ifndef PT_STACK_LDS
-#define PT_STACK_LDS 8
+#define PT_STACK_LDS 7
 #endif
 constexpr int kStackLds = PT_STACK_LDS;        // levels kept in LDS per lane; deeper levels go to a global slab
+
+// child-pair record codes: a node's rank code from the build's rank pass (rank >= 0 of an inner
+// node, -1 - rank of a leaf) -> the 32-bit code the walk carries: the inner record's byte offset,
+// or kLeafBit | the leaf record's byte offset
+constexpr uint32_t kLeafBit = 0x80000000u;
+__host__ __device__ inline uint32_t pairCode(float rankCode)
+{
+    return rankCode >= 0.0f ? (uint32_t)rankCode * 64u : kLeafBit | ((uint32_t)(-1.0f - rankCode) * 48u);
+}
 
 enum Counter { C_PATHS, C_SEGMENTS, C_NODE, C_LEAF, C_HIT, C_RGBA8, C_OVERFLOW, C_HDR, C_NUM };
 enum ErrBits { E_STACK = 1u };
@@ -101,7 +110,8 @@ struct TraceArgs {
     long long tri_texels;
     const float4* bvh_pairs;   // child-pair inner records of tAABBTexture (PROG_PAIRS variants only)
     const float4* bvh_leaves;  // ... and its leaf records
-    float bvh_root_code;       // code of node 0
+    uint32_t bvh_root_code;    // pairCode of node 0
+    uint32_t bvh_pairs_bytes, bvh_leaves_bytes;   // sizes of the two record arrays (buffer descriptors)
     float2* spill;             // megakernel BVH stack levels >= kStackLds: [level][grid lane]
     unsigned spill_stride;
     Tex8 albedo, bump, metal, emissive;

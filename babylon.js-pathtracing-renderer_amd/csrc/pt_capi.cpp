@@ -25,6 +25,7 @@
 #include "pt_args.h"
 
 extern "C" {
+hipError_t pt_launch_exhaustive(int op, unsigned long long* bad, hipStream_t s);
 hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
@@ -69,7 +70,8 @@ struct pt_texture {
     void* pairs_mem = nullptr;
     const float4* pairs_inner = nullptr;
     const float4* pairs_leaf = nullptr;
-    float pairs_root = 0.0f;
+    uint32_t pairs_root = 0;
+    uint32_t pairs_inner_bytes = 0, pairs_leaf_bytes = 0;
     const pt_texture* pairs_tri = nullptr;
     unsigned long long pairs_gen = ~0ull, pairs_tri_gen = ~0ull;
     bool pairs_ok = false;
@@ -441,8 +443,12 @@ bool ensure_pairs(pt_ctx* c, pt_texture* t, const pt_texture* tri, int* rc)
         }
         if (e == hipSuccess) e = pass(3, nullptr, nullptr);
         if (e == hipSuccess) e = pass(4, (float4*)t->pairs_inner, (float4*)t->pairs_leaf);
-        if (e == hipSuccess) e = hipMemcpyAsync(&t->pairs_root, code, sizeof(float), hipMemcpyDeviceToHost, c->stream);
+        float root = 0.0f;
+        if (e == hipSuccess) e = hipMemcpyAsync(&root, code, sizeof(float), hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        t->pairs_root = pt::pairCode(root);
+        t->pairs_inner_bytes = (uint32_t)(n_inner * 64);
+        t->pairs_leaf_bytes = (uint32_t)(n_leaf * 48);
     }
     if (scratch) { hipStreamSynchronize(c->stream); hipFree(scratch); }
     if (e != hipSuccess) { *rc = hipfail(c, e, "BVH child-pair build"); return false; }
@@ -499,6 +505,8 @@ int render_trace(pt_effect* fx, pt_texture* target)
             a.bvh_pairs = bvh->pairs_inner;
             a.bvh_leaves = bvh->pairs_leaf;
             a.bvh_root_code = bvh->pairs_root;
+            a.bvh_pairs_bytes = bvh->pairs_inner_bytes;
+            a.bvh_leaves_bytes = bvh->pairs_leaf_bytes;
         }
         if (prc) return prc;
         c->bvh_used = a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
@@ -1020,6 +1028,22 @@ int pt_queue_stats(pt_ctx* c, uint32_t out[16])
             out[b] += h[b * pt::kShards + s];
             if (b < 6) out[8 + b] += h[(8 + b) * pt::kShards + s];
         }
+    return PT_OK;
+}
+
+int pt_math_exhaustive(pt_ctx* c, int op, uint64_t* mismatches)
+{
+    if (!c || !mismatches || op != 0) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    unsigned long long* d = nullptr;
+    HIPCHK(c, hipMalloc(&d, sizeof(unsigned long long)));
+    HIPCHK(c, hipMemsetAsync(d, 0, sizeof(unsigned long long), c->stream));
+    HIPCHK(c, pt_launch_exhaustive(op, d, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    unsigned long long h = 0;
+    HIPCHK(c, hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost));
+    hipFree(d);
+    *mismatches = h;
     return PT_OK;
 }
 

@@ -46,11 +46,11 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, bool pair
 }
 // waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 80 -> 6; the
 // textured variant keeps 2 rather than spill)
-// (measured with 8 LDS stack levels: the child-pair walk gains 2 % on the bunny and 7 % on the
-// dragon stand-in at 6 waves over 5, although the shading code then spills 64 B; 7-8 waves and
-// more LDS levels lose; the reference walk loses above 4)
+// (measured: 7 waves with 7 LDS stack levels - LDS allows 7 blocks of 22.5 KB per CU - beat 6
+// waves with 8 levels by 4 % on the dragon stand-in and tie on the bunny, though the shading code
+// spills more; 5 waves and 8 waves with 6 levels lose; the reference walk loses above 4)
 #ifndef PT_MINWAVES_PAIRS
-#define PT_MINWAVES_PAIRS 6
+#define PT_MINWAVES_PAIRS 7
 #endif
 template <int P> constexpr int kMinWaves = kHasTex<P> ? 2 : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
 
@@ -98,7 +98,7 @@ PT_D f3 specularLobeDir(Path& p, f3 rdir, float roughness)
 {
     roughness = gclamp(roughness, 0.0f, 1.0f);
     float exponent = gmix(7.0f, 0.0f, sqrtf(roughness));
-    float cosTheta = gpow(rng(p), 1.0f / (gexp(exponent) + 1.0f));
+    float cosTheta = gpow(rng(p), grcp(gexp(exponent) + 1.0f));
     float sinTheta = sqrtf(gmax(0.0f, 1.0f - cosTheta * cosTheta));
     float phi = rng(p) * kTwoPi;
     float sn, cs;
@@ -145,7 +145,7 @@ PT_D float unitSphere(f3 ro, f3 rd, f3& n)
     float a = dot(rd, rd);
     float b = 2.0f * dot(rd, ro);
     float c = dot(ro, ro) - 1.0f;
-    float invA = 1.0f / a;          // solveQuadratic, js/PathTracingCommon.js:631-641
+    float invA = grcp(a);          // solveQuadratic, js/PathTracingCommon.js:631-641
     b *= invA;
     c *= invA;
     float nh = -b * 0.5f;
@@ -167,7 +167,7 @@ PT_D float quadTriangle(const TriArg& T, f3 ro, f3 rd)
     f3 pv = cross(rd, T.e2);
     const float dd = dot(T.e1, pv);
     if (recipNegative(dd)) return kINF;   // det < 0: back face, decided before the division
-    float det = 1.0f / dd;
+    float det = grcp(dd);
     f3 tv = ro - T.v0;
     float u = dot(tv, pv) * det;
     if (u < 0.0f || u > 1.0f) return kINF;   // the miss is an OR: its first terms decide early
@@ -187,21 +187,29 @@ PT_D float box(f3 mn, f3 mx, f3 ro, f3 inv)
 // box() for a ray whose model-space origin and inverse direction are finite and nonzero and a box
 // without NaN: then no slab product is NaN, and IEEE min/max (v_min3 / v_max3) pick the same values
 // as the GLSL's y<x?y:x forms up to the sign of a zero, which only ever feeds comparisons
+// (the min/max are issued as v_min/v_max/v_min3/v_max3 directly: through fminf/fmaxf the compiler
+// adds a quieting v_max x,x per operand it cannot prove canonical, 6 per box)
+PT_D float vmin(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+PT_D float vmax(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+PT_D float vmax0(float a) { float r; asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(a)); return r; }
+PT_D float vmin3(float a, float b, float c) { float r; asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c)); return r; }
+PT_D float vmax3(float a, float b, float c) { float r; asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c)); return r; }
 PT_D float boxFast(f3 mn, f3 mx, f3 ro, f3 inv)
 {
     f3 nr = (mn - ro) * inv;
     f3 fr = (mx - ro) * inv;
-    float t0 = fmaxf(fmaxf(fminf(nr.x, fr.x), fminf(nr.y, fr.y)), fminf(nr.z, fr.z));
-    float t1 = fminf(fminf(fmaxf(nr.x, fr.x), fmaxf(nr.y, fr.y)), fmaxf(nr.z, fr.z));
-    return fmaxf(t0, 0.0f) > t1 ? kINF : t0;
+    float t0 = vmax3(vmin(nr.x, fr.x), vmin(nr.y, fr.y), vmin(nr.z, fr.z));
+    float t1 = vmin3(vmax(nr.x, fr.x), vmax(nr.y, fr.y), vmax(nr.z, fr.z));
+    return vmax0(t0) > t1 ? kINF : t0;
 }
 PT_D bool finite3(f3 v) { return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z); }
 
-PT_D float bvhTriangle(f3 v0, f3 v1, f3 v2, f3 ro, f3 rd, float& u, float& v, bool dbl)
+// BVH_TriangleIntersect / BVH_DoubleSidedTriangleIntersect (js/PathTracingCommon.js:1214-1245)
+// from v0 and the edges e1 = v1 - v0, e2 = v2 - v0
+PT_D float bvhTriangleE(f3 v0, f3 e1, f3 e2, f3 ro, f3 rd, float& u, float& v, bool dbl)
 {
-    f3 e1 = v1 - v0, e2 = v2 - v0;
     f3 pv = cross(rd, e2);
-    float det = 1.0f / dot(e1, pv);
+    float det = grcp(dot(e1, pv));
     f3 tv = ro - v0;
     u = dot(tv, pv) * det;
     f3 qv = cross(tv, e1);
@@ -210,6 +218,10 @@ PT_D float bvhTriangle(f3 v0, f3 v1, f3 v2, f3 ro, f3 rd, float& u, float& v, bo
     bool miss = u < 0.0f || u > 1.0f || v < 0.0f || u + v > 1.0f || t <= 0.0f;
     if (!dbl) miss = miss || det < 0.0f;
     return miss ? kINF : t;
+}
+PT_D float bvhTriangle(f3 v0, f3 v1, f3 v2, f3 ro, f3 rd, float& u, float& v, bool dbl)
+{
+    return bvhTriangleE(v0, v1 - v0, v2 - v0, ro, rd, u, v, dbl);
 }
 
 // texelFetch on a RGBA32F data texture by linear texel index (== ivec2(mod(i,2048), i/2048) for
@@ -345,11 +357,14 @@ PT_D void bvhWalkRef(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float4 c0
 }
 
 // Child-pair records (pt_pairs_* in pt_kernels.hip; only for trees whose links are exact in-range
-// integers, see pt_capi.cpp ensure_pairs). Nodes are addressed by a code: rank >= 0 of an inner
-// node in the dense inner-record array, or -1 - rank of a leaf in the dense leaf-record array.
+// integers, see pt_capi.cpp ensure_pairs). Nodes are addressed by a 32-bit code (pairCode,
+// pt_args.h): the byte offset of an inner node's record in the dense inner-record array, or
+// kLeafBit | the byte offset of a leaf's record in the dense leaf-record array, kept as float bits
+// in records and stack entries. Both arrays are read through buffer descriptors, so an inner code
+// is the load's voffset as it stands (no float->int conversion or 64-bit address arithmetic).
 //   inner record (64 B, one line): A.min.xyz A.max.x | A.max.yz B.min.xy | B.min.z B.max.xyz | codeA codeB
 //     (A = the node's left child n+1, B = its right-child link)
-//   leaf record (48 B): the leaf triangle's vertex texels (9 floats), its idObject
+//   leaf record (48 B): the leaf triangle's v0, e1 = v1 - v0, e2 = v2 - v0 (9 floats), its idObject
 // An inner step is one 64-byte line instead of two 32-byte nodes in different lines, a pop needs
 // no fetch (the stack entry (tNear, code) already says what the node is), and a leaf's vertices
 // sit in a dense 48-byte record instead of the first third of a 128-byte triangle texel group:
@@ -359,12 +374,41 @@ PT_D void bvhWalkRef(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float4 c0
 // for boxFast (records are NaN-free, checked at build). A schedule that interleaved walk steps
 // with other lanes' shading on top of it measured slower.
 struct PairWalk {
-    float code, hitT;        // node to process, closest hit so far
+    uint32_t code;           // node to process
+    float hitT;              // closest hit so far
     float triID, triU, triV; // the hit triangle (lookup), its barycentrics
     int sp;                  // stack pointer
     bool pop, lookup;
 };
-PT_D void pairWalkBegin(PairWalk& w, float rootCode, float rootT, float hitT)
+// the record arrays as buffer descriptors, built from kernel arguments and made provably
+// wave-uniform (readfirstlane) so that no waterfall loop wraps the loads
+struct PairBufs {
+    __amdgpu_buffer_rsrc_t inner, leaf;
+};
+PT_D __amdgpu_buffer_rsrc_t uniformRsrc(const void* p, uint32_t bytes)
+{
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                             (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+PT_D PairBufs pairBufs(const TraceArgs& a)
+{
+    return PairBufs{ uniformRsrc(a.bvh_pairs, a.bvh_pairs_bytes), uniformRsrc(a.bvh_leaves, a.bvh_leaves_bytes) };
+}
+typedef unsigned int vu4 __attribute__((ext_vector_type(4)));
+typedef unsigned int vu2 __attribute__((ext_vector_type(2)));
+PT_D float4 ldRec4(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    const vu4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+PT_D float2 ldRec2(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    const vu2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
+    return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+}
+PT_D void pairWalkBegin(PairWalk& w, uint32_t rootCode, float rootT, float hitT)
 {
     w.code = rootCode; w.hitT = hitT; w.sp = 0;
     w.pop = !(rootT < hitT);
@@ -377,21 +421,21 @@ PT_D bool pairWalkFast(f3 O, f3 inv)
 }
 // one step; false once the stack has run empty (the walk is over)
 template <class Stk>
-PT_D bool pairWalkStep(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, bool fast, Stk& st, PairWalk& w,
-                       BvhResult& r)
+PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv, bool dbl, bool fast, Stk& st,
+                       PairWalk& w, BvhResult& r)
 {
     if (w.pop) {
         w.sp--;
         if (w.sp < 0) return false;
         const float2 e = stackPop(st, w.sp, make_float2(kINF, 0.0f));
         if (e.x >= w.hitT) return true;
-        w.code = e.y;
+        w.code = __float_as_uint(e.y);
         r.nodes++;
     }
     w.pop = true;
-    if (w.code >= 0.0f) {
-        const float4* rec = a.bvh_pairs + 4u * (unsigned)w.code;
-        const float4 r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+    if (!(w.code & kLeafBit)) {
+        const float4 r0 = ldRec4(b.inner, w.code), r1 = ldRec4(b.inner, w.code + 16u), r2 = ldRec4(b.inner, w.code + 32u);
+        const float2 r3 = ldRec2(b.inner, w.code + 48u);
         r.nodes += 2;
         float tA, tB;
         if (fast) {
@@ -401,23 +445,24 @@ PT_D bool pairWalkStep(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, bool fa
             tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
             tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
         }
-        float cA = r3.x, cB = r3.y;
+        float cA = r3.x, cB = r3.y;   // codes as float bits: only moved, never computed on
         if (tB < tA) {
             float tt = tB; tB = tA; tA = tt;
             float tc = cB; cB = cA; cA = tc;
         }
-        if (tB < w.hitT) { w.code = cB; w.pop = false; }
+        if (tB < w.hitT) { w.code = __float_as_uint(cB); w.pop = false; }
         if (tA < w.hitT) {
             if (!w.pop) { stackPush(a, st, w.sp, make_float2(tB, cB), r.ovf); w.sp++; }
-            w.code = cA; w.pop = false;
+            w.code = __float_as_uint(cA); w.pop = false;
         }
         return true;
     }
-    const float4* lf = a.bvh_leaves + 3u * (unsigned)(-1.0f - w.code);
-    const float4 t0 = lf[0], t1 = lf[1], t2 = lf[2];
+    const uint32_t lo = w.code & ~kLeafBit;
+    const float4 t0 = ldRec4(b.leaf, lo), t1 = ldRec4(b.leaf, lo + 16u);
+    const float2 t2 = ldRec2(b.leaf, lo + 32u);
     r.leaves++;
     float tu, tv;
-    const float d = bvhTriangle(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
+    const float d = bvhTriangleE(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
     if (d < w.hitT) { w.hitT = d; w.triID = 8.0f * t2.y; w.triU = tu; w.triV = tv; w.lookup = true; }
     return true;
 }
@@ -428,7 +473,8 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     PairWalk w;
     pairWalkBegin(w, a.bvh_root_code, curT, hitT);
     const bool fast = pairWalkFast(O, inv);
-    while (pairWalkStep(a, O, D, inv, dbl, fast, st, w, r)) {}
+    const PairBufs b = pairBufs(a);
+    while (pairWalkStep(a, b, O, D, inv, dbl, fast, st, w, r)) {}
     hitT = w.hitT;
     if (w.lookup) { r.triID = w.triID; r.triU = w.triU; r.triV = w.triV; r.lookup = true; }
 }

@@ -99,7 +99,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
 
     // ---- BVH walk (js/GLTFModelPathTracing_FragmentShader.js:201-298), pt_device.h
     f3 O = mul(a.model, rayO, 1.0f), D = mul(a.model, rayD, 0.0f);
-    f3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+    f3 inv = mk(grcp(D.x), grcp(D.y), grcp(D.z));
     const bool dbl = (!a.uses_albedo && a.model_mat == TRANSPARENT);
     float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
     float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
@@ -387,9 +387,9 @@ __global__ __launch_bounds__(256) void pt_output(OutputArgs a)
 //           root); `bad` flags links the records cannot express (right child not an exact integer
 //           in [0, nrec), left child n+1 beyond the texture) -> the host keeps the reference walk
 //   pass 2  per 1024-node block counts; the host scans them
-//   pass 3  dense ranks -> codes: inner rank, or -1 - leaf rank
+//   pass 3  dense ranks -> rank codes: inner rank, or -1 - leaf rank
 //   pass 4  inner records (64 B): A.min.xyz A.max.x | A.max.yz B.min.xy | B.min.z B.max.xyz |
-//           codeA codeB; leaf records (48 B): the three vertex texels' first 9 floats, idObject
+//           codeA codeB (pairCode: record byte offsets, float bits); leaf records (48 B): v0, e1 = v1 - v0, e2 = v2 - v0, idObject
 constexpr int kPairsBlock = 1024;   // nodes per scan block (256 threads x 4)
 
 __global__ __launch_bounds__(256) void pt_pairs_kinds(const float4* aabb, long long texels, unsigned nrec,
@@ -481,20 +481,35 @@ __global__ __launch_bounds__(256) void pt_pairs_build(const float4* aabb, long l
         o[0] = make_float4(a0.y, a0.z, a0.w, a1.y);
         o[1] = make_float4(a1.z, a1.w, b0.y, b0.z);
         o[2] = make_float4(b0.w, b1.y, b1.z, b1.w);
-        o[3] = make_float4(code[n + 1u], code[(unsigned)idB], 0.0f, 0.0f);
+        o[3] = make_float4(__uint_as_float(pairCode(code[n + 1u])), __uint_as_float(pairCode(code[(unsigned)idB])), 0.0f, 0.0f);
     } else if (leafref[n]) {
         const float hdr = fetch32(aabb, texels, fn * 2.0f).x;
         const float id = 8.0f * hdr;
         const float4 t0 = fetch32(tri, tri_texels, id), t1 = fetch32(tri, tri_texels, id + 1.0f),
                      t2 = fetch32(tri, tri_texels, id + 2.0f);
+        // edges e1 = v1 - v0, e2 = v2 - v0 are the walk's first two IEEE subtractions, done here once
+        const f3 v0 = mk(t0.x, t0.y, t0.z), e1 = mk(t0.w, t1.x, t1.y) - v0, e2 = mk(t1.z, t1.w, t2.x) - v0;
         float4* o = leaf_rec + 3ull * (unsigned)(-1.0f - code[n]);
-        o[0] = t0;
-        o[1] = t1;
-        o[2] = make_float4(t2.x, hdr, 0.0f, 0.0f);
+        o[0] = make_float4(v0.x, v0.y, v0.z, e1.x);
+        o[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+        o[2] = make_float4(e2.z, hdr, 0.0f, 0.0f);
     }
 }
 
 // ------------------------------------------------------------------------------ self-test
+// every binary32 pattern with bits 31..24 == hi: fast device sequence vs the IEEE operation it
+// stands for (NaN == NaN); one atomic per wave with a mismatch
+__global__ __launch_bounds__(256) void pt_exhaustive_kernel(int op, uint32_t hi, unsigned long long* bad)
+{
+    const uint32_t bits = (hi << 24) | (blockIdx.x * 256u + threadIdx.x);
+    const float x = __uint_as_float(bits);
+    float got = 0.0f, ref = 0.0f;
+    if (op == 0) { got = grcp(x); ref = 1.0f / x; }
+    const bool ok = (ref != ref) ? (got != got) : (__float_as_uint(got) == __float_as_uint(ref));
+    const unsigned long long m = __ballot(!ok);
+    if (m && (threadIdx.x & 63u) == (unsigned)(__ffsll((long long)m) - 1)) atomicAdd(bad, (unsigned long long)__popcll(m));
+}
+
 __global__ void pt_math_probe_kernel(int op, const float* x, const float* y, float* out, int n)
 {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -515,7 +530,8 @@ __global__ void pt_math_probe_kernel(int op, const float* x, const float* y, flo
     case 10: r = sqrtf(a); break;
     case 11: { Path p; p.s0 = (uint32_t)a; p.s1 = (uint32_t)b; r = rng(p); break; }
     case 12: r = a / b; break;
-    case 13: r = 1.0f / sqrtf(a); break;
+    case 13: r = grcp(sqrtf(a)); break;
+    case 14: r = grcp(a); break;
     default: r = 0.0f;
     }
     out[i] = r;
@@ -594,6 +610,13 @@ hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s)
 {
     dim3 grid((a->width + 15) / 16, (a->height + 15) / 16);
     hipLaunchKernelGGL(pt::pt_output, grid, dim3(256), 0, s, *a);
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_exhaustive(int op, unsigned long long* bad, hipStream_t s)
+{
+    for (uint32_t hi = 0; hi < 256u; hi++)
+        hipLaunchKernelGGL(pt::pt_exhaustive_kernel, dim3(65536), dim3(256), 0, s, op, hi, bad);
     return hipGetLastError();
 }
 

@@ -89,7 +89,7 @@ PT_D float rayleighPhase(float cosTheta) { return 0.05968310365946075f * (1.0f +
 PT_HD float hgPhase(float cosTheta, float g)
 {
     float g2 = g * g;
-    float inverse = 1.0f / gpow(gmax(0.0f, 1.0f - 2.0f * g * cosTheta + g2), 1.5f);
+    float inverse = grcp(gpow(gmax(0.0f, 1.0f - 2.0f * g * cosTheta + g2), 1.5f));
     return 0.07957747154594767f * ((1.0f - g2) * inverse);
 }
 PT_D f3 pow3(f3 v, float e) { return mk(gpow(v.x, e), gpow(v.y, e), gpow(v.z, e)); }
@@ -99,7 +99,7 @@ PT_D f3 skyColor(const SkyArgs& k, f3 rayDir)
     const float cosViewSunAngle = dot(vd, k.sun);
     const float zenithAngle = gacos(gmax(0.0f, dot(mk(0.0f, 1.0f, 0.0f), vd)));
     const float inverse =
-        1.0f / (gcos(zenithAngle) + 0.15f * gpow(93.885f - ((zenithAngle * 180.0f) / 3.14159265358979323f), -1.253f));
+        grcp(gcos(zenithAngle) + 0.15f * gpow(93.885f - ((zenithAngle * 180.0f) / 3.14159265358979323f), -1.253f));
     const float rl = 8400.0f * inverse, ml = 1250.0f * inverse;
     const f3 e = k.rayleigh * rl + k.mie * ml;
     const f3 Fex = mk(gexp(-e.x), gexp(-e.y), gexp(-e.z));

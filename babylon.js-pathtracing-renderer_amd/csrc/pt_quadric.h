@@ -18,7 +18,7 @@ struct Roots {
 // neg_halfB = 0 inside the conditional)
 PT_D Roots solveQuadratic(float A, float B, float C)
 {
-    float invA = 1.0f / A;
+    float invA = grcp(A);
     B *= invA;
     C *= invA;
     float nh = -B * 0.5f;
@@ -48,7 +48,7 @@ PT_D float unitCylinder(f3 ro, f3 rd, f3& n)
 PT_D float unitCone(f3 ro, f3 rd, float k, f3& n)
 {
     k = gclamp(k, 0.01f, 1.0f);
-    float j = 1.0f / k;
+    float j = grcp(k);
     float h = j * 2.0f - 1.0f;
     float a = j * rd.x * rd.x + j * rd.z * rd.z - (k * 0.25f) * rd.y * rd.y;
     float b = 2.0f * (j * rd.x * ro.x + j * rd.z * ro.z - (k * 0.25f) * rd.y * (ro.y - h));
@@ -165,7 +165,7 @@ PT_D float unitFlattenedRing(f3 ro, f3 rd, float k, f3& n)
 
 PT_D float unitBox(f3 ro, f3 rd, f3& n)
 {
-    const f3 inv = mk(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
+    const f3 inv = mk(grcp(rd.x), grcp(rd.y), grcp(rd.z));
     const f3 nr = (mk(-1.0f, -1.0f, -1.0f) - ro) * inv;
     const f3 fr = (mk(1.0f, 1.0f, 1.0f) - ro) * inv;
     const f3 tmin = mk(gmin(nr.x, fr.x), gmin(nr.y, fr.y), gmin(nr.z, fr.z));
@@ -200,7 +200,7 @@ PT_D float pyramidFrustum(f3 ro, f3 rd, float k, f3& n)
     float xt = kINF, zt = kINF;
     f3 xn = mk(0.0f, 0.0f, 0.0f), zn = xn;
     k = gclamp(k, 0.01f, 1.0f);
-    const float j = 1.0f / k;
+    const float j = grcp(k);
     const float h = j * 2.0f - 1.0f;
     float a = j * rd.x * rd.x - (k * 0.25f) * rd.y * rd.y;
     float b = 2.0f * (j * rd.x * ro.x - (k * 0.25f) * rd.y * (ro.y - h));

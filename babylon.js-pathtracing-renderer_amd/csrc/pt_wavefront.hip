@@ -164,7 +164,7 @@ __global__ __launch_bounds__(kBlock) void wf_extend(TraceArgs a, WfBufs w, int b
                 if (COUNT) count_add<true>(a, C_SEGMENTS, 1);
                 if (kIsGltf<PROG>) {
                     f3 O = mul(a.model, ro, 1.0f), D = mul(a.model, rd, 0.0f);
-                    f3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+                    f3 inv = mk(grcp(D.x), grcp(D.y), grcp(D.z));
                     float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
                     if (COUNT) count_add<true>(a, C_NODE, 1);
                     float tRoot = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b
         float hitT = w.hit0[i].x;
         f3 ro = mk(A.x, A.y, A.z), rd = mk(B.x, B.y, B.z);
         f3 O = mul(a.model, ro, 1.0f), D = mul(a.model, rd, 0.0f);
-        f3 inv = mk(1.0f / D.x, 1.0f / D.y, 1.0f / D.z);
+        f3 inv = mk(grcp(D.x), grcp(D.y), grcp(D.z));
         const bool dbl = (!a.uses_albedo && a.model_mat == TRANSPARENT);
         // the root was fetched and tested by wf_extend (and counted there); its box is hit
         float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);

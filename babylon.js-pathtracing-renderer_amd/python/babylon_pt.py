@@ -39,7 +39,7 @@ SYMBOLS = [
     "pt_render_target_resize", "pt_texture_size", "pt_texture_destroy",
     "pt_render", "pt_read_pixels", "pt_write_pixels",
     "pt_set_row_partition", "pt_set_backend", "pt_set_bvh_layout", "pt_bvh_layout_used", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
-    "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_bvh_build", "pt_version",
+    "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_math_exhaustive", "pt_bvh_build", "pt_version",
 ]
 
 _lib = None
@@ -80,6 +80,7 @@ def lib():
         "pt_timing_end": ([vp, i32, ctypes.POINTER(ctypes.c_double), ip], i32),
         "pt_read_counters": ([vp, ctypes.POINTER(ctypes.c_uint64)], i32), "pt_reset_counters": ([vp], i32),
         "pt_math_probe": ([vp, i32, vp, vp, vp, i32], i32),
+        "pt_math_exhaustive": ([vp, i32, vp], i32),
         "pt_queue_stats": ([vp, ctypes.POINTER(ctypes.c_uint32)], i32), "pt_version": ([], ctypes.c_char_p),
     }
     for name, (args, res) in sig.items():
@@ -192,6 +193,12 @@ class Engine:
         self.check(lib().pt_math_probe(self.ctx, op, x.ctypes.data, None if y is None else y.ctypes.data,
                                        out.ctypes.data, x.size), "pt_math_probe")
         return out
+
+    def math_exhaustive(self, op):
+        """Mismatches of device fast sequence `op` vs its IEEE operation over all 2^32 inputs."""
+        n = ctypes.c_uint64(0)
+        self.check(lib().pt_math_exhaustive(self.ctx, op, ctypes.byref(n)), "pt_math_exhaustive")
+        return n.value
 
     def dispose(self):
         if self.ctx:

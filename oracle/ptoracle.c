@@ -1417,6 +1417,9 @@ int pto_math_probe(int op, const float* x, const float* y2, float* out, int n)
         case 8: out[i] = g_exp(a); break;
         case 9: out[i] = g_log(a); break;
         case 10: out[i] = sqrtf(a); break;
+        case 12: out[i] = a / b; break;
+        case 13: out[i] = 1.0f / sqrtf(a); break;   /* normalize()'s 1/length */
+        case 14: out[i] = 1.0f / a; break;
         case 11: {
             Inv s; memset(&s, 0, sizeof(s));
             s.seed[0] = (uint32_t)a; s.seed[1] = (uint32_t)b;

@@ -38,7 +38,7 @@ def test_library_identity(engine):
     assert bp.lib().pt_version().decode().endswith("gfx950")
 
 
-@pytest.mark.parametrize("op", list(range(12)))
+@pytest.mark.parametrize("op", list(range(15)))
 def test_pinned_math_bitexact(engine, op):
     """Device built-ins == oracle built-ins, bit for bit, over ranges the shaders use and edges."""
     import ptoracle as po
@@ -58,6 +58,12 @@ def test_pinned_math_bitexact(engine, op):
         x = np.concatenate([rng.uniform(0, 1, n), rng.uniform(0, 50, n), [0.0, 1.0]])
     elif op == 10:          # sqrt
         x = np.concatenate([rng.uniform(0, 4, n), 10.0 ** rng.uniform(-40, 38, n), [0.0, -1.0, np.inf]])
+    elif op in (12, 13, 14):  # a / b, 1 / sqrt(a), 1 / a: every exponent, denormals, edges
+        x = np.concatenate([rng.integers(0, 2 ** 32, 2 * n, dtype=np.uint64).astype(np.uint32).view(np.float32),
+                            rng.uniform(-4, 4, n).astype(np.float32),
+                            np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 1.2e-38, 8.5e37, 8.6e37,
+                                      2.0 ** 126, -2.0 ** 126, 2.0 ** -126, 2.0 ** 127], np.float32)])
+        x = x.astype(np.float64)
     else:                   # rng stream from seeds
         x = rng.integers(0, 2 ** 24, 2 * n).astype(np.float64)
     x = x.astype(np.float32)
@@ -69,11 +75,19 @@ def test_pinned_math_bitexact(engine, op):
         y = np.concatenate([rng.uniform(0.01, 3.0, x.size - 2), [2.2, 0.4545]]).astype(np.float32)
     elif op == 11:
         y = rng.integers(0, 2 ** 24, x.size).astype(np.float32)
+    elif op == 12:
+        y = rng.integers(0, 2 ** 32, x.size, dtype=np.uint64).astype(np.uint32).view(np.float32).copy()
     ref = po.math_probe(op, x, y)
     got = engine.math_probe(op, x, y)
     same = (ref.view(np.uint32) == got.view(np.uint32)) | (np.isnan(ref) & np.isnan(got))
     assert same.all(), "op %d: %d mismatches, e.g. x=%r ref=%r got=%r" % (
         op, (~same).sum(), x[~same][:3], ref[~same][:3], got[~same][:3])
+
+
+def test_fast_reciprocal_is_ieee_on_every_input(engine):
+    """grcp (v_rcp_f32 + one FMA Newton step, IEEE division outside [2^-126, 2^126)) equals the
+    correctly rounded 1.0f / x for all 2^32 binary32 inputs (NaN == NaN)."""
+    assert engine.math_exhaustive(0) == 0
 
 
 def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1):

@@ -19,6 +19,7 @@ ap.add_argument("--stream", default="gltf_bunny_1080p")
 ap.add_argument("--frames", type=int, default=20)
 ap.add_argument("--backends", default="megakernel,wavefront")
 ap.add_argument("--layouts", default="pairs,reference")
+ap.add_argument("--no-mesh-variant", action="store_true", help="skip the mesh-out-of-view run")
 ap.add_argument("--dragon", action="store_true", help="the StanfordDragon stand-in mesh instead of the stream's")
 a = ap.parse_args()
 meta = H.stream(a.stream)
@@ -33,7 +34,7 @@ for backend, layout in itertools.product(a.backends.split(","), a.layouts.split(
     e.set_backend(backend)
     e.set_bvh_layout(layout)
     call_pt = [c for c in p.meta["frames"][-1] if c["effect"] == "pathTracingEffectWrapper"][0]
-    for variant in ("mesh", "no_mesh") if "uGLTF_Model_InvMatrix" in call_pt["uniforms"] else ("mesh",):
+    for variant in ("mesh", "no_mesh") if "uGLTF_Model_InvMatrix" in call_pt["uniforms"] and not a.no_mesh_variant else ("mesh",):
         over = None
         if variant == "no_mesh":
             call0 = [c for c in p.meta["frames"][-1] if c["effect"] == "pathTracingEffectWrapper"][0]
