@@ -35,6 +35,8 @@ namespace pt {
 typedef float vf2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) vf2 lds_float2;
 typedef __attribute__((address_space(1))) vf2 glb_float2;
+// LS = lanes of the block = the stride of one stack level in LDS
+template <int LS>
 struct MegaStack {
     lds_float2* lds;
     unsigned slot;
@@ -44,14 +46,14 @@ struct MegaStack {
     PT_D float2 get(int si) const
     {
         vf2 e;
-        if (si < kStackLds) e = lds[si * kBlock + slot];
+        if (si < kStackLds) e = lds[si * LS + slot];
         else e = slab[(unsigned)(si - kStackLds) * stride + deep];
         return make_float2(e.x, e.y);
     }
     PT_D void put(int si, float2 e)
     {
         const vf2 v = { e.x, e.y };
-        if (si < kStackLds) lds[si * kBlock + slot] = v;
+        if (si < kStackLds) lds[si * LS + slot] = v;
         else slab[(unsigned)(si - kStackLds) * stride + deep] = v;
     }
 };
@@ -89,7 +91,7 @@ PT_D void meshHit(const TraceArgs& a, float triID, float triU, float triV, Hit& 
 // SceneIntersect: js/BabylonPathTracing_FragmentShader.js:47-112 (Cornell),
 // js/TransformedQuadricGeometry_FragmentShader.js:77-317 (quadrics) and
 // js/GLTFModelPathTracing_FragmentShader.js:116-346 (glTF, with the BVH walk)
-template <int PROG, bool COUNT>
+template <int PROG, bool COUNT, int LS>
 PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* lds, unsigned lane_slot,
                          unsigned deep, Cnt& cnt)
 {
@@ -104,7 +106,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
     float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
     BvhResult br = { 0.0f, 0.0f, 0.0f, false, 1u, 0u, 0u };
-    MegaStack st{ (lds_float2*)lds, lane_slot, (glb_float2*)a.spill, deep, a.spill_stride };
+    MegaStack<LS> st{ (lds_float2*)lds, lane_slot, (glb_float2*)a.spill, deep, a.spill_stride };
     if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
     else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, h.t, st, br);
     if (COUNT) { cnt.node += br.nodes; cnt.leaf += br.leaves; cnt.ovf += br.ovf; }
@@ -112,55 +114,87 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
 }
 
 // One iteration of CalculateRadiance's loop: SceneIntersect, then the shading step
-template <int PROG, bool COUNT, class G>
+template <int PROG, bool COUNT, int LS, class G>
 PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, float2* lds, unsigned lane_slot,
                      unsigned deep, Cnt& cnt)
 {
     Hit h;
-    sceneIntersect<PROG, COUNT>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt);
+    sceneIntersect<PROG, COUNT, LS>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt);
     return shadeStep<PROG, COUNT, G>(a, p, s, g, accum, h, cnt);
 }
 
-template <int PROG, bool COUNT, class G>
+template <int PROG, bool COUNT, int LS, class G>
 PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_slot, unsigned deep, Cnt& cnt)
 {
     PState s;
     pathBegin(s, g);
     f3 accum = mk(0, 0, 0);
 #pragma unroll 1
-    while (bounceStep<PROG, COUNT, G>(a, p, s, g, accum, lds, lane_slot, deep, cnt)) {}
+    while (bounceStep<PROG, COUNT, LS, G>(a, p, s, g, accum, lds, lane_slot, deep, cnt)) {}
     return max3s(accum, 0.0f);
 }
 
 PT_D float xorq(float v, int m) { return __shfl_xor(v, m, 64); }
 
+// Workgroups of kTraceBlock lanes. At one wave per workgroup (64, the default) every 8x8 wave tile
+// is its own workgroup: a wave that finishes frees its LDS (stack + G-buffer, 5.5 KB) at once,
+// instead of holding a 4-wave workgroup's 22.5 KB until the slowest of the four (sky next to
+// mesh) is done - LDS is what caps residency at 7 waves/SIMD.
+#ifndef PT_TRACE_BLOCK
+#define PT_TRACE_BLOCK 64
+#endif
+constexpr int kTraceBlock = PT_TRACE_BLOCK;
+#ifndef PT_TILE_GROUPS
+#define PT_TILE_GROUPS 1
+#endif
+constexpr int kTraceSub = 4 / (kTraceBlock / 64);   // workgroups per 16x16 tile
+static_assert(kTraceBlock == 64 || kTraceBlock == 256, "trace workgroups are one wave or one 16x16 tile");
+
 template <int PROG, bool COUNT>
-__global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
+__global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
 {
-    __shared__ float2 lds_stack[kStackLds * kBlock];
-    __shared__ float lds_gout[8 * kBlock];
+    __shared__ float2 lds_stack[kStackLds * kTraceBlock];
+    __shared__ float lds_gout[8 * kTraceBlock];
     const unsigned tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
+    const int lane = tid & 63;
+    // the 8x8 wave tile of this wave inside its 16x16 tile (grid.x = tiles_x * kTraceSub)
+    int wave, tx;
+    if (kTraceSub == 1) {
+        wave = (int)(tid >> 6);
+        tx = (int)blockIdx.x;
+    } else if (PT_TILE_GROUPS) {
+        // runs of 32 workgroups = 8 tiles x 4 quadrants, quadrant-major: the quadrants of one tile
+        // are workgroups 8 apart, which the dispatcher deals to the same XCD (one L2), while
+        // neighbouring tiles still go round-robin over the XCDs (a short last run keeps the map a
+        // bijection)
+        const unsigned g = blockIdx.x >> 5, r = blockIdx.x & 31u;
+        const unsigned T = min(8u, gridDim.x / 4u - g * 8u);
+        tx = (int)(g * 8u + r % T);
+        wave = (int)(r / T);
+    } else {
+        wave = (int)(blockIdx.x & 3u);
+        tx = (int)(blockIdx.x >> 2);
+    }
     const int lx = (lane & 1) | ((lane >> 1) & 6);
     const int ly = ((lane >> 1) & 1) | ((lane >> 3) & 6);
     const int band = blockIdx.y * a.num_parts + a.part;         // global 16-row band of this block
-    const int px = blockIdx.x * kTile + (wave & 1) * 8 + lx;
+    const int px = tx * kTile + (wave & 1) * 8 + lx;
     const int py = band * kTile + (wave >> 1) * 8 + ly;
     // stack levels >= kStackLds: a global slab [level][lane of the grid] (a private array would be
     // scratch, which the runtime reserves for every resident wave)
-    const unsigned deep = (blockIdx.y * gridDim.x + blockIdx.x) * kBlock + tid;
+    const unsigned deep = (blockIdx.y * gridDim.x + blockIdx.x) * kTraceBlock + tid;
 
     // lanes whose whole 2x2 quad lies beyond the (even-rounded) target do no work; quad helpers
     // that only complete a quad at an odd edge are shaded like GL helper invocations
     const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1);
     Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
-    GOutLds gl{ (lds_float*)lds_gout, tid };
+    GOutLds<kTraceBlock> gl{ (lds_float*)lds_gout, tid };
     gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
     f3 r = mk(0, 0, 0);
     if (active) {
         Path p;
         cameraRay(a, px, py, p);
-        r = radiance<PROG, COUNT>(a, p, gl, lds_stack, tid, deep, cnt);
+        r = radiance<PROG, COUNT, kTraceBlock>(a, p, gl, lds_stack, tid, deep, cnt);
     }
     const GOut g = gl.load();
 
@@ -279,7 +313,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_persist(TraceArgs 
             if (next >= end) break;
             continue;
         }
-        if (alive && !bounceStep<PROG, COUNT>(a, p, s, g, accum, lds_stack, tid, deep, cnt)) {
+        if (alive && !bounceStep<PROG, COUNT, kBlock>(a, p, s, g, accum, lds_stack, tid, deep, cnt)) {
             const f3 r = max3s(accum, 0.0f);
             w.gb0[pix] = make_float4(g.nrm.x, g.nrm.y, g.nrm.z, g.id);
             w.gb1[pix] = make_float4(g.col.x, g.col.y, g.col.z, g.sharp);
@@ -544,7 +578,7 @@ extern "C" {
 
 hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s)
 {
-    dim3 grid(grid_x, grid_y), block(pt::kBlock);
+    dim3 grid(grid_x * pt::kTraceSub, grid_y), block(pt::kTraceBlock);
     // texture-free models (the bench's StanfordBunny) take the variant without PBR code
     prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr);
 #define PT_CASE(P)                                                                                  \

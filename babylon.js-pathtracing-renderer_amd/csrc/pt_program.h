@@ -39,11 +39,12 @@ struct GOut {
     PT_D void setSharp(float v) { sharp = v; }
 };
 typedef __attribute__((address_space(3))) float lds_float;
+template <int LS>   // lanes of the workgroup = the stride of one field
 struct GOutLds {
     lds_float* p;
     unsigned slot;
-    PT_D void put(int f, float v) { p[f * kBlock + slot] = v; }
-    PT_D float get(int f) const { return p[f * kBlock + slot]; }
+    PT_D void put(int f, float v) { p[f * LS + slot] = v; }
+    PT_D float get(int f) const { return p[f * LS + slot]; }
     PT_D void clear() { for (int f = 0; f < 8; f++) put(f, 0.0f); }
     PT_D void setNrm(f3 v) { put(0, v.x); put(1, v.y); put(2, v.z); }
     PT_D void setCol(f3 v) { put(3, v.x); put(4, v.y); put(5, v.z); }
