@@ -46,11 +46,11 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, bool pair
 }
 // waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 80 -> 6; the
 // textured variant keeps 2 rather than spill)
-// (measured: 7 waves with 7 LDS stack levels - LDS allows 7 blocks of 22.5 KB per CU - beat 6
-// waves with 8 levels by 4 % on the dragon stand-in and tie on the bunny, though the shading code
-// spills more; 5 waves and 8 waves with 6 levels lose; the reference walk loses above 4)
+// (measured with one-wave workgroups and 7 LDS stack levels: 6 waves (80 VGPRs, 12 B of spill)
+// ~1-2 % ahead of 7 (72 VGPRs) and of 8 with 6 levels; 5 waves lose 6 %; 4-6 or 9-12 LDS levels
+// lose at 6 waves; the reference walk loses above 4)
 #ifndef PT_MINWAVES_PAIRS
-#define PT_MINWAVES_PAIRS 7
+#define PT_MINWAVES_PAIRS 6
 #endif
 template <int P> constexpr int kMinWaves = kHasTex<P> ? 2 : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
 
