@@ -96,8 +96,12 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
                          unsigned deep, Cnt& cnt)
 {
     if (COUNT) cnt.seg++;
-    analyticIntersect<PROG>(a, rayO, rayD, h);
-    if (!kIsGltf<PROG>) return;
+    // the analytic winner's t, id and object-space normal; its other attributes are resolved after
+    // the walk, and only if the mesh does not win (meshHit sets them all): fewer values live across
+    // the walk, same results
+    f3 sn;
+    analyticNearest<PROG>(a, rayO, rayD, h, sn);
+    if (!kIsGltf<PROG>) { analyticAttributes<PROG>(a, h, sn); return; }
 
     // ---- BVH walk (js/GLTFModelPathTracing_FragmentShader.js:201-298), pt_device.h
     f3 O = mul(a.model, rayO, 1.0f), D = mul(a.model, rayD, 0.0f);
@@ -111,6 +115,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, h.t, st, br);
     if (COUNT) { cnt.node += br.nodes; cnt.leaf += br.leaves; cnt.ovf += br.ovf; }
     if (br.lookup) meshHit<PROG, COUNT>(a, br.triID, br.triU, br.triV, h, cnt);
+    else analyticAttributes<PROG>(a, h, sn);
 }
 
 // One iteration of CalculateRadiance's loop: SceneIntersect, then the shading step
