@@ -149,6 +149,7 @@ struct WfBufs {
 
 struct OutputArgs {
     int width, height;      // output (canvas or render target) size
+    int num_parts, part;    // with an output partition: only 16-row bands b % num_parts == part
     int acc_w, acc_h;       // accumulation texture size (texelFetch bounds)
     float one_over_n, exposure;
     const float4* acc;

@@ -95,6 +95,8 @@ struct pt_ctx {
     unsigned long long* d_counters = nullptr;
     bool counting = false;
     int num_parts = 1, part = 0;
+    bool output_partition = false;
+    bool canvas_external = false;     // pt_canvas_wrap: caller-owned canvas memory
     int backend = PT_BACKEND_MEGAKERNEL;
     int bvh_layout = PT_BVH_PAIRS;
     int bvh_used = -1;
@@ -591,6 +593,8 @@ int render_output(pt_effect* fx, pt_texture* target)
     a.acc_h = acc->h;
     a.one_over_n = uf(fx, "uOneOverSampleCounter");
     a.exposure = uf(fx, "uToneMappingExposure");
+    a.num_parts = c->output_partition ? c->num_parts : 1;
+    a.part = c->output_partition ? c->part : 0;
     if (target) {
         if (target->kind != TEX_RT) return fail(c, PT_ERR_ARG, "screenOutput target must be a render target or the canvas");
         a.width = target->w; a.height = target->h; a.out_f = (float4*)target->d;
@@ -705,7 +709,7 @@ void pt_ctx_destroy(pt_ctx* c)
         if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
         if (c->ev1[i]) hipEventDestroy(c->ev1[i]);
     }
-    if (c->canvas) hipFree(c->canvas);
+    if (c->canvas && !c->canvas_external) hipFree(c->canvas);
     if (c->wf_mem) hipFree(c->wf_mem);
     if (c->mk_spill) hipFree(c->mk_spill);
     if (c->gb_mem) hipFree(c->gb_mem);
@@ -735,13 +739,39 @@ int pt_canvas_resize(pt_ctx* c, int w, int h)
 {
     if (!c || w < 0 || h < 0) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    if (w == c->cw && h == c->ch && c->canvas) return PT_OK;
-    if (c->canvas) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->canvas)); c->canvas = nullptr; }
+    if (w == c->cw && h == c->ch && c->canvas && !c->canvas_external) return PT_OK;
+    if (c->canvas) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (!c->canvas_external) HIPCHK(c, hipFree(c->canvas));
+        c->canvas = nullptr;
+    }
+    c->canvas_external = false;
     c->cw = w; c->ch = h;
     if (w * (size_t)h) {
         HIPCHK(c, hipMalloc(&c->canvas, (size_t)w * h * sizeof(uchar4)));
         HIPCHK(c, hipMemsetAsync(c->canvas, 0, (size_t)w * h * sizeof(uchar4), c->stream));
     }
+    return PT_OK;
+}
+
+int pt_canvas_wrap(pt_ctx* c, int w, int h, void* ptr)
+{
+    if (!c || w <= 0 || h <= 0 || !ptr) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->canvas) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (!c->canvas_external) HIPCHK(c, hipFree(c->canvas));
+    }
+    c->canvas = (uchar4*)ptr;
+    c->canvas_external = true;
+    c->cw = w; c->ch = h;
+    return PT_OK;
+}
+
+int pt_set_output_partition(pt_ctx* c, int enable)
+{
+    if (!c) return PT_ERR_ARG;
+    c->output_partition = enable != 0;
     return PT_OK;
 }
 

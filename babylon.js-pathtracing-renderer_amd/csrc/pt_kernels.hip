@@ -369,8 +369,9 @@ PT_D float4 accAt(const OutputArgs& a, int x, int y)
 
 __global__ __launch_bounds__(256) void pt_output(OutputArgs a)
 {
+    // one block per 16x16 tile of an owned band (blockIdx.y = the owned band's ordinal)
     const int x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const int y = blockIdx.y * 16 + (threadIdx.x >> 4);
+    const int y = (blockIdx.y * a.num_parts + a.part) * 16 + (threadIdx.x >> 4);
     if (x >= a.width || y >= a.height) return;
     float4 m25[25];
 #pragma unroll
@@ -647,7 +648,9 @@ hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStre
 
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s)
 {
-    dim3 grid((a->width + 15) / 16, (a->height + 15) / 16);
+    const int nb = (a->height + 15) / 16;
+    dim3 grid((a->width + 15) / 16, a->part < nb ? (nb - a->part + a->num_parts - 1) / a->num_parts : 0);
+    if (grid.y == 0) return hipSuccess;
     hipLaunchKernelGGL(pt::pt_output, grid, dim3(256), 0, s, *a);
     return hipGetLastError();
 }

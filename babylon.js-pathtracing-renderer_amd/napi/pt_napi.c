@@ -260,6 +260,16 @@ static napi_value RowPartition(napi_env env, napi_callback_info info)
 { napi_value a[MAXARGS]; if (args(env, info, a, 3) < 0) return NULL; return num(env, pt_set_row_partition((pt_ctx*)handle(env, a[0]), i32(env, a[1]), i32(env, a[2]))); }
 static napi_value SetBackend(napi_env env, napi_callback_info info)
 { napi_value a[MAXARGS]; if (args(env, info, a, 2) < 0) return NULL; return num(env, pt_set_backend((pt_ctx*)handle(env, a[0]), i32(env, a[1]))); }
+static napi_value SetOutputPartition(napi_env env, napi_callback_info info)
+{ napi_value a[MAXARGS]; if (args(env, info, a, 2) < 0) return NULL; return num(env, pt_set_output_partition((pt_ctx*)handle(env, a[0]), i32(env, a[1]))); }
+static napi_value CanvasWrap(napi_env env, napi_callback_info info)
+{
+    napi_value a[MAXARGS]; if (args(env, info, a, 4) < 0) return NULL;
+    uint64_t ptr = 0; bool lossless;
+    napi_valuetype t; napi_typeof(env, a[3], &t);
+    if (t == napi_bigint) napi_get_value_bigint_uint64(env, a[3], &ptr, &lossless);
+    return num(env, pt_canvas_wrap((pt_ctx*)handle(env, a[0]), i32(env, a[1]), i32(env, a[2]), (void*)(uintptr_t)ptr));
+}
 static napi_value SetBvhLayout(napi_env env, napi_callback_info info)
 { napi_value a[MAXARGS]; if (args(env, info, a, 2) < 0) return NULL; return num(env, pt_set_bvh_layout((pt_ctx*)handle(env, a[0]), i32(env, a[1]))); }
 static napi_value BvhLayoutUsed(napi_env env, napi_callback_info info)
@@ -345,7 +355,7 @@ static napi_value Init(napi_env env, napi_value exports)
         { "pt_render_target_create", RtCreate }, { "pt_render_target_wrap", RtWrap },
         { "pt_render_target_resize", RtResize }, { "pt_texture_size", TexSize }, { "pt_texture_destroy", TexDestroy },
         { "pt_render", Render }, { "pt_read_pixels", ReadPixels }, { "pt_write_pixels", WritePixels },
-        { "pt_set_row_partition", RowPartition }, { "pt_set_backend", SetBackend }, { "pt_set_bvh_layout", SetBvhLayout },
+        { "pt_set_row_partition", RowPartition }, { "pt_set_backend", SetBackend }, { "pt_set_output_partition", SetOutputPartition }, { "pt_canvas_wrap", CanvasWrap }, { "pt_set_bvh_layout", SetBvhLayout },
         { "pt_bvh_layout_used", BvhLayoutUsed }, { "pt_set_stream", SetStream }, { "pt_texture_device_ptr", TexDevicePtr },
         { "pt_last_render_ms", LastRenderMs }, { "pt_timing_begin", TimingBegin }, { "pt_timing_end", TimingEnd },
         { "pt_set_counting", SetCounting }, { "pt_read_counters", ReadCounters }, { "pt_reset_counters", ResetCounters }, { "pt_queue_stats", QueueStats },

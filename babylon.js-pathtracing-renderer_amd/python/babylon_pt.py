@@ -38,7 +38,7 @@ SYMBOLS = [
     "pt_texture_create_rgba32f", "pt_texture_create_rgba8", "pt_render_target_create", "pt_render_target_wrap",
     "pt_render_target_resize", "pt_texture_size", "pt_texture_destroy",
     "pt_render", "pt_read_pixels", "pt_write_pixels",
-    "pt_set_row_partition", "pt_set_backend", "pt_set_bvh_layout", "pt_bvh_layout_used", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
+    "pt_set_row_partition", "pt_set_output_partition", "pt_canvas_wrap", "pt_set_backend", "pt_set_bvh_layout", "pt_bvh_layout_used", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
     "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_math_exhaustive", "pt_bvh_build", "pt_version",
 ]
 
@@ -72,7 +72,8 @@ def lib():
         "pt_render": ([vp, vp], i32), "pt_read_pixels": ([vp, vp, vp, ctypes.c_size_t], i32),
         "pt_write_pixels": ([vp, vp, vp, ctypes.c_size_t], i32),
         "pt_set_row_partition": ([vp, i32, i32], i32), "pt_texture_device_ptr": ([vp], vp),
-        "pt_set_backend": ([vp, i32], i32), "pt_set_stream": ([vp, vp], i32),
+        "pt_set_backend": ([vp, i32], i32), "pt_set_output_partition": ([vp, i32], i32),
+        "pt_canvas_wrap": ([vp, i32, i32, vp], i32), "pt_set_stream": ([vp, vp], i32),
         "pt_set_bvh_layout": ([vp, i32], i32), "pt_bvh_layout_used": ([vp], i32),
         "pt_bvh_build": ([vp, vp, i32, vp, i32], i32),
         "pt_last_render_ms": ([vp, i32, f32p], i32), "pt_set_counting": ([vp, i32], i32),
@@ -131,6 +132,14 @@ class Engine:
 
     def set_row_partition(self, parts, part):
         self.check(lib().pt_set_row_partition(self.ctx, parts, part), "pt_set_row_partition")
+
+    def set_output_partition(self, on):
+        """screenOutput shades only this context's row bands (halo rows must be exchanged first)."""
+        self.check(lib().pt_set_output_partition(self.ctx, 1 if on else 0), "pt_set_output_partition")
+
+    def canvas_wrap(self, w, h, device_ptr):
+        """The RGBA8 canvas over caller-owned device memory (e.g. a torch uint8 tensor)."""
+        self.check(lib().pt_canvas_wrap(self.ctx, w, h, ctypes.c_void_p(device_ptr)), "pt_canvas_wrap")
 
     def set_stream(self, hip_stream):
         """Enqueue on a caller-owned stream (an int handle, e.g. torch.cuda.current_stream().cuda_stream)."""
@@ -522,6 +531,37 @@ def gather_bands(dist, acc_padded, world, rank, send_buf, gather_list, full_padd
         fv = band_view(full_padded, world)
         for r in range(world):
             fv[:, r].copy_(gather_list[r])
+
+
+def exchange_halos(dist, acc_padded, world, rank, bufs):
+    """Before a partitioned screenOutput: fill the 2 rows above and below each of this rank's bands
+    with the neighbouring bands' rows. Band b = g*world + r; its lower neighbour b-1 belongs to rank
+    r-1 (mod world) and its upper neighbour b+1 to rank r+1, so every rank sends its bands' two top
+    rows to rank r-1 and its two bottom rows to rank r+1 (one batched P2P round over RCCL or gloo),
+    and lands what it receives at those rows' own places in the frame. `bufs` = halo_buffers(...)."""
+    if world == 1:
+        return
+    bv = band_view(acc_padded, world)
+    lo, hi = (rank - 1) % world, (rank + 1) % world
+    bufs["send_top"].copy_(bv[:, rank, 0:2])
+    bufs["send_bot"].copy_(bv[:, rank, BAND - 2:BAND])
+    # the same posting order on every rank (tops first, then bottoms), so that at world 2, where both
+    # neighbours are one rank, the two messages of a pair still match in order
+    ops = [dist.P2POp(dist.isend, bufs["send_top"], lo), dist.P2POp(dist.isend, bufs["send_bot"], hi),
+           dist.P2POp(dist.irecv, bufs["recv_top"], hi), dist.P2POp(dist.irecv, bufs["recv_bot"], lo)]
+    for r in dist.batch_isend_irecv(ops):
+        r.wait()
+    bv[:, lo, BAND - 2:BAND].copy_(bufs["recv_bot"])   # rank r-1's bottom rows, under our bands
+    bv[:, hi, 0:2].copy_(bufs["recv_top"])              # rank r+1's top rows, over our bands
+
+
+def halo_buffers(acc_padded, world):
+    """Send/receive buffers for exchange_halos (same device and dtype as the accumulation)."""
+    import torch
+    rows, w, c = acc_padded.shape
+    shape = (rows // (BAND * world), 2, w, c)
+    return {k: torch.empty(shape, dtype=acc_padded.dtype, device=acc_padded.device)
+            for k in ("send_top", "send_bot", "recv_top", "recv_bot")}
 
 
 def load_stream(path):

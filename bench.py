@@ -10,8 +10,10 @@ screenOutput, as in the reference's render loop (js/GLTF_Model_Path_Tracing.js:1
 
 Multi-GPU (one process per GPU, launched by torch.distributed.run): weak scaling over the
 framebuffer. N GPUs render a frame of N x 2.07 MP (1920x1080, 3840x1080, 3840x2160, 7680x2160 for
-N = 1, 2, 4, 8), split into 16-row bands dealt round-robin (pt_set_row_partition); each frame
-the ranks' accumulation bands are gathered to rank 0 over RCCL and rank 0 runs screenOutput.
+N = 1, 2, 4, 8), split into 16-row bands dealt round-robin (pt_set_row_partition). Each frame every
+rank exchanges the 2 accumulation rows above and below its bands with its band neighbours (RCCL
+P2P), runs screenOutput on its own bands (pt_set_output_partition) into a canvas over a torch
+tensor, and the RGBA8 bands are gathered to rank 0 (RCCL) - 4 B per pixel cross the fabric, not 16.
 
 Prints ONE JSON line (rank 0).
 """
@@ -119,7 +121,7 @@ def main():
     mesh_arrays = H.synthetic_dragon() if args.workload == "dragon" else H.mesh(meta)
     mesh = H.texture_payloads(meta, mesh_arrays)
 
-    rt_ptrs, acc_t, full_t = None, None, None
+    rt_ptrs, acc_t = None, None
     pad_bands = bp.padded_bands(Hh, world)
     if dist is not None:
         import torch
@@ -138,11 +140,15 @@ def main():
 
     if dist is not None:
         import torch
-        full_t = torch.zeros((pad_bands * 16, W, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
-        send_t = torch.zeros((pad_bands // world, 16, W, 4), dtype=torch.float32, device="cuda")
+        # the canvas is the first H rows of a band-padded uint8 tensor: screenOutput writes this
+        # rank's bands there, and they are gathered to rank 0's full canvas
+        canvas_t = torch.zeros((pad_bands * 16, W, 4), dtype=torch.uint8, device="cuda")
+        engine.canvas_wrap(W, Hh, canvas_t.data_ptr())
+        engine.set_output_partition(True)
+        halo = bp.halo_buffers(acc_t, world)
+        full_t = torch.zeros((pad_bands * 16, W, 4), dtype=torch.uint8, device="cuda") if rank == 0 else None
+        send_t = torch.zeros((pad_bands // world, 16, W, 4), dtype=torch.uint8, device="cuda")
         gather_list = [torch.empty_like(send_t) for _ in range(world)] if rank == 0 else None
-        out_rt = bp.RenderTargetTexture("gathered", (W, Hh), engine, full_t.data_ptr()) if rank == 0 else None
-        out_wrapper = player.wrappers["screenOutputEffectWrapper"]
 
     def step(k):
         frame = player.synth_frame(k)
@@ -154,16 +160,11 @@ def main():
         if dist is None:
             player.play_call(out_call)
             return
-        # RCCL gather of the accumulation bands to rank 0, then screenOutput there (all on the
-        # current stream: no host synchronisation inside the frame)
-        bp.gather_bands(dist, acc_t, world, rank, send_t, gather_list, full_t)
-        if rank == 0:
-            fx = out_wrapper.effect
-            fx.setTexture("accumulationBuffer", out_rt)
-            u = out_call["uniforms"]
-            fx.setFloat("uOneOverSampleCounter", u["uOneOverSampleCounter"][1][0])
-            fx.setFloat("uToneMappingExposure", u["uToneMappingExposure"][1][0])
-            player.renderer.render(out_wrapper, None)
+        # halo rows from the band neighbours (RCCL P2P), screenOutput of this rank's bands, RCCL
+        # gather of the RGBA8 bands to rank 0 (all on the current stream: no host sync in a frame)
+        bp.exchange_halos(dist, acc_t, world, rank, halo)
+        player.play_call(out_call)
+        bp.gather_bands(dist, canvas_t, world, rank, send_t, gather_list, full_t)
 
     def barrier_sync():
         engine.sync()
@@ -240,7 +241,8 @@ def main():
                   "a 524,288-triangle procedural stand-in for the missing StanfordDragon.glb, built by the native builder")),
         "config": {"workload": workload, "width": W, "height": Hh, "spp_per_frame": 1, "max_bounces": 6,
                    "triangles": int(mesh_arrays["tri"].shape[0]), "parallelism": "row-bands x%d" % world,
-                   "gather": "rccl gather of RGBA32F bands to rank 0 per frame" if world > 1 else None},
+                   "gather": ("per frame: 2-row halo exchange with band neighbours (RCCL P2P), screenOutput "
+                              "of own bands, RCCL gather of RGBA8 bands to rank 0") if world > 1 else None},
         "pathtrace_mpaths_per_s": round(W * Hh / world / (avg_launch_ms * 1e-3) / 1e6 * world, 2),
         "kernel_ms": {"pathtrace": round(avg_launch_ms, 4), "screen_copy": round(cp_ms / max(1, pt_n), 4),
                       "screen_output": round(out_ms / max(1, pt_n), 4)},

@@ -120,10 +120,19 @@ int pt_read_pixels(pt_ctx* ctx, const pt_texture* tex, void* dst, size_t bytes);
 int pt_write_pixels(pt_ctx* ctx, pt_texture* tex, const void* src, size_t bytes);
 
 /* ---- MI355X extensions (no reference counterpart) -------------------------------------------
- * Row-band sharding for multi-GPU rendering: this context's path-tracing passes shade only the
- * 16-row bands b with b % num_parts == part (bands are whole 2x2 quads, so derivatives are
- * unchanged). screenOutput/copy stay full-frame. num_parts = 1 restores full frames. */
+ * Row-band sharding for multi-GPU rendering: this context's path-tracing and screenCopy passes
+ * shade only the 16-row bands b with b % num_parts == part (bands are whole 2x2 quads, so
+ * derivatives are unchanged). num_parts = 1 restores full frames. */
 int pt_set_row_partition(pt_ctx* ctx, int num_parts, int part);
+/* screenOutput under the row partition too (enable = 1): only the owned bands of the output are
+ * written. Its 5x5 filter reads the accumulation 2 rows beyond each band, so those halo rows must
+ * hold the neighbouring ranks' values (babylon_pt.exchange_halos) before the draw. Default 0:
+ * screenOutput shades the whole frame. */
+int pt_set_output_partition(pt_ctx* ctx, int enable);
+/* The canvas over caller-owned device memory: width*height RGBA8 texels, rows bottom-up (e.g. a
+ * torch tensor that RCCL gathers from). Not freed by the context; pt_canvas_resize replaces it
+ * with context-owned memory again. */
+int pt_canvas_wrap(pt_ctx* ctx, int width, int height, void* device_ptr);
 /* Path-tracing backend of this context: PT_BACKEND_MEGAKERNEL (default: one kernel, one lane per
  * path), PT_BACKEND_WAVEFRONT (per-segment kernels over compacted path queues) or
  * PT_BACKEND_PERSISTENT (waves regenerate finished lanes with new pixels; G-buffer + finish pass).

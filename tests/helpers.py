@@ -220,3 +220,9 @@ def synthetic_dragon(nu=512, nv=512, knot=(1, 1), tube=9.0):
     lo, hi = pos.min(1), pos.max(1)
     aabb_in = np.concatenate([lo, hi, (lo + hi) * 0.5], 1).astype(np.float32)
     return {"bvh": bp.bvh_build(aabb_in), "tri": tri, "aabb_in": aabb_in}
+
+
+def po_screen_output(acc, one_over_n, exposure=1.0):
+    """The oracle's screenOutput (js/PathTracingCommon.js:19-309) of an RGBA32F frame -> RGBA8."""
+    import ptoracle as po
+    return po.screen_output(acc, one_over_n, exposure)

@@ -59,3 +59,51 @@ def test_band_gather_assembles_the_frame(tmp_path, world):
     meta = H.stream(name)
     ref, _, _ = H.oracle_replay(meta, 1, width=w, height=h)
     assert np.array_equal(got.view(np.uint32), ref[0].view(np.uint32))
+
+
+def _worker_output(rank, world, port, name, w, h, out_path):
+    """Distributed screenOutput: each rank shades its bands, exchanges 2-row halos with its band
+    neighbours (babylon_pt.exchange_halos), runs screenOutput on its own bands only and the RGBA8
+    bands are gathered to rank 0 - the path bench.py takes at N > 1."""
+    import babylon_pt as bp
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        meta = H.stream(name)
+        sc = H.oracle_scene(meta, w, h)
+        u = H.with_resolution(H.path_call(meta["frames"][0])["uniforms"], w, h)
+        pad = bp.padded_bands(h, world)
+        acc = torch.zeros((pad * 16, w, 4), dtype=torch.float32)
+        prev = np.zeros((h, w, 4), np.float32)
+        mine = bp.owned_rows(h, world, rank)
+        for b in range(rank, (h + 15) // 16, world):
+            r0, r1 = b * 16, min(h, (b + 1) * 16)
+            out, _ = sc.path_trace(u, prev, r0, r1, nthreads=2)
+            acc[r0:r1] = torch.from_numpy(out[r0:r1])
+        bp.exchange_halos(dist, acc, world, rank, bp.halo_buffers(acc, world))
+        # the halo rows now hold the neighbours' values; everything else not owned stays zero
+        local = acc[:h].numpy()
+        out8 = torch.zeros((pad * 16, w, 4), dtype=torch.uint8)
+        shaded = H.po_screen_output(local, 1.0)
+        out8[mine] = torch.from_numpy(shaded[mine])
+        send = torch.zeros((pad // world, 16, w, 4), dtype=torch.uint8)
+        glist = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+        full = torch.zeros((pad * 16, w, 4), dtype=torch.uint8) if rank == 0 else None
+        bp.gather_bands(dist, out8, world, rank, send, glist, full)
+        if rank == 0:
+            np.save(out_path, full[:h].numpy())
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_partitioned_output_with_halo_exchange(tmp_path, world):
+    name, w, h = "gltf_teapot_320x180", 96, 72
+    out = str(tmp_path / "canvas.npy")
+    mp.spawn(_worker_output, args=(world, _free_port(), name, w, h, out), nprocs=world, join=True)
+    got = np.load(out)
+    meta = H.stream(name)
+    ref, _, _ = H.oracle_replay(meta, 1, width=w, height=h)
+    want = H.po_screen_output(ref[0], 1.0)
+    assert np.array_equal(got, want)

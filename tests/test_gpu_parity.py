@@ -90,7 +90,7 @@ def test_fast_reciprocal_is_ieee_on_every_input(engine):
     assert engine.math_exhaustive(0) == 0
 
 
-def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1):
+def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1, split_output=False):
     import babylon_pt as bp
     m = None
     if meta["scene"] in ("gltf", "hdri"):
@@ -110,8 +110,17 @@ def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1):
                 engine.set_row_partition(parts, p)
                 player.play_call(calls[0])
             engine.set_row_partition(1, 0)
-            for c in calls[1:]:
-                player.play_call(c)
+            if split_output:   # copy full-frame, then screenOutput band by band (output partition)
+                player.play_call(calls[1])
+                engine.set_output_partition(True)
+                for p in range(parts):
+                    engine.set_row_partition(parts, p)
+                    player.play_call(calls[2])
+                engine.set_output_partition(False)
+                engine.set_row_partition(1, 0)
+            else:
+                for c in calls[1:]:
+                    player.play_call(c)
         engine.sync()
         accs.append(player.textures["pathTracingRenderTarget"].read())
         canvases.append(engine.read_canvas(w, h))
@@ -285,6 +294,17 @@ def test_row_partition_is_exact(engine, backend, parts):
     split, _, _ = _replay_gpu(engine, meta, 2, parts=parts)
     for a, b in zip(full, split):
         assert _bits_equal(a, b), _diff_report(a, b)
+
+
+@pytest.mark.parametrize("parts", [2, 3, 8])
+def test_partitioned_screen_output_is_exact(engine, parts):
+    """screenOutput under the output partition, band by band, gives the full-frame canvas (the
+    halo rows are all present here: every part writes the same accumulation target)."""
+    meta = H.stream("gltf_teapot_320x180")
+    _, full, _ = _replay_gpu(engine, meta, 2)
+    _, split, _ = _replay_gpu(engine, meta, 2, parts=parts, split_output=True)
+    for a, b in zip(full, split):
+        assert np.array_equal(a, b)
 
 
 def test_odd_sizes_bitexact(engine, backend):
