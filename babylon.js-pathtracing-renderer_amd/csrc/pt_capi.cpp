@@ -1063,7 +1063,7 @@ int pt_queue_stats(pt_ctx* c, uint32_t out[16])
 
 int pt_math_exhaustive(pt_ctx* c, int op, uint64_t* mismatches)
 {
-    if (!c || !mismatches || op != 0) return PT_ERR_ARG;
+    if (!c || !mismatches || op < 0 || op > 1) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     unsigned long long* d = nullptr;
     HIPCHK(c, hipMalloc(&d, sizeof(unsigned long long)));

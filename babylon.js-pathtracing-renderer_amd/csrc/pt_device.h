@@ -76,7 +76,7 @@ PT_D float blueNoise_rand(Path& p)
     int channel = (int)gmod(p.counter, 2.0f);
     return gfract(channel == 0 ? p.bn0 : p.bn1);
 }
-PT_D float tentFilter(float x) { return (x < 0.5f) ? sqrtf(2.0f * x) - 1.0f : 1.0f - sqrtf(2.0f - (2.0f * x)); }
+PT_D float tentFilter(float x) { return (x < 0.5f) ? gsqrt(2.0f * x) - 1.0f : 1.0f - gsqrt(2.0f - (2.0f * x)); }
 PT_D f3 onb_u(f3 nl)
 {
     f3 a = (fabsf(nl.y) < 0.9f) ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
@@ -84,12 +84,12 @@ PT_D f3 onb_u(f3 nl)
 }
 PT_D f3 cosWeightedDir(Path& p, f3 nl)
 {
-    float r = sqrtf(rng(p));
+    float r = gsqrt(rng(p));
     float phi = rng(p) * kTwoPi;
     float sn, cs;
     gsincos(phi, sn, cs);
     float x = r * cs, y = r * sn;
-    float z = sqrtf(1.0f - x * x - y * y);
+    float z = gsqrt(1.0f - x * x - y * y);
     f3 U = onb_u(nl);
     f3 V = cross(nl, U);
     return normalize(U * x + V * y + nl * z);
@@ -97,9 +97,9 @@ PT_D f3 cosWeightedDir(Path& p, f3 nl)
 PT_D f3 specularLobeDir(Path& p, f3 rdir, float roughness)
 {
     roughness = gclamp(roughness, 0.0f, 1.0f);
-    float exponent = gmix(7.0f, 0.0f, sqrtf(roughness));
+    float exponent = gmix(7.0f, 0.0f, gsqrt(roughness));
     float cosTheta = gpow(rng(p), grcp(gexp(exponent) + 1.0f));
-    float sinTheta = sqrtf(gmax(0.0f, 1.0f - cosTheta * cosTheta));
+    float sinTheta = gsqrt(gmax(0.0f, 1.0f - cosTheta * cosTheta));
     float phi = rng(p) * kTwoPi;
     float sn, cs;
     gsincos(phi, sn, cs);
@@ -114,9 +114,9 @@ PT_D float fresnel(f3 rdir, f3 n, float etai, float etat, float& ratioIoR)
     float cosi = gclamp(dot(rdir, n), -1.0f, 1.0f);
     if (cosi > 0.0f) { etai = etat; etat = temp; }
     ratioIoR = etai / etat;
-    float sint = ratioIoR * sqrtf(1.0f - (cosi * cosi));
+    float sint = ratioIoR * gsqrt(1.0f - (cosi * cosi));
     if (sint >= 1.0f) return 1.0f;
-    float cost = sqrtf(1.0f - (sint * sint));
+    float cost = gsqrt(1.0f - (sint * sint));
     cosi = fabsf(cosi);
     float Rs = ((etat * cosi) - (etai * cost)) / ((etat * cosi) + (etai * cost));
     float Rp = ((etai * cosi) - (etat * cost)) / ((etai * cosi) + (etat * cost));
@@ -131,7 +131,7 @@ PT_D f3 sampleQuadLight(Path& p, const TraceArgs& a, f3 x, f3 nl, float& weight)
     q.z = gmix(L.v0.z, L.v2.z, gclamp(rng(p), 0.1f, 0.9f));
     f3 d = q - x;
     float d2 = dot(d, d);
-    float cos_a_max = sqrtf(1.0f - gclamp(a.light_r2 / d2, 0.0f, 1.0f));
+    float cos_a_max = gsqrt(1.0f - gclamp(a.light_r2 / d2, 0.0f, 1.0f));
     d = normalize(d);
     float dotNl = gmax(0.0f, dot(nl, d));
     float w = 2.0f * (1.0f - cos_a_max) * gmax(0.0f, -dot(d, L.normal)) * dotNl;
@@ -151,7 +151,7 @@ PT_D float unitSphere(f3 ro, f3 rd, f3& n)
     float nh = -b * 0.5f;
     float u2 = nh * nh - c;
     float u;
-    if (u2 < 0.0f) { nh = 0.0f; u = 0.0f; } else u = sqrtf(u2);
+    if (u2 < 0.0f) { nh = 0.0f; u = 0.0f; } else u = gsqrt(u2);
     float t0 = nh - u, t1 = nh + u;
     float t = t0 > 0.0f ? t0 : t1 > 0.0f ? t1 : kINF;
     if (t != kINF) { f3 h = ro + rd * t; n = mk(2.0f * h.x, 2.0f * h.y, 2.0f * h.z); }

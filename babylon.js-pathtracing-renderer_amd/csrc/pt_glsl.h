@@ -33,6 +33,27 @@ PT_HD float grcp(float x)
     return 1.0f / x;
 }
 
+// correctly rounded sqrt(x). On the device, for x in [2^-96, 2^126]: v_sqrt_f32 and the one-ulp
+// correction by the signs of the FMA residuals x - s(s -/+ ulp) (the correction hipcc emits too,
+// without its tiny-input scaling and special-value selects: 9 VALU instead of 17); every other
+// input (zero, tiny, huge, negative, inf, NaN) takes sqrtf. Checked exhaustively on gfx950
+// (pt_math_exhaustive op 1).
+PT_HD float gsqrt(float x)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+    const uint32_t b = __builtin_bit_cast(uint32_t, x);
+    if (__builtin_expect(b - 0x0f800000u <= 0x7e800000u - 0x0f800000u, 1)) {
+        const float s = __builtin_amdgcn_sqrtf(x);
+        const uint32_t sb = __builtin_bit_cast(uint32_t, s);
+        const float dn = __builtin_bit_cast(float, sb - 1u), up = __builtin_bit_cast(float, sb + 1u);
+        float r = __builtin_fmaf(-dn, s, x) <= 0.0f ? dn : s;
+        r = __builtin_fmaf(-up, s, x) > 0.0f ? up : r;
+        return r;
+    }
+#endif
+    return sqrtf(x);
+}
+
 PT_HD float gmin(float x, float y) { return y < x ? y : x; }
 PT_HD float gmax(float x, float y) { return x < y ? y : x; }
 PT_HD float gclamp(float x, float a, float b) { return gmin(gmax(x, a), b); }
@@ -156,7 +177,7 @@ PT_HD float gacos(float x)
 {
     if (!(x >= -1.0f && x <= 1.0f)) return __builtin_nanf("");
     if (x == -1.0f) return 3.14159265358979323f;
-    return 2.0f * gatan(sqrtf((1.0f - x) / (1.0f + x)));
+    return 2.0f * gatan(gsqrt((1.0f - x) / (1.0f + x)));
 }
 
 // ------------------------------------------------------------------------------------- vec3
@@ -170,8 +191,8 @@ PT_HD f3 operator-(f3 a) { return mk(-a.x, -a.y, -a.z); }
 PT_HD f3 operator/(f3 a, f3 b) { return mk(a.x / b.x, a.y / b.y, a.z / b.z); }
 PT_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 PT_HD f3 cross(f3 a, f3 b) { return mk(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y); }
-PT_HD float length(f3 a) { return sqrtf(dot(a, a)); }
-PT_HD f3 normalize(f3 a) { float inv = grcp(sqrtf(dot(a, a))); return a * inv; }
+PT_HD float length(f3 a) { return gsqrt(dot(a, a)); }
+PT_HD f3 normalize(f3 a) { float inv = grcp(gsqrt(dot(a, a))); return a * inv; }
 PT_HD float distance(f3 a, f3 b) { return length(a - b); }
 PT_HD f3 reflect(f3 I, f3 N) { return I - N * (2.0f * dot(N, I)); }
 PT_HD f3 refract(f3 I, f3 N, float eta)
@@ -179,7 +200,7 @@ PT_HD f3 refract(f3 I, f3 N, float eta)
     float d = dot(N, I);
     float k = 1.0f - eta * eta * (1.0f - d * d);
     if (k < 0.0f) return mk(0.0f, 0.0f, 0.0f);
-    return I * eta - N * (eta * d + sqrtf(k));
+    return I * eta - N * (eta * d + gsqrt(k));
 }
 PT_HD f3 mix3(f3 a, f3 b, float t) { return mk(gmix(a.x, b.x, t), gmix(a.y, b.y, t), gmix(a.z, b.z, t)); }
 PT_HD f3 clamp3(f3 a, float lo, float hi) { return mk(gclamp(a.x, lo, hi), gclamp(a.y, lo, hi), gclamp(a.z, lo, hi)); }

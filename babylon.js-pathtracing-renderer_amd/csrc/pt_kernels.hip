@@ -545,6 +545,7 @@ __global__ __launch_bounds__(256) void pt_exhaustive_kernel(int op, uint32_t hi,
     const float x = __uint_as_float(bits);
     float got = 0.0f, ref = 0.0f;
     if (op == 0) { got = grcp(x); ref = 1.0f / x; }
+    else if (op == 1) { got = gsqrt(x); ref = sqrtf(x); }
     const bool ok = (ref != ref) ? (got != got) : (__float_as_uint(got) == __float_as_uint(ref));
     const unsigned long long m = __ballot(!ok);
     if (m && (threadIdx.x & 63u) == (unsigned)(__ffsll((long long)m) - 1)) atomicAdd(bad, (unsigned long long)__popcll(m));
@@ -567,10 +568,10 @@ __global__ void pt_math_probe_kernel(int op, const float* x, const float* y, flo
     case 7: r = gpow(a, b); break;
     case 8: r = gexp(a); break;
     case 9: r = glog(a); break;
-    case 10: r = sqrtf(a); break;
+    case 10: r = gsqrt(a); break;
     case 11: { Path p; p.s0 = (uint32_t)a; p.s1 = (uint32_t)b; r = rng(p); break; }
     case 12: r = a / b; break;
-    case 13: r = grcp(sqrtf(a)); break;
+    case 13: r = grcp(gsqrt(a)); break;
     case 14: r = grcp(a); break;
     default: r = 0.0f;
     }

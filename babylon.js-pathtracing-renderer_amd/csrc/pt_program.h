@@ -380,7 +380,7 @@ PT_D void cameraRay(const TraceArgs& a, int px, int py, Path& p)
     float rad = rng(p) * a.aperture;
     float sn, cs;
     gsincos(ang, sn, cs);
-    f3 apert = (camRight * cs + camUp * sn) * sqrtf(rad);
+    f3 apert = (camRight * cs + camUp * sn) * gsqrt(rad);
     p.rd = normalize(focal - apert);
     p.ro = camPos + apert;
 }

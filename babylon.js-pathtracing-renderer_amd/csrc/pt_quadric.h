@@ -24,7 +24,7 @@ PT_D Roots solveQuadratic(float A, float B, float C)
     float nh = -B * 0.5f;
     float u2 = nh * nh - C;
     float u;
-    if (u2 < 0.0f) { nh = 0.0f; u = 0.0f; } else u = sqrtf(u2);
+    if (u2 < 0.0f) { nh = 0.0f; u = 0.0f; } else u = gsqrt(u2);
     return Roots{ nh - u, nh + u };
 }
 
@@ -248,8 +248,8 @@ PT_D float unitRectangle(f3 ro, f3 rd)
 
 PT_D float mapTorus(f3 p, float k)
 {
-    const float a = sqrtf(p.x * p.x + p.z * p.z) - (1.0f - k);
-    return sqrtf(a * a + p.y * p.y) - k;
+    const float a = gsqrt(p.x * p.x + p.z * p.z) - (1.0f - k);
+    return gsqrt(a * a + p.y * p.y) - k;
 }
 
 // ray-marched torus (<= 500 sphere-tracing steps from the bounding cylinder / caps)

@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kBlock) void wf_raygen(TraceArgs a, WfBufs w)
         float rad = rng(p) * a.aperture;
         float sn, cs;
         gsincos(ang, sn, cs);
-        f3 apert = (camRight * cs + camUp * sn) * sqrtf(rad);
+        f3 apert = (camRight * cs + camUp * sn) * gsqrt(rad);
         p.rd = normalize(focal - apert);
         p.ro = camPos + apert;
         // per-pixel outputs start at the `out` parameters' pinned zero

@@ -173,7 +173,8 @@ int pt_queue_stats(pt_ctx* ctx, uint32_t out[16]);
 /* Device self-test of the pinned GLSL built-ins (ops as the oracle's pto_math_probe). */
 int pt_math_probe(pt_ctx* ctx, int op, const float* x, const float* y, float* out, int n);
 /* Exhaustive device self-test of a fast built-in sequence against the IEEE operation it replaces,
- * over all 2^32 binary32 inputs: op 0 = the reciprocal (grcp vs 1.0f/x). Writes the mismatch count. */
+ * over all 2^32 binary32 inputs: op 0 = the reciprocal (grcp vs 1.0f/x), op 1 = the square root
+ * (gsqrt vs sqrtf). Writes the mismatch count. */
 int pt_math_exhaustive(pt_ctx* ctx, int op, uint64_t* mismatches);
 /* BVH_Build_Iterative(workList, aabb_array) (js/BVH_Fast_Builder.js:320-406) as native host code:
  * aabb_in = the per-triangle AABBs the setup script fills (9 floats: min.xyz, max.xyz,

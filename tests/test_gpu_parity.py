@@ -90,6 +90,12 @@ def test_fast_reciprocal_is_ieee_on_every_input(engine):
     assert engine.math_exhaustive(0) == 0
 
 
+def test_fast_sqrt_is_ieee_on_every_input(engine):
+    """gsqrt (v_sqrt_f32 + residual-sign correction on [2^-96, 2^126], sqrtf elsewhere) equals
+    the correctly rounded sqrtf for all 2^32 binary32 inputs (NaN == NaN)."""
+    assert engine.math_exhaustive(1) == 0
+
+
 def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1, split_output=False):
     import babylon_pt as bp
     m = None
