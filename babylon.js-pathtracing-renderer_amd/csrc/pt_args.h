@@ -155,6 +155,7 @@ struct OutputArgs {
     const float4* acc;
     uchar4* canvas;         // RGBA8 target (NULL when writing float)
     float4* out_f;          // RGBA32F target (NULL when writing the canvas)
+    float4* copy_dst;       // a deferred screenCopy of `acc` fused into this pass (NULL: none)
 };
 
 struct CopyArgs {

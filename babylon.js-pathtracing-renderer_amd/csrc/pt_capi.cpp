@@ -96,6 +96,9 @@ struct pt_ctx {
     bool counting = false;
     int num_parts = 1, part = 0;
     bool output_partition = false;
+    // screenCopy deferred to ride along with the next screenOutput of the same source (flushed as
+    // its own kernel before anything else could observe the target: flush_copy)
+    struct { bool on; pt_texture* src; pt_texture* dst; int num_parts, part; } pending_copy = {};
     bool canvas_external = false;     // pt_canvas_wrap: caller-owned canvas memory
     int backend = PT_BACKEND_MEGAKERNEL;
     int bvh_layout = PT_BVH_PAIRS;
@@ -564,6 +567,27 @@ int render_trace(pt_effect* fx, pt_texture* target)
     return end_draw(c, fx->prog);
 }
 
+int launch_copy(pt_ctx* c, pt_texture* src, pt_texture* dst, int num_parts, int part)
+{
+    pt::CopyArgs a{ dst->w, dst->h, num_parts, part, (const float4*)src->d, (float4*)dst->d };
+    const int nb = (dst->h + pt::kTile - 1) / pt::kTile;
+    int gx = (dst->w + 255) / 256, gy = part < nb ? (nb - part + num_parts - 1) / num_parts : 0;
+    if (gy > 0) HIPCHK(c, pt_launch_copy(&a, gx, gy, c->stream));
+    return PT_OK;
+}
+
+// run a deferred screenCopy now, as its own kernel (timed as a screenCopy draw)
+int flush_copy(pt_ctx* c)
+{
+    if (!c->pending_copy.on) return PT_OK;
+    c->pending_copy.on = false;
+    int rc = begin_draw(c, PT_PROG_SCREEN_COPY);
+    if (rc) return rc;
+    rc = launch_copy(c, c->pending_copy.src, c->pending_copy.dst, c->pending_copy.num_parts, c->pending_copy.part);
+    if (rc) return rc;
+    return end_draw(c, PT_PROG_SCREEN_COPY);
+}
+
 int render_copy(pt_effect* fx, pt_texture* target)
 {
     pt_ctx* c = fx->ctx;
@@ -571,14 +595,12 @@ int render_copy(pt_effect* fx, pt_texture* target)
     if (!target || target->kind != TEX_RT) return fail(c, PT_ERR_ARG, "screenCopy needs a render target");
     if (!src || src->kind == TEX_U8 || src->w != target->w || src->h != target->h)
         return fail(c, PT_ERR_STATE, "pathTracedImageBuffer must be an RGBA32F texture of the target's size");
-    int rc = begin_draw(c, fx->prog);
+    int rc = flush_copy(c);
     if (rc) return rc;
-    if (src != target) {
-        pt::CopyArgs a{ target->w, target->h, c->num_parts, c->part, (const float4*)src->d, (float4*)target->d };
-        int gx = (target->w + 255) / 256, gy = bands_owned(c, target->h);
-        if (gy > 0) HIPCHK(c, pt_launch_copy(&a, gx, gy, c->stream));
-    }
-    return end_draw(c, fx->prog);
+    // deferred: the render loop's next draw is screenOutput of the same source, which writes the
+    // copy target in the same pass (render_output); any other use flushes it first (flush_copy)
+    if (src != target) c->pending_copy = { true, src, target, c->num_parts, c->part };
+    return PT_OK;
 }
 
 int render_output(pt_effect* fx, pt_texture* target)
@@ -595,6 +617,14 @@ int render_output(pt_effect* fx, pt_texture* target)
     a.exposure = uf(fx, "uToneMappingExposure");
     a.num_parts = c->output_partition ? c->num_parts : 1;
     a.part = c->output_partition ? c->part : 0;
+    // fuse the deferred screenCopy when this pass covers exactly its texels: same source, same
+    // frame size, same bands, and the copy target is not this pass's output
+    const auto& pc = c->pending_copy;
+    const int ow = target ? target->w : (c->cw || c->ch ? c->cw : acc->w), oh = target ? target->h : (c->cw || c->ch ? c->ch : acc->h);
+    const bool fuse = pc.on && pc.src == acc && pc.dst != target && ow == acc->w && oh == acc->h &&
+                      pc.num_parts == a.num_parts && (pc.num_parts == 1 || pc.part == a.part);
+    if (fuse) { a.copy_dst = (float4*)pc.dst->d; c->pending_copy.on = false; }
+    else { int frc = flush_copy(c); if (frc) return frc; }
     if (target) {
         if (target->kind != TEX_RT) return fail(c, PT_ERR_ARG, "screenOutput target must be a render target or the canvas");
         a.width = target->w; a.height = target->h; a.out_f = (float4*)target->d;
@@ -699,6 +729,7 @@ void pt_ctx_destroy(pt_ctx* c)
 {
     if (!c) return;
     hipSetDevice(c->device);
+    c->pending_copy.on = false;   // nothing can observe its target any more
     if (c->stream) hipStreamSynchronize(c->stream);
     std::vector<pt_effect*> fx(c->effects.begin(), c->effects.end());
     for (auto* f : fx) pt_effect_destroy(f);
@@ -725,6 +756,7 @@ int pt_sync(pt_ctx* c)
 {
     if (!c) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = flush_copy(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     unsigned flags = 0;
     HIPCHK(c, hipMemcpy(&flags, c->d_err, sizeof(flags), hipMemcpyDeviceToHost));
@@ -876,6 +908,7 @@ int pt_render_target_resize(pt_texture* t, int w, int h)
     pt_ctx* c = t->ctx;
     if (w == t->w && h == t->h) return PT_OK;
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = flush_copy(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (t->d) HIPCHK(c, hipFree(t->d));
     t->d = nullptr;
@@ -898,6 +931,7 @@ void pt_texture_destroy(pt_texture* t)
     if (!t) return;
     pt_ctx* c = t->ctx;
     hipSetDevice(c->device);
+    if (c->pending_copy.on && (c->pending_copy.src == t || c->pending_copy.dst == t)) flush_copy(c);
     for (auto* fx : c->effects)
         for (auto& kv : fx->samplers)
             if (kv.second == t) kv.second = nullptr;
@@ -915,6 +949,10 @@ int pt_render(pt_effect* fx, pt_texture* target)
     pt_ctx* c = fx->ctx;
     if (target && target->ctx != c) return fail(c, PT_ERR_ARG, "target belongs to another context");
     HIPCHK(c, hipSetDevice(c->device));
+    if (fx->prog != PT_PROG_SCREEN_OUTPUT && fx->prog != PT_PROG_SCREEN_COPY) {
+        int rc = flush_copy(c);
+        if (rc) return rc;
+    }
     switch (fx->prog) {
     case PT_PROG_CORNELL:
     case PT_PROG_QUADRIC:
@@ -931,6 +969,7 @@ int pt_read_pixels(pt_ctx* c, const pt_texture* t, void* dst, size_t bytes)
 {
     if (!c || !dst) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = flush_copy(c)) return rc;
     const void* src = t ? t->d : (const void*)c->canvas;
     size_t need = t ? t->bytes : (size_t)c->cw * c->ch * sizeof(uchar4);
     if (bytes < need) return fail(c, PT_ERR_ARG, "destination too small");
@@ -943,6 +982,7 @@ int pt_write_pixels(pt_ctx* c, pt_texture* t, const void* src, size_t bytes)
 {
     if (!c || !t || !src || bytes != t->bytes) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = flush_copy(c)) return rc;
     HIPCHK(c, hipMemcpyAsync(t->d, src, bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     t->gen++;
@@ -953,6 +993,7 @@ int pt_set_stream(pt_ctx* c, void* stream)
 {
     if (!c) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = flush_copy(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));   // work already queued finishes first
     c->stream = stream ? (hipStream_t)stream : c->own_stream;
     return PT_OK;
@@ -1005,6 +1046,7 @@ int pt_timing_end(pt_ctx* c, int prog, double* total_ms, int* launches)
 {
     if (!c || !total_ms || !launches) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = flush_copy(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     double t = 0.0;
     int n = 0;

@@ -369,13 +369,25 @@ PT_D float4 accAt(const OutputArgs& a, int x, int y)
 
 __global__ __launch_bounds__(256) void pt_output(OutputArgs a)
 {
-    // one block per 16x16 tile of an owned band (blockIdx.y = the owned band's ordinal)
-    const int x = blockIdx.x * 16 + (threadIdx.x & 15);
-    const int y = (blockIdx.y * a.num_parts + a.part) * 16 + (threadIdx.x >> 4);
+    // one block per 16x16 tile of an owned band (blockIdx.y = the owned band's ordinal); the tile's
+    // 20x20 neighbourhood (+-2 texels, texelFetch semantics: 0 outside the accumulation texture) is
+    // staged once in LDS, so each texel is read from L2 once instead of by 25 taps
+    __shared__ float4 tile[20 * 20];
+    const int x0 = blockIdx.x * 16, y0 = (blockIdx.y * a.num_parts + a.part) * 16;
+    for (int i = threadIdx.x; i < 400; i += 256) {
+        const int tx = i % 20, ty = i / 20;
+        tile[i] = accAt(a, x0 + tx - 2, y0 + ty - 2);
+    }
+    __syncthreads();
+    const int lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
+    const int x = x0 + lx, y = y0 + ly;
     if (x >= a.width || y >= a.height) return;
     float4 m25[25];
 #pragma unroll
-    for (int k = 0; k < 25; k++) m25[k] = accAt(a, x + (k % 5) - 2, y + 2 - (k / 5));
+    for (int k = 0; k < 25; k++) m25[k] = tile[(ly + 2 + 2 - (k / 5)) * 20 + (lx + 2 + (k % 5) - 2)];
+    // the frame's screenCopy (js/PathTracingCommon.js:1-16), deferred by the host to ride along:
+    // the same texel of the same source, written to the copy target
+    if (a.copy_dst) a.copy_dst[(long long)y * a.acc_w + x] = m25[12];
     const float th = 1.0f;
     float4 cp = m25[12];
     float fr = cp.x, fg = cp.y, fb = cp.z;

@@ -111,6 +111,10 @@ void pt_texture_destroy(pt_texture* tex);
 /* ---- draw: replaces eRenderer.render(effectWrapper, renderTargetOrNull)
  * (js/GLTF_Model_Path_Tracing.js:1230-1235). target NULL = the canvas. */
 int pt_render(pt_effect* fx, pt_texture* target);
+/* (A screenCopy draw may be deferred until the next draw: when that draw is the screenOutput of
+ * the same source it writes the copy in the same pass. Every pt_* call that could observe the copy
+ * target - another draw, read/write pixels, resize, destroy, pt_sync, pt_set_stream - runs it
+ * first; code reading a wrapped render target's memory directly calls pt_sync before.) */
 
 /* readPixels of a render target (RGBA32F, 16 B/texel) or of the canvas (tex NULL, RGBA8),
  * rows bottom-up; synchronises. */

@@ -313,6 +313,29 @@ def test_partitioned_screen_output_is_exact(engine, parts):
         assert np.array_equal(a, b)
 
 
+def test_deferred_screen_copy_is_observed_exactly(engine):
+    """screenCopy is deferred to ride along with the next screenOutput of the same source; reading
+    its target first, or drawing anything else first, must still see the copy."""
+    import babylon_pt as bp
+    meta = H.stream("gltf_teapot_320x180")
+    player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, H.mesh(meta)))
+    pt_call, cp_call, out_call = meta["frames"][0]
+    player.play_call(pt_call)
+    player.play_call(cp_call)
+    acc = player.textures["pathTracingRenderTarget"].read()          # flushes nothing it needs
+    copied = player.textures["screenCopyRenderTarget"].read()        # must flush the copy
+    assert _bits_equal(acc, copied)
+    # copy deferred, then the next frame's path tracing reads it as previousBuffer
+    f1 = meta["frames"][1]
+    player.play_call(f1[0])
+    player.play_call(f1[1])
+    player.play_call(meta["frames"][2][0])                            # flush before this draw
+    engine.sync()
+    ref, _, _ = H.oracle_replay(meta, 3)
+    # frame 2's path tracing used frame 1's copy as history
+    assert _bits_equal(ref[2], player.textures["pathTracingRenderTarget"].read())
+
+
 def test_odd_sizes_bitexact(engine, backend):
     """Odd target sizes: quad helpers beyond the edge, partial 16x16 tiles, partial bands."""
     meta = H.stream("gltf_teapot_320x180")
