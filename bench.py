@@ -33,7 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 FRAME_SIZES = {1: (1920, 1080), 2: (3840, 1080), 4: (3840, 2160), 8: (7680, 2160)}
 PEAK_HBM_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 # algorithmic bytes per counted event
-BYTES = {"node_fetches": 32, "leaf_tests": 48, "hit_lookups": 128, "rgba8_taps": 4}
+BYTES = {"node_fetches": 32, "leaf_tests": 48, "hit_lookups": 128, "rgba8_taps": 4, "hdr_taps": 16}
 PIXEL_IO = 32                  # previousBuffer texel read + accumulation texel write (+4 B blue noise = an rgba8 tap)
 
 
@@ -47,13 +47,13 @@ def algorithmic_bytes(cnt):
     return sum(cnt[k] * b for k, b in BYTES.items()) + PIXEL_IO * cnt["paths"]
 
 
-def cpu_baseline(meta, width, height, budget_s, mesh=None):
+def cpu_baseline(meta, width, height, budget_s, mesh=None, maps=None):
     """The CPU oracle (C restatement of the reference GLSL, OpenMP over rows) on this host,
     timing whole 1920x1080 frames of the same stream until ~budget_s of wall time is spent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import helpers as H
     cores = min(16, os.cpu_count() or 1)
-    sc = H.oracle_scene(meta, width, height, mesh)
+    sc = H.oracle_scene(meta, width, height, mesh, maps)
     acc = np.zeros((height, width, 4), np.float32)
     frames, t0 = 0, time.perf_counter()
     while True:
@@ -95,10 +95,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-oracle baseline (0 = skip)")
     ap.add_argument("--no-output", action="store_true", help="time pathTracing+copy only (no screenOutput/gather)")
-    ap.add_argument("--workload", choices=("dragon", "bunny"), default="dragon",
+    ap.add_argument("--workload", choices=("dragon", "bunny", "helmet"), default="dragon",
                     help="dragon (default): the model BASELINE.json's metric names, as the 524,288-triangle "
                          "StanfordDragon stand-in (helpers.synthetic_dragon; the .glb is missing from the reference); "
-                         "bunny: BASELINE configs[1] (the reference's StanfordBunny through its own builder)")
+                         "bunny: BASELINE configs[1] (the reference's StanfordBunny through its own builder); "
+                         "helmet: BASELINE configs[2] (DamagedHelmet in the HDRI scene, all four PBR samplers bound "
+                         "to seeded 2048x2048 stand-ins, seeded 2048x1024 equirect in place of the missing .hdr)")
+    ap.add_argument("--size", default=None, help="WxH frame size at N=1 (e.g. 3840x2160 for the 4K configs)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -115,11 +118,14 @@ def main():
     import babylon_pt as bp
     import helpers as H
 
-    meta = H.stream("gltf_bunny_1080p")
+    meta = H.stream("hdri_helmet_320x180" if args.workload == "helmet" else "gltf_bunny_1080p")
     W, Hh = frame_size(world)
+    if args.size:
+        W, Hh = (int(v) for v in args.size.lower().split("x"))
     engine = bp.Engine(local)
     mesh_arrays = H.synthetic_dragon() if args.workload == "dragon" else H.mesh(meta)
     mesh = H.texture_payloads(meta, mesh_arrays)
+    program = meta["scene"]
 
     rt_ptrs, acc_t = None, None
     pad_bands = bp.padded_bands(Hh, world)
@@ -135,6 +141,10 @@ def main():
         # draws, the band gather (RCCL) and rank 0's screenOutput are ordered on one stream
         engine.set_stream(torch.cuda.current_stream().cuda_stream)
     player = bp.StreamPlayer(engine, meta, H.bluenoise(), mesh, W, Hh, rt_ptrs)
+    if args.workload == "helmet":
+        maps = H.synthetic_pbr_maps(2048)
+        for kind, sampler in H.PBR_SAMPLERS.items():
+            player.textures[sampler] = bp.Texture(engine, maps[kind], name=kind)
     engine.resize_canvas(W, Hh)
     engine.set_row_partition(world, rank)
 
@@ -182,7 +192,7 @@ def main():
         step(k)
     barrier_sync()
     elapsed = time.perf_counter() - t0
-    pt_ms, pt_n = engine.timing_end("gltf")
+    pt_ms, pt_n = engine.timing_end(program)
     cp_ms, _ = engine.timing_end("screenCopy")
     out_ms, _ = engine.timing_end("screenOutput")
 
@@ -219,12 +229,14 @@ def main():
     value = paths / elapsed / 1e6
     avg_launch_ms = pt_ms / max(1, pt_n)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
-    workload = "gltf_%s_%dx%d" % ("bunny" if args.workload == "bunny" else "dragon_standin", W, Hh)
+    workload = "%s_%s_%dx%d" % (program, {"bunny": "bunny", "helmet": "helmet_pbr", "dragon": "dragon_standin"}[args.workload],
+                                W, Hh)
     pmc = load_pmc(workload)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     line = {
-        "metric": baseline_metric() if args.workload == "dragon" else
-                  "Mpaths/s + achieved HBM GB/s, StanfordBunny 1080p 1spp (BASELINE configs[1])",
+        "metric": baseline_metric() if args.workload == "dragon" else {
+            "bunny": "Mpaths/s + achieved HBM GB/s, StanfordBunny 1080p 1spp (BASELINE configs[1])",
+            "helmet": "Mpaths/s + achieved HBM GB/s, DamagedHelmet PBR + HDRI env 1080p (BASELINE configs[2])"}[args.workload],
         "value": round(value, 2),
         "unit": "Mpaths/s",
         "n_gpus": world,
@@ -235,10 +247,14 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": ("synthetic: the reference setup script's recorded StanfordBunny uniform stream, continued with fresh "
+        "data": ("synthetic: the reference setup script's recorded %s uniform stream, continued with fresh "
+                 % ("DamagedHelmet/HDRI" if args.workload == "helmet" else "StanfordBunny") +
                  "uRandomVec2 per frame; mesh textures = " +
-                 ("the reference BVH_Fast_Builder output" if args.workload == "bunny" else
-                  "a 524,288-triangle procedural stand-in for the missing StanfordDragon.glb, built by the native builder")),
+                 {"bunny": "the reference BVH_Fast_Builder output",
+                  "helmet": "the reference BVH_Fast_Builder output for DamagedHelmet (HDRI setup script's stream); "
+                            "PBR maps and environment = seeded stand-ins (helpers.synthetic_pbr_maps / synthetic_hdr)",
+                  "dragon": "a 524,288-triangle procedural stand-in for the missing StanfordDragon.glb, built by the "
+                            "native builder"}[args.workload]),
         "config": {"workload": workload, "width": W, "height": Hh, "spp_per_frame": 1, "max_bounces": 6,
                    "triangles": int(mesh_arrays["tri"].shape[0]), "parallelism": "row-bands x%d" % world,
                    "gather": ("per frame: 2-row halo exchange with band neighbours (RCCL P2P), screenOutput "
@@ -248,12 +264,14 @@ def main():
                       "screen_output": round(out_ms / max(1, pt_n), 4)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
-                     "kernel": "pt_trace<%sGLTF>" % ("PAIRS+" if layout == "pairs" else ""),
+                     "kernel": "pt_trace<%s%s%s>" % ("PAIRS+" if layout == "pairs" else "", program.upper(),
+                                                     "+TEX" if args.workload == "helmet" else ""),
                      "algorithmic_bytes_per_launch": int(bytes_per_launch),
                      "counts_per_launch": {k: v / nc for k, v in cnt.items()}},
     }
     if args.cpu_budget > 0:
-        line["cpu_baseline"] = cpu_baseline(meta, 1920, 1080, args.cpu_budget, mesh_arrays) if world == 1 else None
+        line["cpu_baseline"] = (cpu_baseline(meta, 1920, 1080, args.cpu_budget, mesh_arrays,
+                                             maps if args.workload == "helmet" else None) if world == 1 else None)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

@@ -83,8 +83,10 @@ def lib():
 class Scene:
     """Keeps the sampler arrays alive and builds Frame structs from recorded uniforms."""
 
-    def __init__(self, scene, width, height, bluenoise, bvh=None, tri=None, hdr=None):
-        """hdr: the tHDRTexture payload as the setup script uploads it (rows top-first, invertY)."""
+    def __init__(self, scene, width, height, bluenoise, bvh=None, tri=None, hdr=None, maps=None):
+        """hdr: the tHDRTexture payload as the setup script uploads it (rows top-first, invertY).
+        maps: {"albedo"|"bump"|"metallic"|"emissive": RGBA8 (h, w, 4)} in upload row order."""
+        self.maps = {k: np.ascontiguousarray(v, dtype=np.uint8) for k, v in (maps or {}).items()}
         self.scene = scene
         self.hdr = None if hdr is None else np.ascontiguousarray(np.asarray(hdr, dtype=np.float32)[::-1])
         self.width, self.height = width, height
@@ -113,6 +115,10 @@ class Scene:
         if self.hdr is not None:
             f.hdr = self.hdr.ctypes.data
             f.hdrH, f.hdrW = self.hdr.shape[:2]
+        for k, m in self.maps.items():
+            setattr(f, k, m.ctypes.data)
+            setattr(f, k + "H", m.shape[0])
+            setattr(f, k + "W", m.shape[1])
         if self.bvh is not None:
             f.aabb = self.bvh.ctypes.data
             f.aabbTexels = self.bvh.size // 4

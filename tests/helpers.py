@@ -45,13 +45,13 @@ def output_call(frame):
     return next(c for c in frame if c["shader"] == "screenOutputFragmentShader")
 
 
-def oracle_scene(meta, width=None, height=None, mesh_arrays=None):
+def oracle_scene(meta, width=None, height=None, mesh_arrays=None, maps=None):
     import ptoracle as po
     w, h = width or meta["width"], height or meta["height"]
     if meta["scene"] in ("gltf", "hdri"):
         m = mesh_arrays if mesh_arrays is not None else mesh(meta)
         hdr = synthetic_hdr() if meta["scene"] == "hdri" else None
-        return po.Scene(meta["scene"], w, h, bluenoise(), m["bvh"], m["tri"], hdr)
+        return po.Scene(meta["scene"], w, h, bluenoise(), m["bvh"], m["tri"], hdr, maps)
     return po.Scene(meta["scene"], w, h, bluenoise())
 
 
@@ -65,11 +65,11 @@ def with_resolution(uniforms, w, h):
     return u
 
 
-def oracle_replay(meta, frames=None, width=None, height=None, nthreads=0, with_output=False, mesh=None):
+def oracle_replay(meta, frames=None, width=None, height=None, nthreads=0, with_output=False, mesh=None, maps=None):
     """Run the oracle over the recorded stream: returns accumulation after each frame (+ canvas)."""
     import ptoracle as po
     w, h = width or meta["width"], height or meta["height"]
-    sc = oracle_scene(meta, w, h, mesh)
+    sc = oracle_scene(meta, w, h, mesh, maps)
     acc = np.zeros((h, w, 4), np.float32)
     accs, canvases, counters = [], [], []
     for f in meta["frames"][:frames]:
@@ -226,3 +226,32 @@ def po_screen_output(acc, one_over_n, exposure=1.0):
     """The oracle's screenOutput (js/PathTracingCommon.js:19-309) of an RGBA32F frame -> RGBA8."""
     import ptoracle as po
     return po.screen_output(acc, one_over_n, exposure)
+
+
+# the DamagedHelmet's four PBR samplers, by the names its stream binds (js/GLTF_Model_Path_Tracing.js:
+# 749-758 loads them through the glTF loader; the JPEGs stay in the reference tree)
+PBR_SAMPLERS = {"albedo": "Material_MR (Base Color)", "bump": "Material_MR (Normal)",
+                "metallic": "Material_MR (Metallic Roughness)", "emissive": "Material_MR (Emissive)"}
+
+
+def synthetic_pbr_maps(n=256, seed=7):
+    """Seeded stand-ins for the helmet's PBR maps (RGBA8 n x n): smooth albedo, a normal map around
+    +z, metallic-roughness regions below and above the shader's 0.01 thresholds (diffuse, clear
+    coat, metal: .g roughness, .b metal) and a few emissive spots - every material branch of
+    CalculateRadiance's PBR decode is taken."""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:n, 0:n].astype(np.float64) / n
+    def u8(a):
+        return np.clip(np.rint(a * 255.0), 0, 255).astype(np.uint8)
+    alb = np.stack([0.5 + 0.4 * np.sin(6.3 * x), 0.5 + 0.4 * np.cos(4.1 * y), 0.3 + 0.3 * x * y,
+                    np.ones_like(x)], -1)
+    nx, ny = 0.3 * np.sin(9.0 * x + 2.0 * y), 0.3 * np.cos(7.0 * y)
+    nrm = np.stack([nx * 0.5 + 0.5, ny * 0.5 + 0.5, np.sqrt(np.clip(1.0 - nx * nx - ny * ny, 0, 1)) * 0.5 + 0.5,
+                    np.ones_like(x)], -1)
+    zone = (np.floor(x * 4) + np.floor(y * 4)) % 3            # 0 diffuse, 1 clear coat, 2 metal
+    rough = np.where(zone >= 1, 0.2 + 0.6 * y, 0.0)
+    metal = np.where(zone == 2, 0.9, 0.0)
+    mr = np.stack([np.zeros_like(x), rough, metal, np.ones_like(x)], -1)
+    spots = (rng.random((n, n)) < 0.01).astype(np.float64)
+    emi = np.stack([spots, spots * 0.5, spots * 0.2, np.ones_like(x)], -1)
+    return {"albedo": u8(alb), "bump": u8(nrm), "metallic": u8(mr), "emissive": u8(emi)}

@@ -313,6 +313,27 @@ def test_partitioned_screen_output_is_exact(engine, parts):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("name", ["gltf_helmet_320x180", "hdri_helmet_320x180"])
+def test_pbr_maps_bitexact(engine, backend, name):
+    """DamagedHelmet with all four PBR samplers bound (seeded stand-ins for its JPEG maps:
+    helpers.synthetic_pbr_maps): albedo pow 2.2, normal-map perturbation, metallic-roughness
+    material switches and emission, bit for bit against the oracle on every schedule."""
+    import babylon_pt as bp
+    meta = H.stream(name)
+    maps = H.synthetic_pbr_maps()
+    player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, H.mesh(meta)))
+    for kind, sampler in H.PBR_SAMPLERS.items():
+        player.textures[sampler] = bp.Texture(engine, maps[kind], name=kind)
+    got = []
+    for i in range(3):
+        player.play_frame(i)
+        engine.sync()
+        got.append(player.textures["pathTracingRenderTarget"].read())
+    ref, _, _ = H.oracle_replay(meta, 3, maps=maps)
+    for i, (ra, ga) in enumerate(zip(ref, got)):
+        assert _bits_equal(ra, ga), "%s frame %d: %s" % (name, i, _diff_report(ra, ga))
+
+
 def test_deferred_screen_copy_is_observed_exactly(engine):
     """screenCopy is deferred to ride along with the next screenOutput of the same source; reading
     its target first, or drawing anything else first, must still see the copy."""
