@@ -114,6 +114,11 @@ struct TraceArgs {
     uint32_t bvh_pairs_bytes, bvh_leaves_bytes;   // sizes of the two record arrays (buffer descriptors)
     float2* spill;             // megakernel BVH stack levels >= kStackLds: [level][grid lane]
     unsigned spill_stride;
+    // longest-first dispatch (megakernel): order[L] = the logical workgroup launched as workgroup L
+    // (NULL: identity); each wave records its duration in cost[logical] and a log-scale histogram
+    const unsigned* order;
+    unsigned* cost;
+    unsigned* hist;
     Tex8 albedo, bump, metal, emissive;
     // diagnostics
     unsigned long long* counters;   // C_NUM entries, only with counting builds

@@ -27,6 +27,7 @@
 extern "C" {
 hipError_t pt_launch_exhaustive(int op, unsigned long long* bad, hipStream_t s);
 hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s);
+hipError_t pt_launch_order_build(unsigned n, const unsigned* cost, unsigned* hist, unsigned* order, hipStream_t s);
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
@@ -114,6 +115,14 @@ struct pt_ctx {
     size_t gb_pixels = 0;
     unsigned persist_tiles = 4;   // 8x8 wave tiles per wave (PT_PERSIST_TILES)
     unsigned persist_refill = 16; // finished lanes that trigger a refill (PT_PERSIST_REFILL)
+    // longest-first dispatch of the megakernel (PT_LPT=0 disables): cost[] / order[] of the last
+    // path-tracing draw, reused when the next draw has the same grid, target and program
+    bool lpt = true;
+    unsigned* lpt_mem = nullptr;            // cost[n] | order[n] | hist[128]
+    size_t lpt_n = 0, lpt_cap = 0;
+    bool lpt_valid = false;
+    const void* lpt_key_target = nullptr;
+    int lpt_key_prog = -1, lpt_key_part = -1, lpt_key_parts = -1;
     hipEvent_t ev0[kProgSlots] = {}, ev1[kProgSlots] = {};
     bool ev_used[kProgSlots] = {};
     // timing window: per draw event pairs, reused across windows
@@ -561,7 +570,28 @@ int render_trace(pt_effect* fx, pt_texture* target)
                                         c->persist_refill, c->stream));
             HIPCHK(c, pt_launch_finish(&a, &c->gb, gx, gy, c->stream));
         } else {
+            // longest-first: the previous draw's wave durations order this one's workgroups
+            const size_t n = (size_t)gx * 4 * gy;
+            const bool same = c->lpt_valid && c->lpt_n == n && c->lpt_key_target == target && c->lpt_key_prog == fx->prog &&
+                              c->lpt_key_part == c->part && c->lpt_key_parts == c->num_parts;
+            if (c->lpt && !c->counting) {
+                if (c->lpt_cap < n) {
+                    if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
+                    HIPCHK(c, hipMalloc(&c->lpt_mem, (2 * n + 128) * sizeof(unsigned)));
+                    c->lpt_cap = n;
+                    c->lpt_valid = false;
+                    HIPCHK(c, hipMemsetAsync(c->lpt_mem + 2 * n, 0, 128 * sizeof(unsigned), c->stream));   // pt_order_build re-clears it
+                }
+                a.order = same ? c->lpt_mem + c->lpt_cap : nullptr;
+                a.cost = c->lpt_mem;
+                a.hist = c->lpt_mem + 2 * c->lpt_cap;
+            }
             HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, gy, c->stream));
+            if (a.cost) {
+                HIPCHK(c, pt_launch_order_build((unsigned)n, a.cost, a.hist, c->lpt_mem + c->lpt_cap, c->stream));
+                c->lpt_valid = true; c->lpt_n = n; c->lpt_key_target = target; c->lpt_key_prog = fx->prog;
+                c->lpt_key_part = c->part; c->lpt_key_parts = c->num_parts;
+            }
         }
     }
     return end_draw(c, fx->prog);
@@ -709,6 +739,7 @@ pt_ctx* pt_ctx_create(int device, int* err)
     c->device = device;
     c->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (const char* v = std::getenv("PT_PERSIST_TILES")) c->persist_tiles = (unsigned)std::max(1, std::atoi(v));
+    if (const char* v = std::getenv("PT_LPT")) c->lpt = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
@@ -742,6 +773,7 @@ void pt_ctx_destroy(pt_ctx* c)
     }
     if (c->canvas && !c->canvas_external) hipFree(c->canvas);
     if (c->wf_mem) hipFree(c->wf_mem);
+    if (c->lpt_mem) hipFree(c->lpt_mem);
     if (c->mk_spill) hipFree(c->mk_spill);
     if (c->gb_mem) hipFree(c->gb_mem);
     if (c->d_err) hipFree(c->d_err);

@@ -141,6 +141,33 @@ PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_s
 
 PT_D float xorq(float v, int m) { return __shfl_xor(v, m, 64); }
 
+// longest-first dispatch: wave durations (shader clock) in 8 log-scale buckets per octave
+constexpr int kCostBuckets = 128;
+PT_D int costBucket(unsigned dur)
+{
+    const float l = __log2f((float)dur + 1.0f);   // scheduling only, never in the image
+    return min(kCostBuckets - 1, max(0, (int)((l - 8.0f) * 8.0f)));
+}
+
+// Builds order[] for the next frame from this frame's cost[] / hist[] (one block): slots are dealt
+// bucket by bucket, slowest bucket first; within a bucket the order is whatever the LDS atomics
+// give - any permutation renders the same bits, only the schedule changes. Clears hist[].
+__global__ __launch_bounds__(1024) void pt_order_build(unsigned n, const unsigned* cost, unsigned* hist, unsigned* order)
+{
+    __shared__ unsigned off[kCostBuckets];
+    if (threadIdx.x == 0) {
+        unsigned acc = 0;
+        for (int b = kCostBuckets - 1; b >= 0; b--) { off[b] = acc; acc += hist[b]; }
+    }
+    __syncthreads();
+    for (unsigned t = threadIdx.x; t < n; t += blockDim.x) {
+        const unsigned pos = atomicAdd(&off[costBucket(cost[t])], 1u);
+        if (pos < n) order[pos] = t;
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kCostBuckets; b += blockDim.x) hist[b] = 0;
+}
+
 // Workgroups of kTraceBlock lanes. At one wave per workgroup (64, the default) every 8x8 wave tile
 // is its own workgroup: a wave that finishes frees its LDS (stack + G-buffer, 5.5 KB) at once,
 // instead of holding a 4-wave workgroup's 22.5 KB until the slowest of the four (sky next to
@@ -162,27 +189,33 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     __shared__ float lds_gout[8 * kTraceBlock];
     const unsigned tid = threadIdx.x;
     const int lane = tid & 63;
+    const unsigned long long t_start = clock64();
+    // the logical workgroup this launch slot runs: longest-first order from the previous frame's
+    // wave durations (pt_order_build), or the identity
+    const unsigned Lphys = blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned Llog = a.order ? a.order[Lphys] : Lphys;
+    const unsigned bX = Llog % gridDim.x, bY = Llog / gridDim.x;
     // the 8x8 wave tile of this wave inside its 16x16 tile (grid.x = tiles_x * kTraceSub)
     int wave, tx;
     if (kTraceSub == 1) {
         wave = (int)(tid >> 6);
-        tx = (int)blockIdx.x;
+        tx = (int)bX;
     } else if (PT_TILE_GROUPS) {
         // runs of 32 workgroups = 8 tiles x 4 quadrants, quadrant-major: the quadrants of one tile
         // are workgroups 8 apart, which the dispatcher deals to the same XCD (one L2), while
         // neighbouring tiles still go round-robin over the XCDs (a short last run keeps the map a
         // bijection)
-        const unsigned g = blockIdx.x >> 5, r = blockIdx.x & 31u;
+        const unsigned g = bX >> 5, r = bX & 31u;
         const unsigned T = min(8u, gridDim.x / 4u - g * 8u);
         tx = (int)(g * 8u + r % T);
         wave = (int)(r / T);
     } else {
-        wave = (int)(blockIdx.x & 3u);
-        tx = (int)(blockIdx.x >> 2);
+        wave = (int)(bX & 3u);
+        tx = (int)(bX >> 2);
     }
     const int lx = (lane & 1) | ((lane >> 1) & 6);
     const int ly = ((lane >> 1) & 1) | ((lane >> 3) & 6);
-    const int band = blockIdx.y * a.num_parts + a.part;         // global 16-row band of this block
+    const int band = (int)bY * a.num_parts + a.part;            // global 16-row band of this block
     const int px = tx * kTile + (wave & 1) * 8 + lx;
     const int py = band * kTile + (wave >> 1) * 8 + ly;
     // stack levels >= kStackLds: a global slab [level][lane of the grid] (a private array would be
@@ -230,6 +263,11 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         atomicAdd(&C[C_RGBA8], (unsigned long long)(cnt.tap + 1));
         atomicAdd(&C[C_OVERFLOW], (unsigned long long)cnt.ovf);
         atomicAdd(&C[C_HDR], (unsigned long long)cnt.hdr);
+    }
+    if (a.cost && tid == 0) {   // this wave's duration, for the next frame's longest-first order
+        const unsigned dur = (unsigned)min(clock64() - t_start, 0xffffffffull);
+        a.cost[Llog] = dur;
+        atomicAdd(&a.hist[costBucket(dur)], 1u);
     }
     if (px >= a.width || py >= a.height) return;   // quad helper outside the target
 
@@ -611,6 +649,12 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
     default: return hipErrorInvalidValue;
     }
 #undef PT_CASE
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_order_build(unsigned n, const unsigned* cost, unsigned* hist, unsigned* order, hipStream_t s)
+{
+    hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(1024), 0, s, n, cost, hist, order);
     return hipGetLastError();
 }
 
