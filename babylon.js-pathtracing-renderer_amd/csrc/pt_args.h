@@ -114,11 +114,10 @@ struct TraceArgs {
     uint32_t bvh_pairs_bytes, bvh_leaves_bytes;   // sizes of the two record arrays (buffer descriptors)
     float2* spill;             // megakernel BVH stack levels >= kStackLds: [level][grid lane]
     unsigned spill_stride;
-    // longest-first dispatch (megakernel): order[L] = the logical workgroup launched as workgroup L
-    // (NULL: identity); each wave records its duration in cost[logical] and a log-scale histogram
+    // longest-first dispatch (megakernel): order[slot] = the 16x16 tile dealt to tile slot `slot`
+    // (NULL: row-major); each wave records its duration in cost[tile * 4 + quadrant]
     const unsigned* order;
     unsigned* cost;
-    unsigned* hist;
     Tex8 albedo, bump, metal, emissive;
     // diagnostics
     unsigned long long* counters;   // C_NUM entries, only with counting builds

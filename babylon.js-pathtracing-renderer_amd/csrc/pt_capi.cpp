@@ -27,7 +27,7 @@
 extern "C" {
 hipError_t pt_launch_exhaustive(int op, unsigned long long* bad, hipStream_t s);
 hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s);
-hipError_t pt_launch_order_build(unsigned n, const unsigned* cost, unsigned* hist, unsigned* order, hipStream_t s);
+hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, hipStream_t s);
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
@@ -118,7 +118,7 @@ struct pt_ctx {
     // longest-first dispatch of the megakernel (PT_LPT=0 disables): cost[] / order[] of the last
     // path-tracing draw, reused when the next draw has the same grid, target and program
     bool lpt = true;
-    unsigned* lpt_mem = nullptr;            // cost[n] | order[n] | hist[128]
+    unsigned* lpt_mem = nullptr;            // cost[4 * ntiles] | order[ntiles]
     size_t lpt_n = 0, lpt_cap = 0;
     bool lpt_valid = false;
     const void* lpt_key_target = nullptr;
@@ -571,24 +571,22 @@ int render_trace(pt_effect* fx, pt_texture* target)
             HIPCHK(c, pt_launch_finish(&a, &c->gb, gx, gy, c->stream));
         } else {
             // longest-first: the previous draw's wave durations order this one's workgroups
-            const size_t n = (size_t)gx * 4 * gy;
+            const size_t n = (size_t)gx * gy;   // 16x16 tiles
             const bool same = c->lpt_valid && c->lpt_n == n && c->lpt_key_target == target && c->lpt_key_prog == fx->prog &&
                               c->lpt_key_part == c->part && c->lpt_key_parts == c->num_parts;
             if (c->lpt && !c->counting) {
                 if (c->lpt_cap < n) {
                     if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
-                    HIPCHK(c, hipMalloc(&c->lpt_mem, (2 * n + 128) * sizeof(unsigned)));
+                    HIPCHK(c, hipMalloc(&c->lpt_mem, 5 * n * sizeof(unsigned)));
                     c->lpt_cap = n;
                     c->lpt_valid = false;
-                    HIPCHK(c, hipMemsetAsync(c->lpt_mem + 2 * n, 0, 128 * sizeof(unsigned), c->stream));   // pt_order_build re-clears it
                 }
-                a.order = same ? c->lpt_mem + c->lpt_cap : nullptr;
+                a.order = same ? c->lpt_mem + 4 * c->lpt_cap : nullptr;
                 a.cost = c->lpt_mem;
-                a.hist = c->lpt_mem + 2 * c->lpt_cap;
             }
             HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, gy, c->stream));
             if (a.cost) {
-                HIPCHK(c, pt_launch_order_build((unsigned)n, a.cost, a.hist, c->lpt_mem + c->lpt_cap, c->stream));
+                HIPCHK(c, pt_launch_order_build((unsigned)n, a.cost, c->lpt_mem + 4 * c->lpt_cap, c->stream));
                 c->lpt_valid = true; c->lpt_n = n; c->lpt_key_target = target; c->lpt_key_prog = fx->prog;
                 c->lpt_key_part = c->part; c->lpt_key_parts = c->num_parts;
             }

@@ -149,23 +149,30 @@ PT_D int costBucket(unsigned dur)
     return min(kCostBuckets - 1, max(0, (int)((l - 8.0f) * 8.0f)));
 }
 
-// Builds order[] for the next frame from this frame's cost[] / hist[] (one block): slots are dealt
+// Builds order[] (a permutation of the ntiles 16x16 tiles) for the next frame from this frame's
+// cost[tile*4 + quadrant] (one block): a tile weighs as its slowest quadrant wave; tiles are dealt
 // bucket by bucket, slowest bucket first; within a bucket the order is whatever the LDS atomics
-// give - any permutation renders the same bits, only the schedule changes. Clears hist[].
-__global__ __launch_bounds__(1024) void pt_order_build(unsigned n, const unsigned* cost, unsigned* hist, unsigned* order)
+// give - any permutation renders the same bits, only the schedule changes.
+__global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const unsigned* cost, unsigned* order)
 {
-    __shared__ unsigned off[kCostBuckets];
+    __shared__ unsigned cnt[kCostBuckets];
+    for (int b = threadIdx.x; b < kCostBuckets; b += blockDim.x) cnt[b] = 0;
+    __syncthreads();
+    auto tileBucket = [&](unsigned t) {
+        const unsigned* c = cost + 4u * t;
+        return costBucket(max(max(c[0], c[1]), max(c[2], c[3])));
+    };
+    for (unsigned t = threadIdx.x; t < ntiles; t += blockDim.x) atomicAdd(&cnt[tileBucket(t)], 1u);
+    __syncthreads();
     if (threadIdx.x == 0) {
         unsigned acc = 0;
-        for (int b = kCostBuckets - 1; b >= 0; b--) { off[b] = acc; acc += hist[b]; }
+        for (int b = kCostBuckets - 1; b >= 0; b--) { const unsigned v = cnt[b]; cnt[b] = acc; acc += v; }
     }
     __syncthreads();
-    for (unsigned t = threadIdx.x; t < n; t += blockDim.x) {
-        const unsigned pos = atomicAdd(&off[costBucket(cost[t])], 1u);
-        if (pos < n) order[pos] = t;
+    for (unsigned t = threadIdx.x; t < ntiles; t += blockDim.x) {
+        const unsigned pos = atomicAdd(&cnt[tileBucket(t)], 1u);
+        if (pos < ntiles) order[pos] = t;
     }
-    __syncthreads();
-    for (int b = threadIdx.x; b < kCostBuckets; b += blockDim.x) hist[b] = 0;
 }
 
 // Workgroups of kTraceBlock lanes. At one wave per workgroup (64, the default) every 8x8 wave tile
@@ -190,28 +197,33 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     const unsigned tid = threadIdx.x;
     const int lane = tid & 63;
     const unsigned long long t_start = clock64();
-    // the logical workgroup this launch slot runs: longest-first order from the previous frame's
-    // wave durations (pt_order_build), or the identity
-    const unsigned Lphys = blockIdx.y * gridDim.x + blockIdx.x;
-    const unsigned Llog = a.order ? a.order[Lphys] : Lphys;
-    const unsigned bX = Llog % gridDim.x, bY = Llog / gridDim.x;
-    // the 8x8 wave tile of this wave inside its 16x16 tile (grid.x = tiles_x * kTraceSub)
+    // the 8x8 wave tile of this wave inside its 16x16 tile (grid = tiles_x * kTraceSub x bands)
     int wave, tx;
-    if (kTraceSub == 1) {
-        wave = (int)(tid >> 6);
-        tx = (int)bX;
-    } else if (PT_TILE_GROUPS) {
-        // runs of 32 workgroups = 8 tiles x 4 quadrants, quadrant-major: the quadrants of one tile
-        // are workgroups 8 apart, which the dispatcher deals to the same XCD (one L2), while
-        // neighbouring tiles still go round-robin over the XCDs (a short last run keeps the map a
-        // bijection)
-        const unsigned g = bX >> 5, r = bX & 31u;
-        const unsigned T = min(8u, gridDim.x / 4u - g * 8u);
-        tx = (int)(g * 8u + r % T);
+    unsigned bY, costIdx = ~0u;
+    if (kTraceSub == 4 && PT_TILE_GROUPS) {
+        // launch slots in runs of 32 workgroups = 8 tiles x 4 quadrants, quadrant-major: the
+        // quadrants of one tile are workgroups 8 apart, which the dispatcher deals to the same XCD
+        // (one L2), while the runs' tiles still go round-robin over the XCDs (a short last run keeps
+        // the map a bijection). The tiles come in longest-first order (the previous frame's costs,
+        // pt_order_build) when a.order is set, else row-major.
+        const unsigned tiles_x = gridDim.x / 4u, ntiles = tiles_x * gridDim.y;
+        const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
+        const unsigned g = L >> 5, r = L & 31u;
+        const unsigned T = min(8u, ntiles - g * 8u);
+        const unsigned slot = g * 8u + r % T;
+        const unsigned tile = a.order ? a.order[slot] : slot;
         wave = (int)(r / T);
+        tx = (int)(tile % tiles_x);
+        bY = tile / tiles_x;
+        costIdx = tile * 4u + (unsigned)wave;
+    } else if (kTraceSub == 1) {
+        wave = (int)(tid >> 6);
+        tx = (int)blockIdx.x;
+        bY = blockIdx.y;
     } else {
-        wave = (int)(bX & 3u);
-        tx = (int)(bX >> 2);
+        wave = (int)(blockIdx.x & 3u);
+        tx = (int)(blockIdx.x >> 2);
+        bY = blockIdx.y;
     }
     const int lx = (lane & 1) | ((lane >> 1) & 6);
     const int ly = ((lane >> 1) & 1) | ((lane >> 3) & 6);
@@ -264,11 +276,8 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         atomicAdd(&C[C_OVERFLOW], (unsigned long long)cnt.ovf);
         atomicAdd(&C[C_HDR], (unsigned long long)cnt.hdr);
     }
-    if (a.cost && tid == 0) {   // this wave's duration, for the next frame's longest-first order
-        const unsigned dur = (unsigned)min(clock64() - t_start, 0xffffffffull);
-        a.cost[Llog] = dur;
-        atomicAdd(&a.hist[costBucket(dur)], 1u);
-    }
+    if (a.cost && costIdx != ~0u && tid == 0)   // this wave's duration, for the next frame's order
+        a.cost[costIdx] = (unsigned)min(clock64() - t_start, 0xffffffffull);
     if (px >= a.width || py >= a.height) return;   // quad helper outside the target
 
     // ---- progressive accumulation (js/PathTracingCommon.js:1326-1357)
@@ -652,9 +661,9 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
     return hipGetLastError();
 }
 
-hipError_t pt_launch_order_build(unsigned n, const unsigned* cost, unsigned* hist, unsigned* order, hipStream_t s)
+hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, hipStream_t s)
 {
-    hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(1024), 0, s, n, cost, hist, order);
+    hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(1024), 0, s, ntiles, cost, order);
     return hipGetLastError();
 }
 
