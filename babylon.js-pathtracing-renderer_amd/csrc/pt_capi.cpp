@@ -820,9 +820,9 @@ int pt_canvas_wrap(pt_ctx* c, int w, int h, void* ptr)
 {
     if (!c || w <= 0 || h <= 0 || !ptr) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    if (c->canvas) {
+    if (c->canvas && !c->canvas_external) {   // switching between wrapped canvases needs no sync
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (!c->canvas_external) HIPCHK(c, hipFree(c->canvas));
+        HIPCHK(c, hipFree(c->canvas));
     }
     c->canvas = (uchar4*)ptr;
     c->canvas_external = true;

@@ -555,6 +555,58 @@ def exchange_halos(dist, acc_padded, world, rank, bufs):
     bv[:, hi, 0:2].copy_(bufs["recv_top"])              # rank r+1's top rows, over our bands
 
 
+class PipelinedBandGather:
+    """Per-frame gather of the ranks' RGBA8 bands to rank 0, overlapped with the next frame: two
+    band-padded canvases alternate; frame k renders into target(), submit() starts its gather
+    (async), and the gather that last used a buffer is waited for (and, on rank 0, assembled into
+    a full frame) only when that buffer comes round again, two frames later, or at drain().
+    On rank 0 `frames` collects (frame index, assembled canvas) in order when keep=True."""
+
+    def __init__(self, dist, world, rank, rows, width, device, keep=False):
+        import torch
+        self.dist, self.world, self.rank, self.keep = dist, world, rank, keep
+        self.canvas = [torch.zeros((rows, width, 4), dtype=torch.uint8, device=device) for _ in range(2)]
+        self.send = [torch.zeros((rows // (BAND * world), BAND, width, 4), dtype=torch.uint8, device=device)
+                     for _ in range(2)]
+        self.glist = [[torch.empty_like(self.send[b]) for _ in range(world)] if rank == 0 else None for b in range(2)]
+        self.full = [torch.zeros_like(self.canvas[0]) if rank == 0 else None for _ in range(2)]
+        self.work = [None, None]
+        self.frame_of = [None, None]
+        self.k = 0
+        self.frames = []
+
+    def target(self):
+        """The canvas tensor to render frame k into (its previous gather, two frames ago, is done)."""
+        b = self.k % 2
+        self._finish(b)
+        return self.canvas[b]
+
+    def submit(self):
+        """Start gathering frame k's bands (after its screenOutput was enqueued on this stream)."""
+        b = self.k % 2
+        self.send[b].copy_(band_view(self.canvas[b], self.world)[:, self.rank])
+        self.work[b] = self.dist.gather(self.send[b], self.glist[b], dst=0, async_op=True)
+        self.frame_of[b] = self.k
+        self.k += 1
+
+    def _finish(self, b):
+        if self.work[b] is None:
+            return
+        self.work[b].wait()
+        self.work[b] = None
+        if self.rank == 0:
+            fv = band_view(self.full[b], self.world)
+            for r in range(self.world):
+                fv[:, r].copy_(self.glist[b][r])
+            if self.keep:
+                self.frames.append((self.frame_of[b], self.full[b].clone()))
+
+    def drain(self):
+        """Complete every outstanding gather, oldest first."""
+        for b in sorted((b for b in range(2) if self.work[b] is not None), key=lambda b: self.frame_of[b]):
+            self._finish(b)
+
+
 def halo_buffers(acc_padded, world):
     """Send/receive buffers for exchange_halos (same device and dtype as the accumulation)."""
     import torch

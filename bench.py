@@ -151,14 +151,11 @@ def main():
     if dist is not None:
         import torch
         # the canvas is the first H rows of a band-padded uint8 tensor: screenOutput writes this
-        # rank's bands there, and they are gathered to rank 0's full canvas
-        canvas_t = torch.zeros((pad_bands * 16, W, 4), dtype=torch.uint8, device="cuda")
-        engine.canvas_wrap(W, Hh, canvas_t.data_ptr())
+        # rank's bands there, and they are gathered to rank 0's full canvas - asynchronously, two
+        # canvases alternating, so frame k's gather overlaps frame k+1's path tracing
         engine.set_output_partition(True)
         halo = bp.halo_buffers(acc_t, world)
-        full_t = torch.zeros((pad_bands * 16, W, 4), dtype=torch.uint8, device="cuda") if rank == 0 else None
-        send_t = torch.zeros((pad_bands // world, 16, W, 4), dtype=torch.uint8, device="cuda")
-        gather_list = [torch.empty_like(send_t) for _ in range(world)] if rank == 0 else None
+        gather = bp.PipelinedBandGather(dist, world, rank, pad_bands * 16, W, "cuda")
 
     def step(k):
         frame = player.synth_frame(k)
@@ -170,13 +167,16 @@ def main():
         if dist is None:
             player.play_call(out_call)
             return
-        # halo rows from the band neighbours (RCCL P2P), screenOutput of this rank's bands, RCCL
-        # gather of the RGBA8 bands to rank 0 (all on the current stream: no host sync in a frame)
+        # halo rows from the band neighbours (RCCL P2P), screenOutput of this rank's bands, async
+        # RCCL gather of the RGBA8 bands to rank 0 (no host sync in a frame)
         bp.exchange_halos(dist, acc_t, world, rank, halo)
+        engine.canvas_wrap(W, Hh, gather.target().data_ptr())
         player.play_call(out_call)
-        bp.gather_bands(dist, canvas_t, world, rank, send_t, gather_list, full_t)
+        gather.submit()
 
     def barrier_sync():
+        if dist is not None:
+            gather.drain()   # every frame's gather is part of the timed work
         engine.sync()
         if dist is not None:
             import torch
@@ -258,7 +258,8 @@ def main():
         "config": {"workload": workload, "width": W, "height": Hh, "spp_per_frame": 1, "max_bounces": 6,
                    "triangles": int(mesh_arrays["tri"].shape[0]), "parallelism": "row-bands x%d" % world,
                    "gather": ("per frame: 2-row halo exchange with band neighbours (RCCL P2P), screenOutput "
-                              "of own bands, RCCL gather of RGBA8 bands to rank 0") if world > 1 else None},
+                              "of own bands, async RCCL gather of RGBA8 bands to rank 0 overlapping the next "
+                              "frame") if world > 1 else None},
         "pathtrace_mpaths_per_s": round(W * Hh / world / (avg_launch_ms * 1e-3) / 1e6 * world, 2),
         "kernel_ms": {"pathtrace": round(avg_launch_ms, 4), "screen_copy": round(cp_ms / max(1, pt_n), 4),
                       "screen_output": round(out_ms / max(1, pt_n), 4)},

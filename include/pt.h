@@ -135,7 +135,8 @@ int pt_set_row_partition(pt_ctx* ctx, int num_parts, int part);
 int pt_set_output_partition(pt_ctx* ctx, int enable);
 /* The canvas over caller-owned device memory: width*height RGBA8 texels, rows bottom-up (e.g. a
  * torch tensor that RCCL gathers from). Not freed by the context; pt_canvas_resize replaces it
- * with context-owned memory again. */
+ * with context-owned memory again. Re-wrapping another caller buffer is a host-side switch (no
+ * synchronisation), so a caller can alternate between two canvases frame by frame. */
 int pt_canvas_wrap(pt_ctx* ctx, int width, int height, void* device_ptr);
 /* Path-tracing backend of this context: PT_BACKEND_MEGAKERNEL (default: one kernel, one lane per
  * path), PT_BACKEND_WAVEFRONT (per-segment kernels over compacted path queues) or

@@ -107,3 +107,41 @@ def test_partitioned_output_with_halo_exchange(tmp_path, world):
     ref, _, _ = H.oracle_replay(meta, 1, width=w, height=h)
     want = H.po_screen_output(ref[0], 1.0)
     assert np.array_equal(got, want)
+
+
+def _worker_pipeline(rank, world, port, w, h, frames, out_path):
+    """PipelinedBandGather over gloo: each rank writes frame-dependent values into its own bands
+    of the canvas it is handed; rank 0 must assemble every frame, in order, exactly."""
+    import babylon_pt as bp
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pad = bp.padded_bands(h, world)
+        pipe = bp.PipelinedBandGather(dist, world, rank, pad * 16, w, "cpu", keep=True)
+        mine = bp.owned_rows(h, world, rank)
+        for k in range(frames):
+            canvas = pipe.target()
+            canvas.zero_()
+            canvas[mine] = torch.tensor([k % 251, rank, 7, 255], dtype=torch.uint8)
+            pipe.submit()
+        pipe.drain()
+        if rank == 0:
+            np.save(out_path, np.stack([f[:h].numpy() for _, f in pipe.frames]))
+            assert [i for i, _ in pipe.frames] == list(range(frames))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipelined_band_gather(tmp_path, world):
+    import babylon_pt as bp
+    w, h, frames = 40, 72, 5
+    out = str(tmp_path / "frames.npy")
+    mp.spawn(_worker_pipeline, args=(world, _free_port(), w, h, frames, out), nprocs=world, join=True)
+    got = np.load(out)
+    for k in range(frames):
+        want = np.zeros((h, w, 4), np.uint8)
+        for r in range(world):
+            want[bp.owned_rows(h, world, r)] = [k % 251, r, 7, 255]
+        assert np.array_equal(got[k], want), k
