@@ -578,6 +578,7 @@ int render_trace(pt_effect* fx, pt_texture* target)
                 if (c->lpt_cap < n) {
                     if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
                     HIPCHK(c, hipMalloc(&c->lpt_mem, 5 * n * sizeof(unsigned)));
+                    HIPCHK(c, hipMemsetAsync(c->lpt_mem, 0, 4 * n * sizeof(unsigned), c->stream));
                     c->lpt_cap = n;
                     c->lpt_valid = false;
                 }
