@@ -49,10 +49,13 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, bool pair
 // (measured with one-wave workgroups and 7 LDS stack levels: 6 waves (80 VGPRs, 12 B of spill)
 // ~1-2 % ahead of 7 (72 VGPRs) and of 8 with 6 levels; 5 waves lose 6 %; 4-6 or 9-12 LDS levels
 // lose at 6 waves; the reference walk loses above 4)
+#ifndef PT_MINWAVES_TEX
+#define PT_MINWAVES_TEX 2
+#endif
 #ifndef PT_MINWAVES_PAIRS
 #define PT_MINWAVES_PAIRS 6
 #endif
-template <int P> constexpr int kMinWaves = kHasTex<P> ? 2 : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
+template <int P> constexpr int kMinWaves = kHasTex<P> ? PT_MINWAVES_TEX : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
 
 // ------------------------------------------------------------------------------ per-lane state
 struct Path {
