@@ -101,7 +101,9 @@ def main():
                          "bunny: BASELINE configs[1] (the reference's StanfordBunny through its own builder); "
                          "helmet: BASELINE configs[2] (DamagedHelmet in the HDRI scene, all four PBR samplers bound "
                          "to seeded 2048x2048 stand-ins, seeded 2048x1024 equirect in place of the missing .hdr)")
-    ap.add_argument("--size", default=None, help="WxH frame size at N=1 (e.g. 3840x2160 for the 4K configs)")
+    ap.add_argument("--size", default=None,
+                    help="WxH frame size (e.g. 3840x2160 for the 4K configs); at N > 1 the same frame is split over "
+                         "the GPUs (strong scaling, BASELINE configs[3]: --gpus 8 --size 3840x2160)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,7 +246,8 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        # weak: N GPUs render N x 2.07 MP (frame_size); --size fixes the frame, split over the N GPUs
+        "scaling": "strong" if args.size and world > 1 else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": ("synthetic: the reference setup script's recorded %s uniform stream, continued with fresh "
