@@ -157,11 +157,26 @@ function wrapBuilder() {
   } else {
     frames = [];
   }
-  // recorded frames: the uniform stream the setup script pushes from here on
-  while (frames.length < FRAMES) frame();
+  // recorded frames: the uniform stream the setup script pushes from here on. PT_CONTROLS (JSON,
+  // one entry per recorded frame) drives the script's own input state before that frame, as its
+  // event handlers would: {down: [key names], up: [...], wheel: +1|-1, rot: [pitch, yaw]}
+  // (KeyboardState via onKeyDown/onKeyUp, increaseFOV/decreaseFOV via onMouseWheel, and
+  // camera.rotation as the pointer-lock mouse input leaves it)
+  const controls = process.env.PT_CONTROLS ? JSON.parse(process.env.PT_CONTROLS) : null;
+  const applyControls = (c) => {
+    if (!c) return;
+    const ks = vm.runInThisContext('KeyboardState');
+    for (const k of c.down || []) ks[k] = true;
+    for (const k of c.up || []) ks[k] = false;
+    if (c.wheel > 0) vm.runInThisContext('increaseFOV = true');
+    if (c.wheel < 0) vm.runInThisContext('decreaseFOV = true');
+    if (c.rot) vm.runInThisContext('camera').rotation.set(c.rot[0], c.rot[1], 0);
+  };
+  while (frames.length < FRAMES) { if (controls) applyControls(controls[frames.length]); frame(); }
   frames = frames.slice(0, FRAMES);
   const hasMesh = scene === 'gltf' || scene === 'hdri';
   const meta = { scene, width: W, height: H, seed: Number(SEED), model: hasMesh ? MODEL : null, frames };
+  if (controls) meta.controls = controls;
   if (hasMesh) {
     const tris = vm.runInThisContext('total_number_of_triangles');
     const mt = meshTextures(), n = mt.length;

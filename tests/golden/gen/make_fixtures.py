@@ -15,6 +15,8 @@ outputs as small fixtures:
   browser_env.js syntheticHDR (== tests/helpers.py synthetic_hdr; the reference's .hdr files are
   not in it); the stream records that texture's sha256, the payload itself is regenerated.
 
+  tests/golden/controls_<scene>.json  the same stream with the render loop's inputs driven
+
 usage: python tests/golden/gen/make_fixtures.py [stream names | mesh_<model fixture> ...]   (default: all)
 """
 import sys
@@ -44,6 +46,41 @@ STREAMS = [
     ("hdri_helmet_320x180", "hdri", 320, 180, 3, 13, "Damaged Helmet"),
     ("quadric_256", "quadric", 256, 256, 3, 17, None),
 ]
+# the Cornell render loop driven through its own input state (make_fixtures.js PT_CONTROLS): WASD/QE
+# flight, opposing keys, mouse-wheel FOV, a pointer-lock camera rotation, focus distance and
+# aperture keys (aperture clamped at 0), then still frames. Pins python/pt_controls.py.
+def _controls_script():
+    c = [dict() for _ in range(40)]
+    c[2] = {"down": ["w"]}
+    c[5] = {"up": ["w"]}
+    c[6] = {"down": ["d"]}
+    c[7] = {"down": ["e"]}
+    c[9] = {"up": ["d", "e"]}
+    c[10] = {"down": ["a", "d"]}
+    c[11] = {"up": ["a", "d"]}
+    c[12] = {"wheel": 1}
+    c[13] = {"wheel": 1}
+    c[14] = {"wheel": -1}
+    c[15] = {"rot": [0.1, 0.3]}
+    c[16] = {"down": ["w"]}
+    c[18] = {"up": ["w"]}
+    c[19] = {"down": ["s", "q"]}
+    c[21] = {"up": ["s", "q"]}
+    c[22] = {"down": ["equals"]}
+    c[24] = {"up": ["equals"]}
+    c[25] = {"down": ["dash"]}
+    c[26] = {"up": ["dash"]}
+    c[27] = {"down": ["rightbracket"]}
+    c[29] = {"up": ["rightbracket"], "rot": [-0.25, -0.7]}
+    c[30] = {"down": ["leftbracket", "a"]}
+    c[33] = {"up": ["leftbracket", "a"]}
+    return c
+
+
+CONTROL_STREAMS = [
+    ("controls_cornell", "cornell", 96, 64, 40, 19, None, _controls_script()),
+]
+
 # models of the reference's models/ outside the setup script's menu, loaded through the script's
 # own loadModel(): only their mesh payloads are kept (they pin the asset-pipeline restatement,
 # python/pt_assets.py, on multi-mesh merges and mixed vertex-attribute sets)
@@ -53,12 +90,15 @@ MODEL_FIXTURES = [
 ]
 
 
-def run_stream(name, scene, w, h, frames, seed, model, tmp):
+def run_stream(name, scene, w, h, frames, seed, model, tmp, controls=None):
     out = os.path.join(tmp, name)
     cmd = ["node", os.path.join(HERE, "make_fixtures.js"), scene, out, str(w), str(h), str(frames), str(seed)]
     if model:
         cmd.append(model)
-    subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL)
+    env = dict(os.environ)
+    if controls is not None:
+        env["PT_CONTROLS"] = json.dumps(controls)
+    subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, env=env)
     with open(os.path.join(out, "frames.json")) as f:
         meta = json.load(f)
     mesh = None
@@ -153,6 +193,13 @@ def main():
             with open(os.path.join(GOLD, name + ".json"), "w") as f:
                 json.dump(meta, f, indent=0)
             manifest[name] = {"scene": scene, "width": w, "height": h, "frames": frames, "seed": seed, "model": model}
+        for name, scene, w, h, frames, seed, model, controls in CONTROL_STREAMS:
+            if only and name not in only:
+                continue
+            meta, _ = run_stream(name, scene, w, h, frames, seed, model, tmp, controls)
+            with open(os.path.join(GOLD, name + ".json"), "w") as f:
+                json.dump(meta, f, indent=0)
+            manifest[name] = {"scene": scene, "width": w, "height": h, "frames": frames, "seed": seed, "controls": True}
         for key, model in MODEL_FIXTURES:
             if only and "mesh_" + key not in only:
                 continue

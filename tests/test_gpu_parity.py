@@ -420,3 +420,38 @@ def test_errors_are_codes_not_crashes(engine):
     with pytest.raises(bp.PtError, match="PT_ERR_STATE"):
         bp.EffectRenderer(engine).render(pt, rt)      # samplers unbound
     engine.sync()
+
+
+def test_interactive_loop_bitexact(engine):
+    """The Python host's render loop (pt_controls.RenderLoop) driving the boundary live - its
+    uniforms over the first frame's call template - renders what the oracle renders from the
+    reference's own recorded stream with the same inputs (tests/golden/controls_cornell.json:
+    flight, rotation, FOV, focus, aperture, then accumulation)."""
+    import babylon_pt as bp
+    import pt_controls as pc
+    meta = H.stream("controls_cornell")
+    nf = 24
+    ref_acc, ref_can, _ = H.oracle_replay(meta, nf, with_output=True)
+    rng = iter(bp.splitmix64_uniforms(meta["seed"], 2 * nf))
+    loop = pc.RenderLoop(meta["width"], meta["height"], random=lambda: next(rng))
+    player = bp.StreamPlayer(engine, meta, H.bluenoise())
+    engine.resize_canvas(player.width, player.height)
+    template = meta["frames"][0]
+    for i in range(nf):
+        c = meta["controls"][i]
+        for k in c.get("down", []):
+            loop.key_down(k)
+        for k in c.get("up", []):
+            loop.key_up(k)
+        if c.get("wheel"):
+            loop.wheel(c["wheel"])
+        if c.get("rot"):
+            loop.camera.rotation = [float(c["rot"][0]), float(c["rot"][1]), 0.0]
+        u = loop.step()
+        for call in template:
+            player.play_call(call, uniform_override=u)
+        engine.sync()
+        ga = player.textures["pathTracingRenderTarget"].read()
+        gc = engine.read_canvas(player.width, player.height)
+        assert _bits_equal(ref_acc[i], ga), "frame %d accumulation: %s" % (i, _diff_report(ref_acc[i], ga))
+        assert _bits_equal(ref_can[i], gc), "frame %d canvas: %s" % (i, _diff_report(ref_can[i], gc))
