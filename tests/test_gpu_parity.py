@@ -228,6 +228,7 @@ def test_dragon_standin_1080p_bitexact_and_counters(engine, backend):
     engine.reset_counters()
     try:
         player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, mesh))
+        engine.resize_canvas(meta["width"], meta["height"])
         got_acc, got_can = [], []
         for i in range(2):
             player.play_frame(i)
