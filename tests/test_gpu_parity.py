@@ -96,11 +96,11 @@ def test_fast_sqrt_is_ieee_on_every_input(engine):
     assert engine.math_exhaustive(1) == 0
 
 
-def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1, split_output=False):
+def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1, split_output=False, mesh=None):
     import babylon_pt as bp
     m = None
     if meta["scene"] in ("gltf", "hdri"):
-        m = H.texture_payloads(meta, H.mesh(meta))
+        m = H.texture_payloads(meta, mesh if mesh is not None else H.mesh(meta))
     player = bp.StreamPlayer(engine, meta, H.bluenoise(), m, width, height)
     accs, canvases = [], []
     w, h = player.width, player.height
@@ -456,3 +456,19 @@ def test_interactive_loop_bitexact(engine):
         gc = engine.read_canvas(player.width, player.height)
         assert _bits_equal(ref_acc[i], ga), "frame %d accumulation: %s" % (i, _diff_report(ref_acc[i], ga))
         assert _bits_equal(ref_can[i], gc), "frame %d canvas: %s" % (i, _diff_report(ref_can[i], gc))
+
+
+def test_dragon_4k_eight_bands_bitexact(engine):
+    """BASELINE configs[3] on one GPU: the 524,288-triangle dragon stand-in at 3840x2160 under the
+    bunny stream's camera, rendered as 8 band partitions (the rows each of 8 ranks owns), copied
+    full-frame and output band by band (pt_set_output_partition) - bit-exact with the oracle's
+    whole-frame render, accumulation and canvas, over 2 frames (history blend included)."""
+    meta = H.stream("gltf_bunny_1080p")
+    mesh = H.synthetic_dragon()
+    W, Hh = 3840, 2160
+    ref_acc, ref_can, _ = H.oracle_replay(meta, 2, width=W, height=Hh, with_output=True, mesh=mesh)
+    got_acc, got_can, _ = _replay_gpu(engine, meta, 2, W, Hh, parts=8, split_output=True, mesh=mesh)
+    for i, (ra, ga, rc, gc) in enumerate(zip(ref_acc, got_acc, ref_can, got_can)):
+        assert ra.shape == (Hh, W, 4)
+        assert _bits_equal(ra, ga), "frame %d accumulation: %s" % (i, _diff_report(ra, ga))
+        assert _bits_equal(rc, gc), "frame %d canvas: %s" % (i, _diff_report(rc, gc))
