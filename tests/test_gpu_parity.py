@@ -472,3 +472,29 @@ def test_dragon_4k_eight_bands_bitexact(engine):
         assert ra.shape == (Hh, W, 4)
         assert _bits_equal(ra, ga), "frame %d accumulation: %s" % (i, _diff_report(ra, ga))
         assert _bits_equal(rc, gc), "frame %d canvas: %s" % (i, _diff_report(rc, gc))
+
+
+@pytest.mark.parametrize("n", [4, 200, 201, 4999, 5001, 1024 * 64])
+def test_screen_output_sample_count_branches(engine, n):
+    """screenOutput at the sample counts a converged run reaches (BASELINE configs[4]: 1024 spp and
+    beyond): the edge-aware filter, the sharp-pixel bypass once 1/N < 0.005 and the full bypass
+    once 1/N < 0.0002 (js/PathTracingCommon.js:293-296), on a real accumulation buffer whose
+    alpha carries the path tracer's edge flags (1.01 / -1 / 0) - bit-exact with the oracle."""
+    import babylon_pt as bp
+    meta = H.stream("cornell_256")
+    player = bp.StreamPlayer(engine, meta, H.bluenoise())
+    engine.resize_canvas(player.width, player.height)
+    for i in range(len(meta["frames"])):
+        player.play_frame(i)
+    engine.sync()
+    acc = player.textures["pathTracingRenderTarget"].read()
+    flags = set(np.unique(acc[..., 3]).tolist())
+    assert flags <= {0.0, -1.0, np.float32(1.01).item()} and len(flags) >= 2, flags
+    inv = float(np.float32(1.0 / n))
+    out_call = next(c for c in meta["frames"][-1] if c["shader"] == "screenOutputFragmentShader")
+    player.play_call(out_call, uniform_override={"uOneOverSampleCounter": ["f", [inv]]})
+    engine.sync()
+    got = engine.read_canvas(player.width, player.height)
+    exp = out_call["uniforms"].get("uToneMappingExposure", ["f", [1.0]])[1][0]
+    want = H.po_screen_output(acc, inv, exp)
+    assert _bits_equal(want, got), _diff_report(want, got)

@@ -255,3 +255,28 @@ def test_quadric_intersectors_hit_their_surfaces(shape):
     p = ro[hit].astype(np.float64) + rd[hit].astype(np.float64) * t[hit, None].astype(np.float64)
     tol = 0.02 if shape == 11 else 2e-3   # the torus is ray-marched to |d| < 0.01
     assert np.quantile(_implicit(shape, k, p), 0.99) < tol
+
+
+def test_screen_output_bypass_thresholds():
+    """The two bypasses of js/PathTracingCommon.js:293-296 switch on where the GPU test
+    (test_screen_output_sample_count_branches) places N: from N = 201 (1/N < 0.005) a sharp pixel
+    (a = 1.01) no longer sees its neighbours, from N = 5001 (1/N < 0.0002) no pixel does."""
+    rs = np.random.RandomState(3)
+    acc = np.zeros((24, 24, 4), np.float32)
+    acc[..., :3] = rs.uniform(0, 50, (24, 24, 3)).astype(np.float32)
+    acc[..., 3] = rs.choice(np.array([0.0, 1.01, -1.0], np.float32), (24, 24))
+    acc[12, 12, 3] = np.float32(1.01)    # a sharp pixel
+    acc[12, 6, 3] = 0.0                  # a filtered one
+    other = acc.copy()
+    other[10:15, 10:15, :3] += 7.0       # its neighbourhoods change, the pixels themselves do not
+    other[12, 12, :3] = acc[12, 12, :3]
+    other[10:15, 4:9, :3] += 7.0
+    other[12, 6, :3] = acc[12, 6, :3]
+
+    def px(a, n, y, x):
+        return po.screen_output(a, float(np.float32(1.0 / n)), 1.0)[y, x].tolist()
+
+    assert px(acc, 200, 12, 12) != px(other, 200, 12, 12)     # filtered
+    assert px(acc, 201, 12, 12) == px(other, 201, 12, 12)     # sharp-pixel bypass
+    assert px(acc, 4999, 12, 6) != px(other, 4999, 12, 6)
+    assert px(acc, 5001, 12, 6) == px(other, 5001, 12, 6)     # full bypass
