@@ -498,3 +498,24 @@ def test_screen_output_sample_count_branches(engine, n):
     exp = out_call["uniforms"].get("uToneMappingExposure", ["f", [1.0]])[1][0]
     want = H.po_screen_output(acc, inv, exp)
     assert _bits_equal(want, got), _diff_report(want, got)
+
+
+@pytest.mark.parametrize("name", ["sky_256", "cornell_256"])
+def test_long_accumulation_bitexact(engine, name):
+    """64 progressive frames past the recording (the render loop's still-camera frames:
+    uSampleCounter / uFrameCounter counting up, fresh uRandomVec2 each frame): the running
+    accumulation and the canvas stay bit-exact with the oracle - no drift in the history blend."""
+    import copy
+    import babylon_pt as bp
+    meta = copy.deepcopy(H.stream(name))
+    player = bp.StreamPlayer(engine, meta, H.bluenoise())
+    meta["frames"] = meta["frames"] + [player.synth_frame(k) for k in range(64)]
+    ref_acc, ref_can, _ = H.oracle_replay(meta, with_output=True)
+    engine.resize_canvas(player.width, player.height)
+    for i in range(len(meta["frames"])):
+        player.play_frame(i)
+    engine.sync()
+    ga = player.textures["pathTracingRenderTarget"].read()
+    gc = engine.read_canvas(player.width, player.height)
+    assert _bits_equal(ref_acc[-1], ga), _diff_report(ref_acc[-1], ga)
+    assert _bits_equal(ref_can[-1], gc), _diff_report(ref_can[-1], gc)
