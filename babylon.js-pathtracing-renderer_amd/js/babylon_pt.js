@@ -13,7 +13,8 @@
 //   new BABYLON.Engine(canvas)                    -> pt_ctx_create           (js/GLTF_Model_Path_Tracing.js:189)
 //   new BABYLON.RenderTargetTexture(n,{w,h},...)  -> pt_render_target_create (:762-768), .resize -> pt_render_target_resize
 //   BABYLON.RawTexture.CreateRGBATexture(...)     -> pt_texture_create_rgba32f / _rgba8 (:466-487)
-//   new BABYLON.Texture(url, ...)                 -> host PNG decode + pt_texture_create_rgba8 (:749-758);
+//   new BABYLON.Texture(url, ...)                 -> host PNG / JPEG decode + pt_texture_create_rgba8 (:749-758);
+//   Texture.updateURL(url, bytes) (glTF loader)   -> the same, for the models' PBR maps
 //                                                    '*.hdr' -> host RGBE decode, readPixels() (js/HDRI_Environment_Path_Tracing.js:764-823)
 //   new BABYLON.EffectWrapper({...})              -> pt_effect_create (GLSL text -> program) (:773-811)
 //   effect.setFloat/.../setMatrix/setTexture      -> pt_set_float / pt_set_int / pt_set_texture (:813-848)
@@ -112,6 +113,20 @@ function decodePNG(buf) {
   return { width: w, height: h, data: out };
 }
 
+// ---------------------------------------------------------------------------------- JPEG (host)
+// JPEG maps (the glTF models' PBR textures) are decoded by the Python host's decoder
+// (decode_image.py: Pillow / libjpeg-turbo) in a child process; PT_PYTHON names the interpreter.
+function decodeImage(buf) {
+  buf = Buffer.from(buf.buffer ? Buffer.from(buf.buffer, buf.byteOffset, buf.byteLength) : buf);
+  if (buf.length >= 4 && buf.readUInt32BE(0) === 0x89504e47) return decodePNG(buf);
+  if (!(buf.length >= 2 && buf[0] === 0xff && buf[1] === 0xd8)) throw new Error('not a PNG or JPEG image');
+  const out = require('child_process').execFileSync(process.env.PT_PYTHON || 'python3',
+    [path.join(__dirname, 'decode_image.py')], { input: buf, maxBuffer: 1 << 30 });
+  const w = out.readUInt32LE(0), h = out.readUInt32LE(4);
+  if (out.length !== 8 + 4 * w * h) throw new Error('image decode: short output');
+  return { width: w, height: h, data: new Uint8Array(out.buffer, out.byteOffset + 8, 4 * w * h) };
+}
+
 function install(BABYLON, opts) {
   opts = Object.assign({ device: 0, width: 1920, height: 1080, baseDir: process.cwd(), addon: null, onError: null,
                         label: null }, opts || {});
@@ -201,13 +216,37 @@ function install(BABYLON, opts) {
     },
   };
 
+  function adoptForeign(ctx, t) {
+    t._ptForeign = null;
+    const bytes = t._buffer;
+    if (!bytes || typeof bytes === 'string') return;
+    try {
+      const img = decodeImage(bytes);
+      const sm = typeof t.samplingMode === 'number' ? t.samplingMode : 3;
+      const h = addon.pt_texture_create_rgba8(ctx, img.width, img.height, img.data, sm, t._invertY ? 1 : 0);
+      if (typeof h !== 'number') t._ptForeign = label(h, t.name || t.url || 'texture');
+    } catch (e) {
+      report('texture ' + (t.name || t.url) + ': ' + e.message + ' (left unbound)');
+    }
+  }
+
   class Texture {
+    // new Texture(url, scene, noMipmap, invertY, samplingMode, onLoad) or, as the glTF loader calls
+    // it, new Texture(null, scene, { invertY, samplingMode, onLoad, ... }) then updateURL(url, bytes)
     constructor(url, scene, noMipmap, invertY, samplingMode, onLoad) {
-      this.name = url;
+      if (noMipmap && typeof noMipmap === 'object') {
+        const o = noMipmap;
+        invertY = o.invertY; samplingMode = o.samplingMode; onLoad = o.onLoad;
+      }
+      this._name = url || '';
       this._ctx = ctxOf(scene);
       this._pt = null;
       this._size = { width: 0, height: 0 };
       this._pixels = null;
+      this._invertY = invertY === undefined ? true : !!invertY;
+      this._sampling = samplingMode === undefined ? 3 : samplingMode;
+      this._onLoad = onLoad;
+      if (url === null || url === undefined) return;   // bytes follow through updateURL
       // page-relative URLs resolve against baseDir, then the extra opts.assetDirs
       const dirs = [opts.baseDir].concat(opts.assetDirs || []);
       const file = path.isAbsolute(url) ? url
@@ -225,15 +264,30 @@ function install(BABYLON, opts) {
         }
         return;
       }
+      let bytes;
+      try { bytes = fs.readFileSync(file); } catch (e) { report('Texture(' + url + '): ' + e.message + ' (left unbound)'); return; }
+      this._upload(bytes, url);
+    }
+    // the glTF loader's path: the image file's bytes (Babylon's Texture.updateURL(url, buffer))
+    updateURL(url, buffer) {
+      if (!this._name || this._name.startsWith('data:')) this._name = url;
+      if (this._pt) { addon.pt_texture_destroy(this._pt); this._pt = null; }
+      if (buffer) this._upload(buffer, url);
+      else report('Texture.updateURL(' + url + '): no image bytes (left unbound)');
+    }
+    _upload(bytes, what) {
       try {
-        const img = decodePNG(fs.readFileSync(file));
+        const img = decodeImage(bytes);
         this._size = { width: img.width, height: img.height };
-        const h = addon.pt_texture_create_rgba8(this._ctx, img.width, img.height, img.data, samplingMode === undefined ? 3 : samplingMode, invertY ? 1 : 0);
-        if (typeof h !== 'number') this._pt = label(h, url);
+        const h = addon.pt_texture_create_rgba8(this._ctx, img.width, img.height, img.data, this._sampling, this._invertY ? 1 : 0);
+        if (typeof h !== 'number') this._pt = label(h, this._name || what);
+        if (this._onLoad) setImmediate(this._onLoad);
       } catch (e) {
-        report('Texture(' + url + '): ' + e.message + ' (left unbound)');
+        report('Texture(' + what + '): ' + e.message + ' (left unbound)');
       }
     }
+    get name() { return this._name; }
+    set name(v) { this._name = v; if (this._pt) label(this._pt, v); }
     getSize() { return this._size; }
     readPixels() { return Promise.resolve(this._pixels); }
     dispose() { if (this._pt) addon.pt_texture_destroy(this._pt); this._pt = null; }
@@ -253,8 +307,12 @@ function install(BABYLON, opts) {
     setInt(n, v) { if (this._pt) check(this._ctx, addon.pt_set_int(this._pt, n, v | 0), 'setInt ' + n); return this; }
     setBool(n, v) { return this.setInt(n, v ? 1 : 0); }
     setTexture(n, t) {
-      // an unloaded Babylon texture (null / undefined, e.g. a model without albedo map) binds nothing
-      if (this._pt) check(this._ctx, addon.pt_set_texture(this._pt, n, t && t._pt ? t._pt : null), 'setTexture ' + n);
+      // an unloaded Babylon texture (null / undefined, e.g. a model without albedo map) binds
+      // nothing; a texture Babylon itself created (the glTF loader's PBR maps) is uploaded once,
+      // from the image bytes it keeps (Texture.updateURL(url, buffer))
+      if (t && !t._pt && t._ptForeign === undefined) adoptForeign(this._ctx, t);
+      const h = t ? (t._pt || t._ptForeign || null) : null;
+      if (this._pt) check(this._ctx, addon.pt_set_texture(this._pt, n, h), 'setTexture ' + n);
       return this;
     }
   }
@@ -293,7 +351,7 @@ function install(BABYLON, opts) {
   set('Texture', Texture);
   set('EffectWrapper', EffectWrapper);
   set('EffectRenderer', EffectRenderer);
-  return { addon, Engine, decodePNG, decodeHDR, nativeBVH: () => nativeBVH(addon) };
+  return { addon, Engine, decodePNG, decodeHDR, decodeImage, nativeBVH: () => nativeBVH(addon) };
 }
 
 // BVH_Build_Iterative(workList, aabb_array) (js/BVH_Fast_Builder.js:320-406) over libpt's native
@@ -309,4 +367,4 @@ function nativeBVH(addon) {
   };
 }
 
-module.exports = { install, decodePNG, decodeHDR, nativeBVH, loadAddon };
+module.exports = { install, decodePNG, decodeHDR, decodeImage, nativeBVH, loadAddon };

@@ -37,7 +37,7 @@ const mock = {
   pt_render_target_resize: (t, w, h) => { t.w = w; t.h = h; return 0; },
   pt_texture_size: (t) => [t.w, t.h],
   pt_texture_create_rgba32f: (ctx, w, h, data) => ({ kind: 'f32', w, h, data }),
-  pt_texture_create_rgba8: (ctx, w, h, data) => ({ kind: 'u8', w, h, data }),
+  pt_texture_create_rgba8: (ctx, w, h, data, sampling, invertY) => { const t = { kind: 'u8', w, h, data, sampling, invertY }; u8.push(t); return t; },
   pt_texture_destroy: () => null,
   pt_render: (fx, target) => {
     frames[frames.length - 1].push({ effect: fx.name, shader: fx.shader, target: target ? target.name : null,
@@ -48,6 +48,7 @@ const mock = {
 };
 let raw = 0;
 const rawData = [];
+const u8 = [];   // every RGBA8 texture created (blue noise, PBR maps)
 const label = (h, name) => { if (name === 'RawTexture') rawData.push(h.data); labelName(h, name); };
 const labelName = (h, name) => { h.name = name === 'RawTexture' ? 'raw' + (raw++) : (name.startsWith('./textures/') ? 'file:' + path.basename(name) : name); };
 
@@ -105,5 +106,7 @@ const f32s = () => { let n = 0; for (const f of frames) for (const c of f) for (
   frames = frames.slice(0, FRAMES);
   const crypto = require('crypto');
   const hashes = rawData.map((d) => crypto.createHash('sha256').update(Buffer.from(d.buffer, d.byteOffset, d.byteLength)).digest('hex'));
-  process.stdout.write(JSON.stringify({ scene, width: W, height: H, frames, f32: f32s(), raw_sha256: hashes }));
+  const rgba8 = u8.map((t) => ({ name: t.name, width: t.w, height: t.h, sampling: t.sampling, invertY: t.invertY,
+                                  sha256: crypto.createHash('sha256').update(Buffer.from(t.data.buffer, t.data.byteOffset, t.data.byteLength)).digest('hex') }));
+  process.stdout.write(JSON.stringify({ scene, width: W, height: H, frames, f32: f32s(), raw_sha256: hashes, rgba8 }));
 })().catch((e) => { console.error(e); process.exit(1); });

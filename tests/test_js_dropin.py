@@ -55,10 +55,7 @@ def test_unmodified_setup_script_drives_the_shim(name, hdr_dir):
         for ca, cb in zip(fa, fb):
             for k in ("effect", "shader", "target", "uniforms"):
                 assert ca[k] == cb[k], "frame %d %s %s" % (i, cb["effect"], k)
-            # known gap: the glTF loader's JPEG PBR maps (DamagedHelmet) are not decoded by the Node
-            # host yet, so the shim binds them as unloaded textures
-            want = {s: (None if s in PBR_MAPS else t) for s, t in cb["samplers"].items()}
-            assert ca["samplers"] == want, "frame %d %s samplers" % (i, cb["effect"])
+            assert ca["samplers"] == cb["samplers"], "frame %d %s samplers" % (i, cb["effect"])
     if meta["scene"] in ("gltf", "hdri"):
         payload = H.texture_payloads(meta, H.mesh(meta))
         want = {hashlib.sha256(payload[k].tobytes()).hexdigest() for k in ("bvh", "tri")}
@@ -66,3 +63,27 @@ def test_unmodified_setup_script_drives_the_shim(name, hdr_dir):
     if meta["scene"] == "hdri":
         # the environment reached the boundary exactly as decoded from the RGBE file
         assert hashlib.sha256(hdr_dir[1].tobytes()).hexdigest() in got["raw_sha256"]
+
+
+def test_gltf_pbr_maps_reach_the_boundary_decoded():
+    """DamagedHelmet's JPEG maps, created by Babylon's own glTF loader and bound by the unmodified
+    script (js/GLTF_Model_Path_Tracing.js:252-272, :822-825), are uploaded by the shim as RGBA8
+    exactly as the Python host decodes them (pt_assets.decode_rgba8), rows top first (the loader's
+    invertY = false), with the loader's sampling mode."""
+    import pt_assets
+    meta = H.stream("gltf_helmet_320x180")
+    got = run(meta["scene"], meta["width"], meta["height"], 1, meta["seed"], meta.get("model"))
+    tex = {t["name"]: t for t in got["rgba8"]}
+    gj = json.load(open(os.path.join(REF, "models", "DamagedHelmet.gltf")))
+    files = {"Material_MR (Base Color)": "materials/DamagedHelmet/Default_albedo.jpg", "Material_MR (Normal)": "materials/DamagedHelmet/Default_normal.jpg",
+             "Material_MR (Metallic Roughness)": "materials/DamagedHelmet/Default_metalRoughness.jpg",
+             "Material_MR (Emissive)": "materials/DamagedHelmet/Default_emissive.jpg"}
+    assert {i["uri"] for i in gj["images"]} >= set(files.values())
+    for name, fn in files.items():
+        t = tex[name]
+        img = pt_assets.decode_rgba8(open(os.path.join(REF, "models", fn), "rb").read())
+        assert (t["width"], t["height"]) == (img.shape[1], img.shape[0])
+        assert t["invertY"] == 0
+        assert t["sha256"] == hashlib.sha256(img.tobytes()).hexdigest(), name
+    sampled = {t for c in got["frames"][0] for s, t in c["samplers"].items() if s in PBR_MAPS}
+    assert sampled == set(files)
