@@ -5,7 +5,7 @@
 //
 // usage: node replay_stream.js <stream.json> <payload_dir> <out_prefix> [frames]
 //   payload_dir holds bluenoise.u8 (256x256 RGBA8) and, for glTF streams, bvh.f32 / tri.f32
-//   (2048x2048 RGBA32F, the RawTexture payloads).
+//   (2048x2048 RGBA32F, the RawTexture payloads), and optionally maps.json (model PBR maps, below).
 'use strict';
 const fs = require('fs');
 const path = require('path');
@@ -29,6 +29,15 @@ const tex = {
 };
 if (meta.textures) {
   for (const [raw, kind] of Object.entries(meta.textures)) tex[raw] = BABYLON.RawTexture.CreateRGBATexture(f32(kind + '.f32'), 2048, 2048, engine, false, false, 1, 1);
+}
+// maps.json (optional): { texture name: image file } - model maps as Babylon's glTF loader leaves
+// them (a texture holding the image file's bytes, invertY false); the shim decodes and uploads them
+// when the script binds them (setTexture)
+const mapsSpec = path.join(payloadDir, 'maps.json');
+if (fs.existsSync(mapsSpec)) {
+  for (const [name, file] of Object.entries(JSON.parse(fs.readFileSync(mapsSpec, 'utf8')))) {
+    tex[name] = { name, url: 'data:' + file, _buffer: new Uint8Array(fs.readFileSync(file)), samplingMode: 3, _invertY: false };
+  }
 }
 const renderer = new BABYLON.EffectRenderer(engine);
 const wrappers = {};
