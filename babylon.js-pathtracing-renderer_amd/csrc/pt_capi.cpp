@@ -44,7 +44,7 @@ hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceArgs* a, cons
 namespace {
 
 enum TexKind { TEX_F32 = 0, TEX_U8 = 1, TEX_RT = 2 };
-constexpr int kProgSlots = 8;
+constexpr int kProgSlots = 9;
 
 struct Uniform {
     int n = 0;
@@ -164,7 +164,8 @@ int classify(const char* src)
     if (!contains(src, "pathtracing_default_main")) return PT_PROG_UNKNOWN;
     if (contains(src, "uniform sampler2D tHDRTexture")) return PT_PROG_HDRI;
     if (contains(src, "uniform mat4 uTorusInvMatrix")) return PT_PROG_QUADRIC;
-    if (contains(src, "pathtracing_physical_sky_functions")) return PT_PROG_SKY;
+    if (contains(src, "pathtracing_physical_sky_functions"))   // the sky scene, or its composite with the
+        return contains(src, "uniform sampler2D tAABBTexture") ? PT_PROG_SKY_MESH : PT_PROG_SKY;   // glTF model block
     if (contains(src, "uniform sampler2D tAABBTexture")) return PT_PROG_GLTF;
     if (contains(src, "uniform int uRightSphereMatType")) return PT_PROG_CORNELL;
     return PT_PROG_UNKNOWN;
@@ -247,8 +248,8 @@ void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
     a.sph[0].color = v3(1.0f, 1.0f, 0.0f);
     a.sph[0].type = pt::CLEARCOAT_DIFFUSE;
     a.sph[1].color = v3(1.0f, 1.0f, 1.0f);
-    const bool mesh = fx->prog == PT_PROG_GLTF || fx->prog == PT_PROG_HDRI;
-    a.sph[1].type = mesh ? pt::METAL : ui(fx, "uRightSphereMatType");
+    const bool gltf = fx->prog == PT_PROG_GLTF || fx->prog == PT_PROG_HDRI;
+    a.sph[1].type = gltf ? pt::METAL : ui(fx, "uRightSphereMatType");
     pt::QuadArg q[6];
     q[0] = quad(v3(0, 0, 1), v3(-W, W, W), v3(W, W, W), v3(W, -W, W), v3(-W, -W, W), white, pt::DIFFUSE);
     q[1] = quad(v3(1, 0, 0), v3(-W, -W, W), v3(-W, -W, -W), v3(-W, W, -W), v3(-W, W, W), v3(0.7f, 0.05f, 0.05f), pt::DIFFUSE);
@@ -275,7 +276,8 @@ void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
     a.light = q[5];
     a.light_r2 = hdist(q[5].v0, q[5].v1) * hdist(q[5].v0, q[5].v3);
     a.nquads = 6;
-    if (fx->prog == PT_PROG_SKY || fx->prog == PT_PROG_HDRI) {
+    const bool sky = fx->prog == PT_PROG_SKY || fx->prog == PT_PROG_SKY_MESH;
+    if (sky || fx->prog == PT_PROG_HDRI) {
         // js/PhysicalSkyModel_FragmentShader.js:383-399, js/HDRIEnvironmentPathTracing_FragmentShader.js:529-542:
         // N_QUADS 4 = back, left, right walls and the floor (the Cornell ceiling and quad light are gone)
         const pt::QuadArg floor = q[4];
@@ -286,7 +288,7 @@ void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
         a.qtype[3] = floor.type;
         a.nquads = 4;
     }
-    if (fx->prog == PT_PROG_SKY) sky_setup(fx, a.sky);
+    if (sky) sky_setup(fx, a.sky);
     if (fx->prog == PT_PROG_QUADRIC) {   // js/TransformedQuadricGeometry_FragmentShader.js:9-24
         static const char* const kShapes[12] = {
             "uSphereInvMatrix", "uCylinderInvMatrix", "uConeInvMatrix", "uParaboloidInvMatrix",
@@ -498,7 +500,7 @@ int render_trace(pt_effect* fx, pt_texture* target)
     a.prev = (const float4*)prev->d;
     a.out = (float4*)target->d;
     a.bluenoise = tex8(bn);
-    const bool mesh = fx->prog == PT_PROG_GLTF || fx->prog == PT_PROG_HDRI;
+    const bool mesh = fx->prog == PT_PROG_GLTF || fx->prog == PT_PROG_HDRI || fx->prog == PT_PROG_SKY_MESH;
     if (mesh) {
         pt_texture* bvh = sampler(fx, "tAABBTexture");
         pt_texture* tri = sampler(fx, "tTriangleTexture");
@@ -581,6 +583,8 @@ int render_trace(pt_effect* fx, pt_texture* target)
                     HIPCHK(c, hipMemsetAsync(c->lpt_mem, 0, 4 * n * sizeof(unsigned), c->stream));
                     c->lpt_cap = n;
                     c->lpt_valid = false;
+                } else if (!same) {   // another grid, target or program: its wave costs start afresh
+                    HIPCHK(c, hipMemsetAsync(c->lpt_mem, 0, 4 * n * sizeof(unsigned), c->stream));
                 }
                 a.order = same ? c->lpt_mem + 4 * c->lpt_cap : nullptr;
                 a.cost = c->lpt_mem;
@@ -854,7 +858,7 @@ pt_effect* pt_effect_create(pt_ctx* c, const char* src, const char* const* un, i
 pt_effect* pt_effect_create_program(pt_ctx* c, int prog, const char* const* un, int nu, const char* const* sn, int ns, int* err)
 {
     if (err) *err = PT_OK;
-    if (!c || nu < 0 || ns < 0 || prog <= PT_PROG_UNKNOWN || prog > PT_PROG_QUADRIC) { if (err) *err = PT_ERR_ARG; return nullptr; }
+    if (!c || nu < 0 || ns < 0 || prog <= PT_PROG_UNKNOWN || prog > PT_PROG_SKY_MESH) { if (err) *err = PT_ERR_ARG; return nullptr; }
     auto* fx = new pt_effect();
     fx->ctx = c;
     fx->prog = prog;
@@ -988,6 +992,7 @@ int pt_render(pt_effect* fx, pt_texture* target)
     case PT_PROG_CORNELL:
     case PT_PROG_QUADRIC:
     case PT_PROG_SKY:
+    case PT_PROG_SKY_MESH:
     case PT_PROG_HDRI:
     case PT_PROG_GLTF: return render_trace(fx, target);
     case PT_PROG_SCREEN_COPY: return render_copy(fx, target);
@@ -1079,6 +1084,7 @@ int pt_timing_end(pt_ctx* c, int prog, double* total_ms, int* launches)
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = flush_copy(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->window = false;   // the window is closed; its draws stay readable by further pt_timing_end calls
     double t = 0.0;
     int n = 0;
     for (auto& d : c->window_draws) {

@@ -14,34 +14,41 @@ using namespace ptg;
 constexpr float kINF = 1000000.0f;   // #define INFINITY 1000000.0 (js/PathTracingCommon.js:329)
 constexpr float kTwoPi = 6.28318530717958648f;
 
-enum { PROG_CORNELL = 3, PROG_GLTF = 4, PROG_HDRI = 5, PROG_SKY = 6, PROG_QUADRIC = 7 };
-// PROG_GLTF_TEX / PROG_HDRI_TEX: the mesh programs instantiated with their PBR / normal-map code
-// (models with an albedo or bump texture); without +PROG_TEX those branches are compiled out.
-enum { PROG_TEX = 100, PROG_GLTF_TEX = 104, PROG_HDRI_TEX = 105 };
+enum { PROG_CORNELL = 3, PROG_GLTF = 4, PROG_HDRI = 5, PROG_SKY = 6, PROG_QUADRIC = 7, PROG_SKYMESH = 8 };
+// PROG_*_TEX: the mesh programs instantiated with their PBR / normal-map code (models with an
+// albedo or bump texture); without +PROG_TEX those branches are compiled out.
+enum { PROG_TEX = 100, PROG_GLTF_TEX = 104, PROG_HDRI_TEX = 105, PROG_SKYMESH_TEX = 108 };
 // +PROG_PAIRS: the same programs walking the child-pair BVH records (bvhWalkPairs) instead of the
 // reference's texel pairs (bvhWalkRef); chosen per draw by the host (pt_capi.cpp ensure_pairs)
 enum { PROG_PAIRS = 1000 };
 template <int P> constexpr int kBase = P % PROG_PAIRS;
 template <int P> constexpr int kScene = kBase<P> % PROG_TEX;
-// the mesh programs (BVH walk, PBR materials): glTF and HDRI
+// the programs whose SceneIntersect walks the glTF model's BVH: glTF, HDRI and the physical-sky
+// composite (PROG_SKYMESH, DESIGN.md §1: the sky scene with the glTF model block appended)
+template <int P> constexpr bool kHasMesh = kScene<P> == PROG_GLTF || kScene<P> == PROG_HDRI || kScene<P> == PROG_SKYMESH;
+// the glTF CalculateRadiance (PBR decode, glossy METAL lobe): glTF and HDRI
 template <int P> constexpr bool kIsGltf = kScene<P> == PROG_GLTF || kScene<P> == PROG_HDRI;
 template <int P> constexpr bool kIsHdri = kScene<P> == PROG_HDRI;
 template <int P> constexpr bool kHasTex = kBase<P> >= PROG_TEX;
-template <int P> constexpr bool kIsSky = P == PROG_SKY;
+// the physical-sky CalculateRadiance (js/PhysicalSkyModel_FragmentShader.js:119-379)
+template <int P> constexpr bool kIsSky = kScene<P> == PROG_SKY || kScene<P> == PROG_SKYMESH;
 template <int P> constexpr bool kIsQuadric = P == PROG_QUADRIC;
-// hitObjectID layout: spheres 0-1 (quadric: shapes 0-11), then the quads; the mesh is 8
+// hitObjectID layout: spheres 0-1 (quadric: shapes 0-11), then the quads, then the mesh
+// (objectCount after the quads: 8 in the glTF scene, 6 in the HDRI scene and the sky composite)
 template <int P> constexpr int kQuadId0 = kIsQuadric<P> ? 12 : 2;
 template <int P> constexpr bool kPairs = P >= PROG_PAIRS;
 // every instantiated program variant
 #define PT_FOR_EACH_PROG(X)                                                                           \
     X(PROG_CORNELL) X(PROG_SKY) X(PROG_QUADRIC) X(PROG_GLTF) X(PROG_GLTF_TEX) X(PROG_HDRI) X(PROG_HDRI_TEX)           \
-    X(PROG_PAIRS + PROG_GLTF) X(PROG_PAIRS + PROG_GLTF_TEX) X(PROG_PAIRS + PROG_HDRI) X(PROG_PAIRS + PROG_HDRI_TEX)
+    X(PROG_SKYMESH) X(PROG_SKYMESH_TEX)                                                                                 \
+    X(PROG_PAIRS + PROG_GLTF) X(PROG_PAIRS + PROG_GLTF_TEX) X(PROG_PAIRS + PROG_HDRI) X(PROG_PAIRS + PROG_HDRI_TEX)     \
+    X(PROG_PAIRS + PROG_SKYMESH) X(PROG_PAIRS + PROG_SKYMESH_TEX)
 
 // the kernel variant of a draw: the scene program, +PROG_TEX when the model carries albedo / bump
 // maps, +PROG_PAIRS when the BVH walk uses child-pair records
 __host__ __device__ inline int resolveProgram(int prog, bool textured, bool pairs)
 {
-    if (prog != PROG_GLTF && prog != PROG_HDRI) return prog;
+    if (prog != PROG_GLTF && prog != PROG_HDRI && prog != PROG_SKYMESH) return prog;
     return prog + (textured ? PROG_TEX : 0) + (pairs ? PROG_PAIRS : 0);
 }
 // waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 80 -> 6; the

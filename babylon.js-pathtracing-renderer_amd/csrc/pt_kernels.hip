@@ -85,7 +85,7 @@ PT_D void meshHit(const TraceArgs& a, float triID, float triU, float triV, Hit& 
     h.normal = normalize(mul3t(a.model, nn));
     h.type = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
     h.color = mk(1.0f, 1.0f, 1.0f);
-    h.id = 8;
+    h.id = meshObjectId<PROG>(a);
 }
 
 // SceneIntersect: js/BabylonPathTracing_FragmentShader.js:47-112 (Cornell),
@@ -101,7 +101,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     // the walk, same results
     f3 sn;
     analyticNearest<PROG>(a, rayO, rayD, h, sn);
-    if (!kIsGltf<PROG>) { analyticAttributes<PROG>(a, h, sn); return; }
+    if (!kHasMesh<PROG>) { analyticAttributes<PROG>(a, h, sn); return; }
 
     // ---- BVH walk (js/GLTFModelPathTracing_FragmentShader.js:201-298), pt_device.h
     f3 O = mul(a.model, rayO, 1.0f), D = mul(a.model, rayD, 0.0f);

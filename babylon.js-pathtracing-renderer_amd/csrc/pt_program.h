@@ -117,6 +117,11 @@ PT_D f3 skyColor(const SkyArgs& k, f3 rayDir)
     return pow3(tex, k.retExp);
 }
 
+// hitObjectID of the glTF model: SceneIntersect's objectCount after the spheres and quads
+// (js/GLTFModelPathTracing_FragmentShader.js:343)
+template <int PROG>
+PT_D int meshObjectId(const TraceArgs& a) { return kQuadId0<PROG> + a.nquads; }
+
 // hitColor / hitType of analytic object `id` (the values SceneIntersect writes with it)
 template <int PROG>
 PT_D void objectMaterial(const TraceArgs& a, int id, f3& color, int& type)
@@ -133,7 +138,7 @@ PT_D void objectMaterial(const TraceArgs& a, int id, f3& color, int& type)
         color = a.sph[id].color; type = a.sph[id].type;
     } else if (id >= q0 && id < q0 + a.nquads) {
         color = a.qcolor[id - q0]; type = a.qtype[id - q0];
-    } else if (id == 8 && kIsGltf<PROG>) {
+    } else if (kHasMesh<PROG> && id == meshObjectId<PROG>(a)) {
         color = mk(1.0f, 1.0f, 1.0f); type = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
     }
 }
@@ -195,7 +200,7 @@ PT_D void analyticIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h)
     analyticNearest<PROG>(a, rayO, rayD, h, sn);
     analyticAttributes<PROG>(a, h, sn);
 }
-// Get_HDR_Color (js/HDRIEnvironmentPathTracing_FragmentShader.js:236-245): equirect lookup
+// Get_HDR_Color (js/HDRIEnvironmentPathTracing_FragmentShader.js:351-360): equirect lookup
 template <bool COUNT>
 PT_D f3 envColor(const TraceArgs& a, f3 rd, Cnt& cnt)
 {
@@ -231,7 +236,7 @@ PT_D bool shadeStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, Hit
             return false;
         }
         if (!sky) return false;
-        // js/PhysicalSkyModel_FragmentShader.js:155-189 (with diffuseCount == 0 the path is still
+        // js/PhysicalSkyModel_FragmentShader.js:155-189 (also the sky composite's; with diffuseCount == 0 the path is still
         // specular, so one of the five cases always ends it)
         const f3 skyc = skyColor(a.sky, p.rd);
         if (bounces == 0) { g.setSharp(1.01f); accum = skyc; }
@@ -254,7 +259,7 @@ PT_D bool shadeStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, Hit
     }
     if (s.sampleLight) return false;
 
-    if (kHasTex<PROG> && hitType == PBR_MATERIAL) {
+    if (kHasTex<PROG> && gltf && hitType == PBR_MATERIAL) {   // (the sky radiance has no PBR decode)
         float tx[4];
         texBilinear(a.albedo, h.u, h.v, tx);
         if (COUNT) cnt.tap += 4;

@@ -162,7 +162,7 @@ __global__ __launch_bounds__(kBlock) void wf_extend(TraceArgs a, WfBufs w, int b
                 const int id = h.id;
                 const f3 hn = id >= 0 ? h.normal : mk(0, 0, 0);
                 if (COUNT) count_add<true>(a, C_SEGMENTS, 1);
-                if (kIsGltf<PROG>) {
+                if (kHasMesh<PROG>) {
                     f3 O = mul(a.model, ro, 1.0f), D = mul(a.model, rd, 0.0f);
                     f3 inv = mk(grcp(D.x), grcp(D.y), grcp(D.z));
                     float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(kBlock) void wf_extend(TraceArgs a, WfBufs w, int b
                 w.hit1[i] = make_float4(hn.x, hn.y, hn.z, 0.0f);
             }
         }
-        if (kIsGltf<PROG>) {
+        if (kHasMesh<PROG>) {
             const unsigned off = block_append(&w.bcnt[b * kShards + it.s], toBvh, sh);
             if (toBvh) w.bvhq[shard0 + off] = i;
         }
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b
                 nn = normalize(S * mN.x + T * mN.y + N * mN.z);
             }
             f3 hn = normalize(mul3t(a.model, nn));
-            w.hit0[i] = make_float4(hitT, u2f(8u), hu, hv);
+            w.hit0[i] = make_float4(hitT, u2f((unsigned)meshObjectId<PROG>(a)), hu, hv);
             w.hit1[i] = make_float4(hn.x, hn.y, hn.z, 0.0f);
         }
         if (COUNT) {
@@ -420,7 +420,7 @@ extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceAr
 #define WF_BOUNCE(P, C)                                                                              \
     for (int b = 0; b < 6; b++) {                                                                    \
         hipLaunchKernelGGL((wf_extend<P, C>), dim3(persist_blocks), blk, 0, s, *a, *w, b);         \
-        if (kIsGltf<P>) hipLaunchKernelGGL((wf_bvh<P, C>), dim3(persist_blocks), blk, 0, s, *a, *w, b); \
+        if (kHasMesh<P>) hipLaunchKernelGGL((wf_bvh<P, C>), dim3(persist_blocks), blk, 0, s, *a, *w, b); \
         hipLaunchKernelGGL((wf_shade<P, C>), dim3(persist_blocks), blk, 0, s, *a, *w, b);          \
     }
 #define WF_CASE_T(P) case P: WF_BOUNCE(P, true) break;

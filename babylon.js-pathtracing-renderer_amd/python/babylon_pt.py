@@ -25,7 +25,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("PT_LIBPT") or os.path.join(PKG, "libpt.so")
 
-PROG = {"screenCopy": 1, "screenOutput": 2, "cornell": 3, "gltf": 4, "hdri": 5, "sky": 6, "quadric": 7}
+PROG = {"screenCopy": 1, "screenOutput": 2, "cornell": 3, "gltf": 4, "hdri": 5, "sky": 6, "quadric": 7, "skymesh": 8}
 ERRORS = {0: "PT_OK", -1: "PT_ERR_ARG", -2: "PT_ERR_HIP", -3: "PT_ERR_SHADER", -4: "PT_ERR_STATE",
           -5: "PT_ERR_OOM", -6: "PT_ERR_DEVICE", -7: "PT_ERR_UNSUPPORTED", -8: "PT_ERR_DATA"}
 NEAREST, BILINEAR, TRILINEAR = 1, 2, 3
@@ -142,7 +142,12 @@ class Engine:
         self.check(lib().pt_canvas_wrap(self.ctx, w, h, ctypes.c_void_p(device_ptr)), "pt_canvas_wrap")
 
     def set_stream(self, hip_stream):
-        """Enqueue on a caller-owned stream (an int handle, e.g. torch.cuda.current_stream().cuda_stream)."""
+        """Enqueue on a caller-owned stream (an int handle, e.g. a dedicated torch.cuda.Stream's
+        .cuda_stream); None restores the context's own stream. A 0 handle is refused: it is HIP's
+        legacy default stream (what torch.cuda.current_stream() is unless a stream was made
+        current), which the context's non-blocking stream would not be ordered with."""
+        if hip_stream is not None and not hip_stream:
+            raise PtError("set_stream(0): pass a dedicated stream's handle (or None for the context's own stream)")
         self.check(lib().pt_set_stream(self.ctx, ctypes.c_void_p(hip_stream) if hip_stream else None), "pt_set_stream")
 
     def set_backend(self, backend):

@@ -47,7 +47,11 @@ enum pt_program {
     PT_PROG_GLTF = 4,           /* js/GLTFModelPathTracing_FragmentShader.js */
     PT_PROG_HDRI = 5,           /* js/HDRIEnvironmentPathTracing_FragmentShader.js */
     PT_PROG_SKY = 6,            /* js/PhysicalSkyModel_FragmentShader.js */
-    PT_PROG_QUADRIC = 7         /* js/TransformedQuadricGeometry_FragmentShader.js */
+    PT_PROG_QUADRIC = 7,        /* js/TransformedQuadricGeometry_FragmentShader.js */
+    /* BASELINE configs[4]: js/PhysicalSkyModel_FragmentShader.js with the glTF model block of
+     * js/GLTFModelPathTracing_FragmentShader.js:201-346 appended to its SceneIntersect (the sky shader
+     * text plus `uniform sampler2D tAABBTexture`); the reference has no such page */
+    PT_PROG_SKY_MESH = 8
 };
 
 /* Babylon sampling-mode constants (BABYLON.Constants.TEXTURE_*_SAMPLINGMODE) */
@@ -162,8 +166,9 @@ void* pt_texture_device_ptr(pt_texture* tex);
  * stream; requires pt_sync first). */
 int pt_last_render_ms(pt_ctx* ctx, int program, float* ms);
 /* Timing window: between pt_timing_begin and pt_timing_end every draw is bracketed by its own
- * HIP event pair (no host sync inside the window); pt_timing_end synchronises and returns the
- * summed device time and launch count of one program kind. */
+ * HIP event pair (no host sync inside the window); pt_timing_end closes the window, synchronises
+ * and returns the summed device time and launch count of one program kind (further pt_timing_end
+ * calls report other kinds from the same window). */
 int pt_timing_begin(pt_ctx* ctx);
 int pt_timing_end(pt_ctx* ctx, int program, double* total_ms, int* launches);
 /* Algorithmic-byte counters: when enabled, path-tracing passes also accumulate

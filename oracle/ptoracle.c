@@ -505,13 +505,14 @@ static Quad mkquad(v3 n, v3 a, v3 b, v3 c, v3 d, v3 col, int type)
 static void SetupScene(Inv* s)
 {
     const pto_frame* f = s->f;
-    if (f->scene == PTO_SCENE_SKY || f->scene == PTO_SCENE_HDRI) {
+    const int sky = f->scene == PTO_SCENE_SKY || f->scene == PTO_SCENE_SKYMESH;
+    if (sky || f->scene == PTO_SCENE_HDRI) {
         /* js/PhysicalSkyModel_FragmentShader.js:383-399 and
          * js/HDRIEnvironmentPathTracing_FragmentShader.js:529-542: N_QUADS 4 (no ceiling, no quad light) */
         float W = 50.0f;
         s->spheres[0].color = V3(1.0f, 1.0f, 0.0f); s->spheres[0].type = CLEARCOAT_DIFFUSE;
         s->spheres[1].color = V3(1.0f, 1.0f, 1.0f);
-        s->spheres[1].type = f->scene == PTO_SCENE_SKY ? f->uRightSphereMatType : METAL;
+        s->spheres[1].type = sky ? f->uRightSphereMatType : METAL;
         s->quads[0] = mkquad(V3(0, 0, 1), V3(-W, W, W), V3(W, W, W), V3(W, -W, W), V3(-W, -W, W), V3(1.0f, 1.0f, 1.0f), DIFFUSE);
         s->quads[1] = mkquad(V3(1, 0, 0), V3(-W, -W, W), V3(-W, -W, -W), V3(-W, W, -W), V3(-W, W, W), V3(0.7f, 0.05f, 0.05f), DIFFUSE);
         s->quads[2] = mkquad(V3(-1, 0, 0), V3(W, -W, -W), V3(W, -W, W), V3(W, W, W), V3(W, W, -W), V3(0.05f, 0.05f, 0.7f), DIFFUSE);
@@ -660,7 +661,7 @@ static void SceneIntersect(Inv* s, v3 rayOrigin, v3 rayDirection, Hit* h)
         }
         objectCount++;
     }
-    if (f->scene != PTO_SCENE_GLTF && f->scene != PTO_SCENE_HDRI) return;
+    if (f->scene != PTO_SCENE_GLTF && f->scene != PTO_SCENE_HDRI && f->scene != PTO_SCENE_SKYMESH) return;
 
     /* ---- BVH traversal, js/GLTFModelPathTracing_FragmentShader.js:201-298 */
     float stackT[STACK_LEVELS], stackId[STACK_LEVELS];
@@ -752,7 +753,7 @@ typedef struct { v3 objectNormal, objectColor; float objectID, pixelSharpness; }
 
 static v3 v_pow22(v3 a) { return V3(g_pow(a.x, 2.2f), g_pow(a.y, 2.2f), g_pow(a.z, 2.2f)); }
 
-/* Get_HDR_Color, js/HDRIEnvironmentPathTracing_FragmentShader.js:236-245 */
+/* Get_HDR_Color, js/HDRIEnvironmentPathTracing_FragmentShader.js:351-360 */
 static v3 Get_HDR_Color(Inv* s, v3 rayDirection)
 {
     const pto_frame* f = s->f;
@@ -1164,7 +1165,7 @@ static void shade_pixel(const pto_frame* f, int px, int py, Shade* out, pto_coun
     s.rayDirection = finalRayDir;
     SetupScene(&s);
     GOut g;
-    v3 r = f->scene == PTO_SCENE_SKY ? CalculateRadianceSky(&s, &g) : CalculateRadiance(&s, &g);
+    v3 r = (f->scene == PTO_SCENE_SKY || f->scene == PTO_SCENE_SKYMESH) ? CalculateRadianceSky(&s, &g) : CalculateRadiance(&s, &g);
     out->rad[0] = r.x; out->rad[1] = r.y; out->rad[2] = r.z;
     out->nrm[0] = g.objectNormal.x; out->nrm[1] = g.objectNormal.y; out->nrm[2] = g.objectNormal.z;
     out->col[0] = g.objectColor.x; out->col[1] = g.objectColor.y; out->col[2] = g.objectColor.z;
@@ -1261,7 +1262,7 @@ static int shade_rows(const pto_frame* f, int row0, int row1, int nthreads, Shad
 int pto_path_trace(const pto_frame* f, const float* prev, float* out, int row0, int row1, int nthreads, pto_counters* counters)
 {
     if (!f || !prev || !out || row0 < 0 || row1 > f->height || row0 >= row1 || !f->blueNoise) return -1;
-    if ((f->scene == PTO_SCENE_GLTF || f->scene == PTO_SCENE_HDRI) && (!f->aabb || !f->tri)) return -2;
+    if ((f->scene == PTO_SCENE_GLTF || f->scene == PTO_SCENE_HDRI || f->scene == PTO_SCENE_SKYMESH) && (!f->aabb || !f->tri)) return -2;
     Shade* sh; int qy0, qy1;
     int Wq = shade_rows(f, row0, row1, nthreads, &sh, &qy0, &qy1, counters);
     if (Wq < 0) return -3;

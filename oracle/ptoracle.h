@@ -14,7 +14,11 @@
 extern "C" {
 #endif
 
-enum { PTO_SCENE_CORNELL = 0, PTO_SCENE_GLTF = 1, PTO_SCENE_SKY = 2, PTO_SCENE_HDRI = 3, PTO_SCENE_QUADRIC = 4 };
+/* PTO_SCENE_SKYMESH: BASELINE configs[4], the physical-sky scene (js/PhysicalSkyModel_FragmentShader.js)
+ * with the glTF model block of js/GLTFModelPathTracing_FragmentShader.js:201-346 appended to its
+ * SceneIntersect (hitObjectID = objectCount = 6); the reference has no such page. */
+enum { PTO_SCENE_CORNELL = 0, PTO_SCENE_GLTF = 1, PTO_SCENE_SKY = 2, PTO_SCENE_HDRI = 3, PTO_SCENE_QUADRIC = 4,
+       PTO_SCENE_SKYMESH = 5 };
 
 /* One frame's uniforms, by the names the setup scripts push (js/GLTF_Model_Path_Tracing.js:813-848,
  * js/Babylon_Path_Tracing.js:339-363). Matrices are Babylon Matrix.m (GLSL column-major). */

@@ -13,7 +13,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libptoracle.so")
 
-SCENES = {"cornell": 0, "gltf": 1, "sky": 2, "hdri": 3, "quadric": 4}
+SCENES = {"cornell": 0, "gltf": 1, "sky": 2, "hdri": 3, "quadric": 4, "skymesh": 5}
 SHAPES = ("uSphereInvMatrix", "uCylinderInvMatrix", "uConeInvMatrix", "uParaboloidInvMatrix", "uHyperboloidInvMatrix",
           "uCapsuleInvMatrix", "uFlattenedRingInvMatrix", "uBoxInvMatrix", "uPyramidFrustumInvMatrix", "uDiskInvMatrix",
           "uRectangleInvMatrix", "uTorusInvMatrix")

@@ -48,7 +48,7 @@ def output_call(frame):
 def oracle_scene(meta, width=None, height=None, mesh_arrays=None, maps=None):
     import ptoracle as po
     w, h = width or meta["width"], height or meta["height"]
-    if meta["scene"] in ("gltf", "hdri"):
+    if meta["scene"] in ("gltf", "hdri", "skymesh"):
         m = mesh_arrays if mesh_arrays is not None else mesh(meta)
         hdr = synthetic_hdr() if meta["scene"] == "hdri" else None
         return po.Scene(meta["scene"], w, h, bluenoise(), m["bvh"], m["tri"], hdr, maps)
@@ -222,6 +222,35 @@ def synthetic_dragon(nu=512, nv=512, knot=(1, 1), tube=9.0):
     return {"bvh": bp.bvh_build(aabb_in), "tri": tri, "aabb_in": aabb_in}
 
 
+# BASELINE configs[4]: the physical-sky page's recorded stream (sky_256) with the glTF page's model
+# uniforms and samplers added, i.e. the effect the sky shader + glTF model block composite declares
+# (DESIGN.md §1). Model transform: a 180-degree turn about y (exact +-1 entries), as the glTF page
+# turns the dragon (js/GLTF_Model_Path_Tracing.js:905-910); material: the page's default, Metal
+# (js/GLTF_Model_Path_Tracing.js:720).
+SKY_MESH_MODEL_INV = [-1.0, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 0.0, -1.0, 0.0, 0.0, 0.0, 0.0, 1.0]
+
+
+def sky_mesh_stream(material=3, model_inv=None):
+    meta = stream("sky_256")
+    meta = dict(meta, scene="skymesh", textures={"raw2": "bvh", "raw3": "tri"}, model="StanfordDragon stand-in")
+    frames = []
+    for f in meta["frames"]:
+        fr = []
+        for c in f:
+            c = dict(c, uniforms=dict(c["uniforms"]), samplers=dict(c["samplers"]))
+            if c["shader"] == "pathTracingFragmentShader":
+                c["uniforms"].update({
+                    "uGLTF_Model_InvMatrix": ["f", list(model_inv or SKY_MESH_MODEL_INV)],
+                    "uModelMaterialType": ["i", [material]],
+                    "uModelUsesAlbedoTexture": ["i", [0]], "uModelUsesBumpTexture": ["i", [0]],
+                    "uModelUsesMetallicTexture": ["i", [0]], "uModelUsesEmissiveTexture": ["i", [0]]})
+                c["samplers"].update({"tAABBTexture": "raw2", "tTriangleTexture": "raw3"})
+            fr.append(c)
+        frames.append(fr)
+    meta["frames"] = frames
+    return meta
+
+
 def po_screen_output(acc, one_over_n, exposure=1.0):
     """The oracle's screenOutput (js/PathTracingCommon.js:19-309) of an RGBA32F frame -> RGBA8."""
     import ptoracle as po
@@ -232,6 +261,41 @@ def po_screen_output(acc, one_over_n, exposure=1.0):
 # 749-758 loads them through the glTF loader; the JPEGs stay in the reference tree)
 PBR_SAMPLERS = {"albedo": "Material_MR (Base Color)", "bump": "Material_MR (Normal)",
                 "metallic": "Material_MR (Metallic Roughness)", "emissive": "Material_MR (Emissive)"}
+
+
+HELMET_MAP_FILES = {"albedo": "Default_albedo.jpg", "bump": "Default_normal.jpg",
+                    "metallic": "Default_metalRoughness.jpg", "emissive": "Default_emissive.jpg"}
+
+
+def helmet_maps():
+    """The DamagedHelmet's four bound PBR maps (tests/golden/helmet_maps/, the reference's own
+    models/materials/DamagedHelmet/*.jpg, bound at js/GLTF_Model_Path_Tracing.js:252-274), decoded
+    as both hosts decode them (pt_assets.decode_rgba8: Pillow / libjpeg-turbo, rows top first,
+    invertY false): {kind: (2048, 2048, 4) uint8}."""
+    import pt_assets
+    out = {}
+    for kind, name in HELMET_MAP_FILES.items():
+        with open(os.path.join(GOLD, "helmet_maps", name), "rb") as f:
+            out[kind] = pt_assets.decode_rgba8(f.read())
+    return out
+
+
+# the bench workloads (bench.py --workload; tools/prof_frames.py): recorded stream, mesh arrays,
+# PBR maps, default frame size
+WORKLOADS = {
+    "dragon": ("gltf_bunny_1080p", "dragon", None, (1920, 1080)),       # BASELINE.json metric
+    "bunny": ("gltf_bunny_1080p", None, None, (1920, 1080)),           # configs[1]
+    "helmet": ("hdri_helmet_320x180", None, "helmet", (1920, 1080)),   # configs[2]
+    "sky_dragon": ("skymesh", "dragon", None, (3840, 2160)),           # configs[4]
+}
+
+
+def workload(name):
+    """(meta, mesh arrays, maps or None, (W, H)) of a bench workload."""
+    key, mesh_kind, maps_kind, size = WORKLOADS[name]
+    meta = sky_mesh_stream() if key == "skymesh" else stream(key)
+    m = synthetic_dragon() if mesh_kind == "dragon" else mesh(meta)
+    return meta, m, (helmet_maps() if maps_kind == "helmet" else None), size
 
 
 def synthetic_pbr_maps(n=256, seed=7):

@@ -98,3 +98,20 @@ def test_cornell_defaults():
     assert u["uQuadLightPlaneSelectionNumber"][1][0] == 6
     assert u["uRightSphereMatType"][1][0] == 3
     assert u["uFrameCounter"][1][0] == 1
+
+
+def test_helmet_maps_are_the_reference_jpegs():
+    """tests/golden/helmet_maps holds the four maps the helmet's material binds, byte for byte the
+    reference's models/materials/DamagedHelmet/*.jpg (sha256 below, taken from the reference tree),
+    and they decode to 2048x2048 RGBA8."""
+    import hashlib
+    want = {"Default_albedo.jpg": "2dc95e87aeb0cd7c8a65ef0eb8b23212388da0534ca379811427a9a8780511f5",
+            "Default_emissive.jpg": "dd0057989f22f93a4ab796d06ebf85a7c12fbfae1d59a86ae8b0c54770dc1159",
+            "Default_metalRoughness.jpg": "0f05e7ffbeaa974f7d2c83436b04109969966d64ab188cbc3a19a265a0a69ae0",
+            "Default_normal.jpg": "f253ba09a90a86ffd8a807dc45d7953111f8b3421e15d7a21d1e915b01dd33c1"}
+    for name, sha in want.items():
+        with open(os.path.join(H.GOLD, "helmet_maps", name), "rb") as f:
+            assert hashlib.sha256(f.read()).hexdigest() == sha, name
+    maps = H.helmet_maps()
+    assert sorted(maps) == sorted(H.PBR_SAMPLERS)
+    assert all(m.shape == (2048, 2048, 4) and m.dtype == np.uint8 for m in maps.values())

@@ -99,7 +99,7 @@ def test_fast_sqrt_is_ieee_on_every_input(engine):
 def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1, split_output=False, mesh=None):
     import babylon_pt as bp
     m = None
-    if meta["scene"] in ("gltf", "hdri"):
+    if meta["scene"] in ("gltf", "hdri", "skymesh"):
         m = H.texture_payloads(meta, mesh if mesh is not None else H.mesh(meta))
     player = bp.StreamPlayer(engine, meta, H.bluenoise(), m, width, height)
     accs, canvases = [], []
@@ -314,14 +314,25 @@ def test_partitioned_screen_output_is_exact(engine, parts):
         assert np.array_equal(a, b)
 
 
+_MAPS = {}
+
+
+def _maps(kind):
+    if kind not in _MAPS:
+        _MAPS[kind] = H.helmet_maps() if kind == "real" else H.synthetic_pbr_maps()
+    return _MAPS[kind]
+
+
+@pytest.mark.parametrize("maps_kind", ["real", "seeded"])
 @pytest.mark.parametrize("name", ["gltf_helmet_320x180", "hdri_helmet_320x180"])
-def test_pbr_maps_bitexact(engine, backend, name):
-    """DamagedHelmet with all four PBR samplers bound (seeded stand-ins for its JPEG maps:
-    helpers.synthetic_pbr_maps): albedo pow 2.2, normal-map perturbation, metallic-roughness
+def test_pbr_maps_bitexact(engine, backend, name, maps_kind):
+    """DamagedHelmet with all four PBR samplers bound - its real maps (the reference's JPEGs,
+    tests/golden/helmet_maps, 2048x2048) and seeded stand-ins that reach every material branch
+    (helpers.synthetic_pbr_maps): albedo pow 2.2, normal-map perturbation, metallic-roughness
     material switches and emission, bit for bit against the oracle on every schedule."""
     import babylon_pt as bp
     meta = H.stream(name)
-    maps = H.synthetic_pbr_maps()
+    maps = _maps(maps_kind)
     player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, H.mesh(meta)))
     for kind, sampler in H.PBR_SAMPLERS.items():
         player.textures[sampler] = bp.Texture(engine, maps[kind], name=kind)
@@ -519,3 +530,117 @@ def test_long_accumulation_bitexact(engine, name):
     gc = engine.read_canvas(player.width, player.height)
     assert _bits_equal(ref_acc[-1], ga), _diff_report(ref_acc[-1], ga)
     assert _bits_equal(ref_can[-1], gc), _diff_report(ref_can[-1], gc)
+
+
+# ------------------------------------------------------------------------- BASELINE configs[4]
+# The physical-sky scene with the glTF model block in its SceneIntersect (PT_PROG_SKY_MESH,
+# DESIGN.md §1), on the 524,288-triangle dragon stand-in.
+
+_DRAGON = {}
+
+
+def _dragon():
+    if "m" not in _DRAGON:
+        _DRAGON["m"] = H.synthetic_dragon()
+    return _DRAGON["m"]
+
+
+@pytest.mark.parametrize("material", [3, 4, 2, 1])
+def test_sky_mesh_bitexact_and_counters(engine, backend, material):
+    """Sky + dragon composite under each model material (Metal = the page default, ClearCoat_Diffuse,
+    Transparent, Diffuse): the sky's CalculateRadiance with mesh hits, shadow rays toward the sun
+    lobe through the BVH, double-sided leaves for Transparent; accumulation, canvas and the
+    algorithmic-byte counters equal the oracle's on every schedule and BVH layout."""
+    meta = H.sky_mesh_stream(material)
+    mesh = _dragon()
+    ref_acc, ref_can, ref_cnt = H.oracle_replay(meta, None, width=320, height=180, with_output=True, mesh=mesh)
+    engine.set_counting(True)
+    engine.reset_counters()
+    try:
+        got_acc, got_can, _ = _replay_gpu(engine, meta, None, 320, 180, mesh=mesh)
+        cnt = engine.counters()
+    finally:
+        engine.set_counting(False)
+    assert engine.bvh_layout_used() == backend[1]
+    for i, (ra, ga, rc, gc) in enumerate(zip(ref_acc, got_acc, ref_can, got_can)):
+        assert _bits_equal(ra, ga), "frame %d accumulation: %s" % (i, _diff_report(ra, ga))
+        assert _bits_equal(rc, gc), "frame %d canvas: %s" % (i, _diff_report(rc, gc))
+    assert cnt == {k: sum(c[k] for c in ref_cnt) for k in ref_cnt[0]}
+    assert sum(c["hit_lookups"] for c in ref_cnt) > 0
+
+
+def test_sky_mesh_effect_from_shader_text(engine):
+    """The composite is recognised from its fragment source: the sky shader text with the glTF
+    model's samplers declared -> PT_PROG_SKY_MESH; the sky shader alone stays PT_PROG_SKY."""
+    import babylon_pt as bp
+    sky = "#include<pathtracing_physical_sky_functions>\nvoid main(){}\n#include<pathtracing_default_main>"
+    comp = "uniform sampler2D tAABBTexture;\nuniform sampler2D tTriangleTexture;\n" + sky
+    assert bp.EffectWrapper(engine, sky, [], [], "sky").program() == bp.PROG["sky"]
+    assert bp.EffectWrapper(engine, comp, [], [], "comp").program() == bp.PROG["skymesh"]
+
+
+def test_sky_mesh_4k_eight_bands_bitexact(engine):
+    """BASELINE configs[4] at its size: 3840x2160, rendered as the 8 band partitions of an 8-GPU
+    node, copied full-frame and output band by band - bit-exact with the oracle's whole-frame
+    render over the recorded frames (history clear, moving-camera blend, still camera)."""
+    meta = H.sky_mesh_stream()
+    mesh = _dragon()
+    W, Hh = 3840, 2160
+    ref_acc, ref_can, _ = H.oracle_replay(meta, None, width=W, height=Hh, with_output=True, mesh=mesh)
+    got_acc, got_can, _ = _replay_gpu(engine, meta, None, W, Hh, parts=8, split_output=True, mesh=mesh)
+    for i, (ra, ga, rc, gc) in enumerate(zip(ref_acc, got_acc, ref_can, got_can)):
+        assert ra.shape == (Hh, W, 4)
+        assert _bits_equal(ra, ga), "frame %d accumulation: %s" % (i, _diff_report(ra, ga))
+        assert _bits_equal(rc, gc), "frame %d canvas: %s" % (i, _diff_report(rc, gc))
+
+
+def test_sky_mesh_converges_1024_frames_bitexact(engine):
+    """configs[4]'s converged run at a reduced size: 1024 progressive frames (the 3 recorded ones,
+    then the render loop's still-camera frames) through pathTracing -> screenCopy -> screenOutput;
+    the accumulation after frame 1024 and the 5x5-filtered canvas at uSampleCounter = 1024 are
+    bit-exact with the oracle's."""
+    import ptoracle as po
+    import babylon_pt as bp
+    meta = H.sky_mesh_stream()
+    mesh = _dragon()
+    W, Hh, N = 128, 72, 1024
+    player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, mesh), W, Hh)
+    engine.resize_canvas(W, Hh)
+    frames = meta["frames"] + [player.synth_frame(k) for k in range(N - len(meta["frames"]))]
+    sc = H.oracle_scene(meta, W, Hh, mesh)
+    acc = np.zeros((Hh, W, 4), np.float32)
+    for f in frames:
+        acc, _ = sc.path_trace(H.with_resolution(H.path_call(f)["uniforms"], W, Hh), acc)
+        for c in f:
+            player.play_call(c)
+    engine.sync()
+    ou = H.output_call(frames[-1])["uniforms"]
+    assert ou["uOneOverSampleCounter"][1][0] == np.float32(1.0 / N)
+    want = po.screen_output(acc, ou["uOneOverSampleCounter"][1][0], ou.get("uToneMappingExposure", ["f", [1.0]])[1][0])
+    ga = player.textures["pathTracingRenderTarget"].read()
+    gc = engine.read_canvas(W, Hh)
+    assert _bits_equal(acc, ga), _diff_report(acc, ga)
+    assert _bits_equal(want, gc), _diff_report(want, gc)
+
+
+def test_helmet_real_maps_1080p_bitexact(engine):
+    """BASELINE configs[2] at its size: DamagedHelmet in the HDRI scene at 1920x1080 with the four
+    real PBR maps bound, 3 recorded frames, accumulation and canvas bit-exact."""
+    import babylon_pt as bp
+    meta = H.stream("hdri_helmet_320x180")
+    maps = _maps("real")
+    W, Hh = 1920, 1080
+    player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, H.mesh(meta)), W, Hh)
+    for kind, sampler in H.PBR_SAMPLERS.items():
+        player.textures[sampler] = bp.Texture(engine, maps[kind], name=kind)
+    engine.resize_canvas(W, Hh)
+    got_acc, got_can = [], []
+    for i in range(3):
+        player.play_frame(i)
+        engine.sync()
+        got_acc.append(player.textures["pathTracingRenderTarget"].read())
+        got_can.append(engine.read_canvas(W, Hh))
+    ref_acc, ref_can, _ = H.oracle_replay(meta, 3, width=W, height=Hh, with_output=True, maps=maps)
+    for i in range(3):
+        assert _bits_equal(ref_acc[i], got_acc[i]), "frame %d: %s" % (i, _diff_report(ref_acc[i], got_acc[i]))
+        assert _bits_equal(ref_can[i], got_can[i]), "frame %d canvas: %s" % (i, _diff_report(ref_can[i], got_can[i]))

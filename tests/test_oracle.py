@@ -280,3 +280,23 @@ def test_screen_output_bypass_thresholds():
     assert px(acc, 201, 12, 12) == px(other, 201, 12, 12)     # sharp-pixel bypass
     assert px(acc, 4999, 12, 6) != px(other, 4999, 12, 6)
     assert px(acc, 5001, 12, 6) == px(other, 5001, 12, 6)     # full bypass
+
+
+def test_sky_mesh_composite_is_the_sky_scene_plus_the_model():
+    """PTO_SCENE_SKYMESH (BASELINE configs[4]) = the physical-sky program with the glTF model block
+    appended to SceneIntersect: with the model moved out of every ray's reach the image is the sky
+    scene's, bit for bit (same SetupScene, same radiance, same rng draws); with the model in view the
+    model's pixels change and the walk is counted."""
+    meta_sky = H.stream("sky_256")
+    tiny = H.synthetic_dragon(32, 32)
+    far = list(H.SKY_MESH_MODEL_INV)
+    far[13] = -1.0e5                                         # model space = world shifted by 1e5 in y
+    meta_far = H.sky_mesh_stream(model_inv=far)
+    sky, _, _ = H.oracle_replay(meta_sky, 2, width=96, height=64)
+    comp, _, cnt = H.oracle_replay(meta_far, 2, width=96, height=64, mesh=tiny)
+    for a, b in zip(sky, comp):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert cnt[0]["hit_lookups"] == 0
+    near, _, cnt = H.oracle_replay(H.sky_mesh_stream(), 2, width=96, height=64, mesh=tiny)
+    assert cnt[0]["hit_lookups"] > 0 and cnt[0]["node_fetches"] > 0
+    assert (near[-1] != sky[-1]).any(-1).mean() > 0.01

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Minimal profiling driver: K frames of a recorded stream (default: the bench workload, StanfordBunny
-1920x1080) through libpt, no counting kernels, no CPU work — for rocprofv3 --pmc / --kernel-trace."""
+"""Minimal profiling driver: K frames of a bench workload (or of a recorded stream) through libpt,
+no counting kernels, no CPU work — the program under rocprofv3 --pmc / --kernel-trace (tools/gpu_pmc.sh,
+and bench.py's live HBM-traffic passes). Never imports torch."""
 import argparse
 import os
 import sys
@@ -13,20 +14,31 @@ import babylon_pt as bp  # noqa: E402
 import helpers as H      # noqa: E402
 
 ap = argparse.ArgumentParser()
+ap.add_argument("--workload", default=None, choices=sorted(H.WORKLOADS), help="a bench.py workload")
 ap.add_argument("--stream", default="gltf_bunny_1080p")
 ap.add_argument("--frames", type=int, default=10)
 ap.add_argument("--width", type=int, default=0)
 ap.add_argument("--height", type=int, default=0)
 ap.add_argument("--dragon", action="store_true", help="the StanfordDragon stand-in mesh instead of the stream's")
 a = ap.parse_args()
-meta = H.stream(a.stream)
+maps = None
+if a.workload:
+    meta, mesh_arrays, maps, (W, Hh) = H.workload(a.workload)
+    a.width, a.height = a.width or W, a.height or Hh
+else:
+    meta = H.stream(a.stream)
+    mesh_arrays = H.synthetic_dragon() if a.dragon else (H.mesh(meta) if meta["scene"] in ("gltf", "hdri") else None)
 e = bp.Engine(0)
-mesh = H.texture_payloads(meta, H.synthetic_dragon() if a.dragon else H.mesh(meta)) if meta["scene"] in ("gltf", "hdri") else None
+mesh = H.texture_payloads(meta, mesh_arrays) if mesh_arrays is not None else None
 p = bp.StreamPlayer(e, meta, H.bluenoise(), mesh, a.width or None, a.height or None)
+if maps:
+    for kind, sampler in H.PBR_SAMPLERS.items():
+        p.textures[sampler] = bp.Texture(e, maps[kind], name=kind)
+e.resize_canvas(p.width, p.height)
 for k in range(a.frames):
     for call in p.synth_frame(k):
         p.play_call(call)
 e.sync()
-print("ok", a.stream, a.frames)
+print("ok", a.workload or a.stream, a.frames)
 if os.environ.get("PT_QSTATS"):
     print("queue stats:", e.queue_stats())
