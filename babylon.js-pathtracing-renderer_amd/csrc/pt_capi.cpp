@@ -1,10 +1,12 @@
-// pt_capi.cpp — the C ABI of libpt.so (include/pt.h): contexts, effects, textures, render
-// targets and draws, mirroring the Babylon effect API the reference's setup scripts call.
+// pt_capi.cpp — one device's part of a libpt context (pt_dev.h): contexts, effects, textures,
+// render targets and draws on one HIP stream of one gfx950 device, mirroring the Babylon effect API
+// the reference's setup scripts call. The exported C ABI (include/pt.h, pt_group.cpp) drives one
+// such part per device of a context and fans every call out over them.
 //
-// What happens on pt_render(effect, target), per recognised program:
+// What happens on dev_render(effect, target), per recognised program:
 //   CORNELL / GLTF  -> uniforms resolved by name, SetupScene() evaluated once on the host with the
 //                      same IEEE ops as the GLSL, one pt_trace launch over the 16-row bands this
-//                      context owns (pt_set_row_partition);
+//                      context owns (dev_set_row_partition);
 //   SCREEN_COPY     -> pt_copy over the owned bands;
 //   SCREEN_OUTPUT   -> pt_output into the canvas (RGBA8) or an RGBA32F target.
 // Everything is enqueued on the context's stream; HIP events bracket every draw for timing.
@@ -23,6 +25,7 @@
 #include <vector>
 
 #include "pt_args.h"
+#include "pt_dev.h"
 
 extern "C" {
 hipError_t pt_launch_exhaustive(int op, unsigned long long* bad, hipStream_t s);
@@ -56,15 +59,15 @@ struct Uniform {
 
 }  // namespace
 
-struct pt_texture {
-    pt_ctx* ctx = nullptr;
+struct DevTex {
+    Dev* ctx = nullptr;
     int kind = TEX_F32;
     int w = 0, h = 0;
     void* d = nullptr;
     size_t bytes = 0;
     int sampling = PT_SAMPLING_NEAREST;
     int invert_y = 0;
-    bool external = false;   // caller-owned device memory (pt_render_target_wrap)
+    bool external = false;   // caller-owned device memory (dev_render_target_wrap)
     unsigned long long gen = 0;   // bumped by every host write of the texels
     // child-pair BVH records derived from this texture and the triangle texture drawn with it
     // (pt_pairs_* passes), valid while both keep the generations they were built from
@@ -73,22 +76,22 @@ struct pt_texture {
     const float4* pairs_leaf = nullptr;
     uint32_t pairs_root = 0;
     uint32_t pairs_inner_bytes = 0, pairs_leaf_bytes = 0;
-    const pt_texture* pairs_tri = nullptr;
+    const DevTex* pairs_tri = nullptr;
     unsigned long long pairs_gen = ~0ull, pairs_tri_gen = ~0ull;
     bool pairs_ok = false;
 };
 
-struct pt_effect {
-    pt_ctx* ctx = nullptr;
+struct DevFx {
+    Dev* ctx = nullptr;
     int prog = PT_PROG_UNKNOWN;
     std::unordered_map<std::string, Uniform> uniforms;
-    std::unordered_map<std::string, pt_texture*> samplers;
+    std::unordered_map<std::string, DevTex*> samplers;
 };
 
-struct pt_ctx {
+struct Dev {
     int device = 0;
     hipStream_t stream = nullptr;      // the stream all work is enqueued on
-    hipStream_t own_stream = nullptr;  // the context's own stream (pt_set_stream(NULL) restores it)
+    hipStream_t own_stream = nullptr;  // the context's own stream (dev_set_stream(NULL) restores it)
     std::string err;
     uchar4* canvas = nullptr;
     int cw = 0, ch = 0;
@@ -99,8 +102,8 @@ struct pt_ctx {
     bool output_partition = false;
     // screenCopy deferred to ride along with the next screenOutput of the same source (flushed as
     // its own kernel before anything else could observe the target: flush_copy)
-    struct { bool on; pt_texture* src; pt_texture* dst; int num_parts, part; } pending_copy = {};
-    bool canvas_external = false;     // pt_canvas_wrap: caller-owned canvas memory
+    struct { bool on; DevTex* src; DevTex* dst; int num_parts, part; } pending_copy = {};
+    bool canvas_external = false;     // dev_canvas_wrap: caller-owned canvas memory
     int backend = PT_BACKEND_MEGAKERNEL;
     int bvh_layout = PT_BVH_PAIRS;
     int bvh_used = -1;
@@ -130,19 +133,19 @@ struct pt_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
     std::vector<std::pair<int, int>> window_draws;   // (program, pool index)
     int pending = -1;
-    std::set<pt_texture*> textures;
-    std::set<pt_effect*> effects;
+    std::set<DevTex*> textures;
+    std::set<DevFx*> effects;
 };
 
 namespace {
 
-int fail(pt_ctx* c, int code, const std::string& msg)
+int fail(Dev* c, int code, const std::string& msg)
 {
     if (c) c->err = msg;
     return code;
 }
 
-int hipfail(pt_ctx* c, hipError_t e, const char* what)
+int hipfail(Dev* c, hipError_t e, const char* what)
 {
     return fail(c, PT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -171,7 +174,7 @@ int classify(const char* src)
     return PT_PROG_UNKNOWN;
 }
 
-float uf(const pt_effect* fx, const char* name, int k = 0)
+float uf(const DevFx* fx, const char* name, int k = 0)
 {
     auto it = fx->uniforms.find(name);
     if (it == fx->uniforms.end() || !it->second.set) return 0.0f;   // GLSL uniforms default to 0
@@ -179,24 +182,24 @@ float uf(const pt_effect* fx, const char* name, int k = 0)
     if (u.is_int) return (float)u.i;
     return k < u.n ? u.f[k] : 0.0f;
 }
-int ui(const pt_effect* fx, const char* name)
+int ui(const DevFx* fx, const char* name)
 {
     auto it = fx->uniforms.find(name);
     if (it == fx->uniforms.end() || !it->second.set) return 0;
     const Uniform& u = it->second;
     return u.is_int ? u.i : (int)u.f[0];
 }
-void um4(const pt_effect* fx, const char* name, ptg::m4& m)
+void um4(const DevFx* fx, const char* name, ptg::m4& m)
 {
     for (int k = 0; k < 16; k++) m.m[k] = uf(fx, name, k);
 }
-pt_texture* sampler(const pt_effect* fx, const char* name)
+DevTex* sampler(const DevFx* fx, const char* name)
 {
     auto it = fx->samplers.find(name);
     return it == fx->samplers.end() ? nullptr : it->second;
 }
 
-pt::Tex8 tex8(const pt_texture* t)
+pt::Tex8 tex8(const DevTex* t)
 {
     pt::Tex8 r{ nullptr, 0, 0 };
     if (t && t->kind == TEX_U8) { r.p = (const uchar4*)t->d; r.w = t->w; r.h = t->h; }
@@ -218,7 +221,7 @@ float hdist(ptg::f3 a, ptg::f3 b)
 
 // The uniform-only terms of Get_Sky_Color (js/PathTracingCommon.js:373-475) with the pinned
 // sequences of pt_glsl.h, once per draw instead of once per sky sample
-void sky_setup(const pt_effect* fx, pt::SkyArgs& k)
+void sky_setup(const DevFx* fx, pt::SkyArgs& k)
 {
     using namespace ptg;
     k.sun = v3(uf(fx, "uSunDirection", 0), uf(fx, "uSunDirection", 1), uf(fx, "uSunDirection", 2));
@@ -237,7 +240,7 @@ void sky_setup(const pt_effect* fx, pt::SkyArgs& k)
 
 // SetupScene() of js/BabylonPathTracing_FragmentShader.js:348-378 and
 // js/GLTFModelPathTracing_FragmentShader.js:613-643, evaluated once per draw.
-void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
+void setup_scene(const DevFx* fx, pt::TraceArgs& a)
 {
     const float W = 50.0f;
     const float L = uf(fx, "uQuadLightRadius") * 0.2f;
@@ -303,19 +306,19 @@ void setup_scene(const pt_effect* fx, pt::TraceArgs& a)
         a.hdr_exposure = uf(fx, "uHDRExposure");
         const float p = uf(fx, "uSunPower");
         a.sun_weight = p * p * 0.0000001f;
-        const pt_texture* h = sampler(fx, "tHDRTexture");
+        const DevTex* h = sampler(fx, "tHDRTexture");
         if (h && h->kind != TEX_U8) { a.hdr.p = (const float4*)h->d; a.hdr.w = h->w; a.hdr.h = h->h; }
     }
 }
 
-int bands_owned(const pt_ctx* c, int height)
+int bands_owned(const Dev* c, int height)
 {
     int nb = (height + pt::kTile - 1) / pt::kTile;
     if (c->part >= nb) return 0;
     return (nb - c->part + c->num_parts - 1) / c->num_parts;
 }
 
-int begin_draw(pt_ctx* c, int prog)
+int begin_draw(Dev* c, int prog)
 {
     if (!c->ev0[prog]) {
         HIPCHK(c, hipEventCreate(&c->ev0[prog]));
@@ -335,7 +338,7 @@ int begin_draw(pt_ctx* c, int prog)
     }
     return PT_OK;
 }
-int end_draw(pt_ctx* c, int prog)
+int end_draw(Dev* c, int prog)
 {
     HIPCHK(c, hipEventRecord(c->ev1[prog], c->stream));
     c->ev_used[prog] = true;
@@ -346,7 +349,7 @@ int end_draw(pt_ctx* c, int prog)
 
 // (re)allocate the wavefront buffers for `tiles` 16x16 tiles of a wq x hq quad-rounded frame and
 // a persistent grid of `blocks` blocks: one slab, carved into the WfBufs arrays
-int wf_reserve(pt_ctx* c, int wq, int hq, int tiles, int blocks)
+int wf_reserve(Dev* c, int wq, int hq, int tiles, int blocks)
 {
     const unsigned cap = (unsigned)((tiles + pt::kShards - 1) / pt::kShards) * pt::kBlock;
     const size_t slots = (size_t)cap * pt::kShards;
@@ -377,7 +380,7 @@ int wf_reserve(pt_ctx* c, int wq, int hq, int tiles, int blocks)
     return PT_OK;
 }
 
-int spill_reserve(pt_ctx* c, size_t lanes)
+int spill_reserve(Dev* c, size_t lanes)
 {
     if (lanes <= c->mk_spill_lanes) return PT_OK;
     if (c->mk_spill) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->mk_spill)); c->mk_spill = nullptr; }
@@ -387,7 +390,7 @@ int spill_reserve(pt_ctx* c, size_t lanes)
     return PT_OK;
 }
 
-int gb_reserve(pt_ctx* c, int wq, int hq)
+int gb_reserve(Dev* c, int wq, int hq)
 {
     const size_t pixels = (size_t)wq * hq;
     if (pixels > c->gb_pixels) {
@@ -408,7 +411,7 @@ int gb_reserve(pt_ctx* c, int wq, int hq)
 // when either texture's texels changed since the last build. Only for data textures (their
 // texels change only through this API) of at most 2^24 texels (node ids and ranks exact in
 // float). Returns false when the reference walk must be used. One host round trip per build.
-bool ensure_pairs(pt_ctx* c, pt_texture* t, const pt_texture* tri, int* rc)
+bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
 {
     *rc = PT_OK;
     const long long texels = (long long)t->w * t->h;
@@ -472,12 +475,12 @@ bool ensure_pairs(pt_ctx* c, pt_texture* t, const pt_texture* tri, int* rc)
     return t->pairs_ok;
 }
 
-int render_trace(pt_effect* fx, pt_texture* target)
+int render_trace(DevFx* fx, DevTex* target)
 {
-    pt_ctx* c = fx->ctx;
+    Dev* c = fx->ctx;
     if (!target || target->kind != TEX_RT) return fail(c, PT_ERR_ARG, "path tracing draws need a render target");
-    pt_texture* prev = sampler(fx, "previousBuffer");
-    pt_texture* bn = sampler(fx, "blueNoiseTexture");
+    DevTex* prev = sampler(fx, "previousBuffer");
+    DevTex* bn = sampler(fx, "blueNoiseTexture");
     if (!prev || prev->kind == TEX_U8 || prev->w != target->w || prev->h != target->h)
         return fail(c, PT_ERR_STATE, "previousBuffer must be an RGBA32F texture of the target's size");
     if (!bn || bn->kind != TEX_U8) return fail(c, PT_ERR_STATE, "blueNoiseTexture must be bound (RGBA8)");
@@ -502,8 +505,8 @@ int render_trace(pt_effect* fx, pt_texture* target)
     a.bluenoise = tex8(bn);
     const bool mesh = fx->prog == PT_PROG_GLTF || fx->prog == PT_PROG_HDRI || fx->prog == PT_PROG_SKY_MESH;
     if (mesh) {
-        pt_texture* bvh = sampler(fx, "tAABBTexture");
-        pt_texture* tri = sampler(fx, "tTriangleTexture");
+        DevTex* bvh = sampler(fx, "tAABBTexture");
+        DevTex* tri = sampler(fx, "tTriangleTexture");
         if (!bvh || !tri || bvh->kind != TEX_F32 || tri->kind != TEX_F32)
             return fail(c, PT_ERR_STATE, "tAABBTexture / tTriangleTexture must be bound RGBA32F data textures");
         um4(fx, "uGLTF_Model_InvMatrix", a.model);
@@ -600,7 +603,7 @@ int render_trace(pt_effect* fx, pt_texture* target)
     return end_draw(c, fx->prog);
 }
 
-int launch_copy(pt_ctx* c, pt_texture* src, pt_texture* dst, int num_parts, int part)
+int launch_copy(Dev* c, DevTex* src, DevTex* dst, int num_parts, int part)
 {
     pt::CopyArgs a{ dst->w, dst->h, num_parts, part, (const float4*)src->d, (float4*)dst->d };
     const int nb = (dst->h + pt::kTile - 1) / pt::kTile;
@@ -610,7 +613,7 @@ int launch_copy(pt_ctx* c, pt_texture* src, pt_texture* dst, int num_parts, int 
 }
 
 // run a deferred screenCopy now, as its own kernel (timed as a screenCopy draw)
-int flush_copy(pt_ctx* c)
+int flush_copy(Dev* c)
 {
     if (!c->pending_copy.on) return PT_OK;
     c->pending_copy.on = false;
@@ -621,10 +624,10 @@ int flush_copy(pt_ctx* c)
     return end_draw(c, PT_PROG_SCREEN_COPY);
 }
 
-int render_copy(pt_effect* fx, pt_texture* target)
+int render_copy(DevFx* fx, DevTex* target)
 {
-    pt_ctx* c = fx->ctx;
-    pt_texture* src = sampler(fx, "pathTracedImageBuffer");
+    Dev* c = fx->ctx;
+    DevTex* src = sampler(fx, "pathTracedImageBuffer");
     if (!target || target->kind != TEX_RT) return fail(c, PT_ERR_ARG, "screenCopy needs a render target");
     if (!src || src->kind == TEX_U8 || src->w != target->w || src->h != target->h)
         return fail(c, PT_ERR_STATE, "pathTracedImageBuffer must be an RGBA32F texture of the target's size");
@@ -636,10 +639,10 @@ int render_copy(pt_effect* fx, pt_texture* target)
     return PT_OK;
 }
 
-int render_output(pt_effect* fx, pt_texture* target)
+int render_output(DevFx* fx, DevTex* target)
 {
-    pt_ctx* c = fx->ctx;
-    pt_texture* acc = sampler(fx, "accumulationBuffer");
+    Dev* c = fx->ctx;
+    DevTex* acc = sampler(fx, "accumulationBuffer");
     if (!acc || acc->kind == TEX_U8) return fail(c, PT_ERR_STATE, "accumulationBuffer must be an RGBA32F texture");
     pt::OutputArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -663,7 +666,7 @@ int render_output(pt_effect* fx, pt_texture* target)
         a.width = target->w; a.height = target->h; a.out_f = (float4*)target->d;
     } else {
         if (c->cw == 0 && c->ch == 0) {
-            int rc = pt_canvas_resize(c, acc->w, acc->h);
+            int rc = dev_canvas_resize(c, acc->w, acc->h);
             if (rc) return rc;
         }
         a.width = c->cw; a.height = c->ch; a.canvas = c->canvas;
@@ -674,9 +677,9 @@ int render_output(pt_effect* fx, pt_texture* target)
     return end_draw(c, fx->prog);
 }
 
-pt_texture* new_texture(pt_ctx* c, int kind, int w, int h, size_t texel, int* err)
+DevTex* new_texture(Dev* c, int kind, int w, int h, size_t texel, int* err)
 {
-    auto* t = new pt_texture();
+    auto* t = new DevTex();
     t->ctx = c; t->kind = kind; t->w = w; t->h = h;
     t->bytes = (size_t)w * (size_t)h * texel;
     if (t->bytes) {
@@ -692,12 +695,12 @@ pt_texture* new_texture(pt_ctx* c, int kind, int w, int h, size_t texel, int* er
     return t;
 }
 
-pt_texture* upload(pt_ctx* c, int kind, int w, int h, const void* data, size_t texel, int sampling, int invert_y, int* err)
+DevTex* upload(Dev* c, int kind, int w, int h, const void* data, size_t texel, int sampling, int invert_y, int* err)
 {
     if (err) *err = PT_OK;
     if (!c || w <= 0 || h <= 0 || (long long)w * h >= (1ll << 31)) { if (err) *err = PT_ERR_ARG; return nullptr; }
     hipSetDevice(c->device);
-    pt_texture* t = new_texture(c, kind, w, h, texel, err);
+    DevTex* t = new_texture(c, kind, w, h, texel, err);
     if (!t) return nullptr;
     t->sampling = sampling; t->invert_y = invert_y;
     hipError_t e = hipSuccess;
@@ -712,7 +715,7 @@ pt_texture* upload(pt_ctx* c, int kind, int w, int h, const void* data, size_t t
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);   // the caller keeps ownership of data
     if (e != hipSuccess) {
         hipfail(c, e, "texture upload");
-        pt_texture_destroy(t);
+        dev_texture_destroy(t);
         if (err) *err = PT_ERR_HIP;
         return nullptr;
     }
@@ -721,11 +724,10 @@ pt_texture* upload(pt_ctx* c, int kind, int w, int h, const void* data, size_t t
 
 }  // namespace
 
-extern "C" {
+// ---------------------------------------------------------------------------- device-level API
+// (pt_dev.h; the exported C ABI in pt_group.cpp forwards here, once per part of a context)
 
-const char* pt_version(void) { return "libpt 0.1.0 gfx950"; }
-
-pt_ctx* pt_ctx_create(int device, int* err)
+Dev* dev_ctx_create(int device, int* err)
 {
     if (err) *err = PT_OK;
     int n = 0;
@@ -738,7 +740,7 @@ pt_ctx* pt_ctx_create(int device, int* err)
         if (err) *err = PT_ERR_DEVICE;   // the code objects are gfx950-only
         return nullptr;
     }
-    auto* c = new pt_ctx();
+    auto* c = new Dev();
     c->device = device;
     c->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (const char* v = std::getenv("PT_PERSIST_TILES")) c->persist_tiles = (unsigned)std::max(1, std::atoi(v));
@@ -753,22 +755,22 @@ pt_ctx* pt_ctx_create(int device, int* err)
     if (e == hipSuccess) e = hipMemset(c->d_counters, 0, pt::C_NUM * sizeof(unsigned long long));
     if (e != hipSuccess) {
         if (err) *err = PT_ERR_HIP;
-        pt_ctx_destroy(c);
+        dev_ctx_destroy(c);
         return nullptr;
     }
     return c;
 }
 
-void pt_ctx_destroy(pt_ctx* c)
+void dev_ctx_destroy(Dev* c)
 {
     if (!c) return;
     hipSetDevice(c->device);
     c->pending_copy.on = false;   // nothing can observe its target any more
     if (c->stream) hipStreamSynchronize(c->stream);
-    std::vector<pt_effect*> fx(c->effects.begin(), c->effects.end());
-    for (auto* f : fx) pt_effect_destroy(f);
-    std::vector<pt_texture*> tx(c->textures.begin(), c->textures.end());
-    for (auto* t : tx) pt_texture_destroy(t);
+    std::vector<DevFx*> fx(c->effects.begin(), c->effects.end());
+    for (auto* f : fx) dev_effect_destroy(f);
+    std::vector<DevTex*> tx(c->textures.begin(), c->textures.end());
+    for (auto* t : tx) dev_texture_destroy(t);
     for (auto& pr : c->pool) { hipEventDestroy(pr.first); hipEventDestroy(pr.second); }
     for (int i = 0; i < kProgSlots; i++) {
         if (c->ev0[i]) hipEventDestroy(c->ev0[i]);
@@ -785,9 +787,9 @@ void pt_ctx_destroy(pt_ctx* c)
     delete c;
 }
 
-const char* pt_last_error(pt_ctx* c) { return c ? c->err.c_str() : "no context"; }
+const char* dev_last_error(Dev* c) { return c ? c->err.c_str() : "no context"; }
 
-int pt_sync(pt_ctx* c)
+int dev_sync(Dev* c)
 {
     if (!c) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -802,7 +804,7 @@ int pt_sync(pt_ctx* c)
     return PT_OK;
 }
 
-int pt_canvas_resize(pt_ctx* c, int w, int h)
+int dev_canvas_resize(Dev* c, int w, int h)
 {
     if (!c || w < 0 || h < 0) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -821,7 +823,7 @@ int pt_canvas_resize(pt_ctx* c, int w, int h)
     return PT_OK;
 }
 
-int pt_canvas_wrap(pt_ctx* c, int w, int h, void* ptr)
+int dev_canvas_wrap(Dev* c, int w, int h, void* ptr)
 {
     if (!c || w <= 0 || h <= 0 || !ptr) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -835,14 +837,14 @@ int pt_canvas_wrap(pt_ctx* c, int w, int h, void* ptr)
     return PT_OK;
 }
 
-int pt_set_output_partition(pt_ctx* c, int enable)
+int dev_set_output_partition(Dev* c, int enable)
 {
     if (!c) return PT_ERR_ARG;
     c->output_partition = enable != 0;
     return PT_OK;
 }
 
-pt_effect* pt_effect_create(pt_ctx* c, const char* src, const char* const* un, int nu, const char* const* sn, int ns, int* err)
+DevFx* dev_effect_create(Dev* c, const char* src, const char* const* un, int nu, const char* const* sn, int ns, int* err)
 {
     if (err) *err = PT_OK;
     if (!c || !src) { if (err) *err = PT_ERR_ARG; return nullptr; }
@@ -852,14 +854,14 @@ pt_effect* pt_effect_create(pt_ctx* c, const char* src, const char* const* un, i
         if (err) *err = PT_ERR_SHADER;
         return nullptr;
     }
-    return pt_effect_create_program(c, prog, un, nu, sn, ns, err);
+    return dev_effect_create_program(c, prog, un, nu, sn, ns, err);
 }
 
-pt_effect* pt_effect_create_program(pt_ctx* c, int prog, const char* const* un, int nu, const char* const* sn, int ns, int* err)
+DevFx* dev_effect_create_program(Dev* c, int prog, const char* const* un, int nu, const char* const* sn, int ns, int* err)
 {
     if (err) *err = PT_OK;
     if (!c || nu < 0 || ns < 0 || prog <= PT_PROG_UNKNOWN || prog > PT_PROG_SKY_MESH) { if (err) *err = PT_ERR_ARG; return nullptr; }
-    auto* fx = new pt_effect();
+    auto* fx = new DevFx();
     fx->ctx = c;
     fx->prog = prog;
     for (int i = 0; i < nu; i++) if (un && un[i]) fx->uniforms[un[i]] = Uniform();
@@ -868,16 +870,16 @@ pt_effect* pt_effect_create_program(pt_ctx* c, int prog, const char* const* un, 
     return fx;
 }
 
-void pt_effect_destroy(pt_effect* fx)
+void dev_effect_destroy(DevFx* fx)
 {
     if (!fx) return;
     fx->ctx->effects.erase(fx);
     delete fx;
 }
 
-int pt_effect_program(const pt_effect* fx) { return fx ? fx->prog : PT_PROG_UNKNOWN; }
+int dev_effect_program(const DevFx* fx) { return fx ? fx->prog : PT_PROG_UNKNOWN; }
 
-int pt_set_float(pt_effect* fx, const char* name, const float* v, int n)
+int dev_set_float(DevFx* fx, const char* name, const float* v, int n)
 {
     if (!fx || !name || !v || n < 1 || n > 16) return PT_ERR_ARG;
     auto it = fx->uniforms.find(name);
@@ -888,7 +890,7 @@ int pt_set_float(pt_effect* fx, const char* name, const float* v, int n)
     return PT_OK;
 }
 
-int pt_set_int(pt_effect* fx, const char* name, int v)
+int dev_set_int(DevFx* fx, const char* name, int v)
 {
     if (!fx || !name) return PT_ERR_ARG;
     auto it = fx->uniforms.find(name);
@@ -898,7 +900,7 @@ int pt_set_int(pt_effect* fx, const char* name, int v)
     return PT_OK;
 }
 
-int pt_set_texture(pt_effect* fx, const char* name, pt_texture* t)
+int dev_set_texture(DevFx* fx, const char* name, DevTex* t)
 {
     if (!fx || !name) return PT_ERR_ARG;
     if (t && t->ctx != fx->ctx) return fail(fx->ctx, PT_ERR_ARG, "texture belongs to another context");
@@ -908,26 +910,26 @@ int pt_set_texture(pt_effect* fx, const char* name, pt_texture* t)
     return PT_OK;
 }
 
-pt_texture* pt_texture_create_rgba32f(pt_ctx* c, int w, int h, const float* data, int sampling, int invert_y, int* err)
+DevTex* dev_texture_create_rgba32f(Dev* c, int w, int h, const float* data, int sampling, int invert_y, int* err)
 {
     return upload(c, TEX_F32, w, h, data, 16, sampling, invert_y, err);
 }
 
-pt_texture* pt_texture_create_rgba8(pt_ctx* c, int w, int h, const uint8_t* data, int sampling, int invert_y, int* err)
+DevTex* dev_texture_create_rgba8(Dev* c, int w, int h, const uint8_t* data, int sampling, int invert_y, int* err)
 {
     return upload(c, TEX_U8, w, h, data, 4, sampling, invert_y, err);
 }
 
-pt_texture* pt_render_target_create(pt_ctx* c, int w, int h, int* err)
+DevTex* dev_render_target_create(Dev* c, int w, int h, int* err)
 {
     return upload(c, TEX_RT, w, h, nullptr, 16, PT_SAMPLING_NEAREST, 0, err);
 }
 
-pt_texture* pt_render_target_wrap(pt_ctx* c, int w, int h, void* dptr, int* err)
+DevTex* dev_render_target_wrap(Dev* c, int w, int h, void* dptr, int* err)
 {
     if (err) *err = PT_OK;
     if (!c || w <= 0 || h <= 0 || !dptr) { if (err) *err = PT_ERR_ARG; return nullptr; }
-    auto* t = new pt_texture();
+    auto* t = new DevTex();
     t->ctx = c; t->kind = TEX_RT; t->w = w; t->h = h;
     t->bytes = (size_t)w * h * 16;
     t->d = dptr;
@@ -936,11 +938,11 @@ pt_texture* pt_render_target_wrap(pt_ctx* c, int w, int h, void* dptr, int* err)
     return t;
 }
 
-int pt_render_target_resize(pt_texture* t, int w, int h)
+int dev_render_target_resize(DevTex* t, int w, int h)
 {
     if (!t || t->kind != TEX_RT || w <= 0 || h <= 0) return PT_ERR_ARG;
     if (t->external) return fail(t->ctx, PT_ERR_ARG, "wrapped render targets are not resizable");
-    pt_ctx* c = t->ctx;
+    Dev* c = t->ctx;
     if (w == t->w && h == t->h) return PT_OK;
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = flush_copy(c)) return rc;
@@ -953,7 +955,7 @@ int pt_render_target_resize(pt_texture* t, int w, int h)
     return PT_OK;
 }
 
-int pt_texture_size(const pt_texture* t, int* w, int* h)
+int dev_texture_size(const DevTex* t, int* w, int* h)
 {
     if (!t) return PT_ERR_ARG;
     if (w) *w = t->w;
@@ -961,10 +963,10 @@ int pt_texture_size(const pt_texture* t, int* w, int* h)
     return PT_OK;
 }
 
-void pt_texture_destroy(pt_texture* t)
+void dev_texture_destroy(DevTex* t)
 {
     if (!t) return;
-    pt_ctx* c = t->ctx;
+    Dev* c = t->ctx;
     hipSetDevice(c->device);
     if (c->pending_copy.on && (c->pending_copy.src == t || c->pending_copy.dst == t)) flush_copy(c);
     for (auto* fx : c->effects)
@@ -978,10 +980,10 @@ void pt_texture_destroy(pt_texture* t)
     delete t;
 }
 
-int pt_render(pt_effect* fx, pt_texture* target)
+int dev_render(DevFx* fx, DevTex* target)
 {
     if (!fx) return PT_ERR_ARG;
-    pt_ctx* c = fx->ctx;
+    Dev* c = fx->ctx;
     if (target && target->ctx != c) return fail(c, PT_ERR_ARG, "target belongs to another context");
     HIPCHK(c, hipSetDevice(c->device));
     if (fx->prog != PT_PROG_SCREEN_OUTPUT && fx->prog != PT_PROG_SCREEN_COPY) {
@@ -1001,7 +1003,7 @@ int pt_render(pt_effect* fx, pt_texture* target)
     }
 }
 
-int pt_read_pixels(pt_ctx* c, const pt_texture* t, void* dst, size_t bytes)
+int dev_read_pixels(Dev* c, const DevTex* t, void* dst, size_t bytes)
 {
     if (!c || !dst) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1014,7 +1016,7 @@ int pt_read_pixels(pt_ctx* c, const pt_texture* t, void* dst, size_t bytes)
     return PT_OK;
 }
 
-int pt_write_pixels(pt_ctx* c, pt_texture* t, const void* src, size_t bytes)
+int dev_write_pixels(Dev* c, DevTex* t, const void* src, size_t bytes)
 {
     if (!c || !t || !src || bytes != t->bytes) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1025,7 +1027,7 @@ int pt_write_pixels(pt_ctx* c, pt_texture* t, const void* src, size_t bytes)
     return PT_OK;
 }
 
-int pt_set_stream(pt_ctx* c, void* stream)
+int dev_set_stream(Dev* c, void* stream)
 {
     if (!c) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1035,7 +1037,7 @@ int pt_set_stream(pt_ctx* c, void* stream)
     return PT_OK;
 }
 
-int pt_set_backend(pt_ctx* c, int backend)
+int dev_set_backend(Dev* c, int backend)
 {
     if (!c || (backend != PT_BACKEND_MEGAKERNEL && backend != PT_BACKEND_WAVEFRONT && backend != PT_BACKEND_PERSISTENT))
         return PT_ERR_ARG;
@@ -1043,16 +1045,16 @@ int pt_set_backend(pt_ctx* c, int backend)
     return PT_OK;
 }
 
-int pt_set_bvh_layout(pt_ctx* c, int layout)
+int dev_set_bvh_layout(Dev* c, int layout)
 {
     if (!c || (layout != PT_BVH_REFERENCE && layout != PT_BVH_PAIRS)) return PT_ERR_ARG;
     c->bvh_layout = layout;
     return PT_OK;
 }
 
-int pt_bvh_layout_used(pt_ctx* c) { return c ? c->bvh_used : PT_ERR_ARG; }
+int dev_bvh_layout_used(Dev* c) { return c ? c->bvh_used : PT_ERR_ARG; }
 
-int pt_set_row_partition(pt_ctx* c, int num_parts, int part)
+int dev_set_row_partition(Dev* c, int num_parts, int part)
 {
     if (!c || num_parts < 1 || part < 0 || part >= num_parts) return PT_ERR_ARG;
     c->num_parts = num_parts;
@@ -1060,9 +1062,9 @@ int pt_set_row_partition(pt_ctx* c, int num_parts, int part)
     return PT_OK;
 }
 
-void* pt_texture_device_ptr(pt_texture* t) { return t ? t->d : nullptr; }
+void* dev_texture_device_ptr(DevTex* t) { return t ? t->d : nullptr; }
 
-int pt_last_render_ms(pt_ctx* c, int prog, float* ms)
+int dev_last_render_ms(Dev* c, int prog, float* ms)
 {
     if (!c || !ms || prog < 0 || prog >= kProgSlots || !c->ev_used[prog]) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1070,7 +1072,7 @@ int pt_last_render_ms(pt_ctx* c, int prog, float* ms)
     return PT_OK;
 }
 
-int pt_timing_begin(pt_ctx* c)
+int dev_timing_begin(Dev* c)
 {
     if (!c) return PT_ERR_ARG;
     c->window = true;
@@ -1078,13 +1080,13 @@ int pt_timing_begin(pt_ctx* c)
     return PT_OK;
 }
 
-int pt_timing_end(pt_ctx* c, int prog, double* total_ms, int* launches)
+int dev_timing_end(Dev* c, int prog, double* total_ms, int* launches)
 {
     if (!c || !total_ms || !launches) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = flush_copy(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->window = false;   // the window is closed; its draws stay readable by further pt_timing_end calls
+    c->window = false;   // the window is closed; its draws stay readable by further dev_timing_end calls
     double t = 0.0;
     int n = 0;
     for (auto& d : c->window_draws) {
@@ -1099,14 +1101,14 @@ int pt_timing_end(pt_ctx* c, int prog, double* total_ms, int* launches)
     return PT_OK;
 }
 
-int pt_set_counting(pt_ctx* c, int enable)
+int dev_set_counting(Dev* c, int enable)
 {
     if (!c) return PT_ERR_ARG;
     c->counting = enable != 0;
     return PT_OK;
 }
 
-int pt_read_counters(pt_ctx* c, uint64_t out[PT_NUM_COUNTERS])
+int dev_read_counters(Dev* c, uint64_t out[PT_NUM_COUNTERS])
 {
     if (!c || !out) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1115,7 +1117,7 @@ int pt_read_counters(pt_ctx* c, uint64_t out[PT_NUM_COUNTERS])
     return PT_OK;
 }
 
-int pt_reset_counters(pt_ctx* c)
+int dev_reset_counters(Dev* c)
 {
     if (!c) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1123,7 +1125,7 @@ int pt_reset_counters(pt_ctx* c)
     return PT_OK;
 }
 
-int pt_queue_stats(pt_ctx* c, uint32_t out[16])
+int dev_queue_stats(Dev* c, uint32_t out[16])
 {
     if (!c || !out) return PT_ERR_ARG;
     std::memset(out, 0, 16 * sizeof(uint32_t));
@@ -1140,7 +1142,7 @@ int pt_queue_stats(pt_ctx* c, uint32_t out[16])
     return PT_OK;
 }
 
-int pt_math_exhaustive(pt_ctx* c, int op, uint64_t* mismatches)
+int dev_math_exhaustive(Dev* c, int op, uint64_t* mismatches)
 {
     if (!c || !mismatches || op < 0 || op > 1) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1156,7 +1158,7 @@ int pt_math_exhaustive(pt_ctx* c, int op, uint64_t* mismatches)
     return PT_OK;
 }
 
-int pt_math_probe(pt_ctx* c, int op, const float* x, const float* y, float* out, int n)
+int dev_math_probe(Dev* c, int op, const float* x, const float* y, float* out, int n)
 {
     if (!c || !x || !out || n <= 0) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1175,4 +1177,12 @@ int pt_math_probe(pt_ctx* c, int op, const float* x, const float* y, float* out,
     return PT_OK;
 }
 
-}  // extern "C"
+
+int dev_device(const Dev* c) { return c->device; }
+hipStream_t dev_stream(const Dev* c) { return c->stream; }
+void* dev_canvas_ptr(Dev* c) { return c->canvas; }
+int dev_flush(Dev* c)
+{
+    HIPCHK(c, hipSetDevice(c->device));
+    return flush_copy(c);
+}

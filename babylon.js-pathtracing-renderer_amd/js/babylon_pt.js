@@ -159,7 +159,10 @@ function install(BABYLON, opts) {
     constructor(canvas, antialias, options) {
       const w = (canvas && canvas.width) || opts.width, h = (canvas && canvas.height) || opts.height;
       super({ renderWidth: w, renderHeight: h, textureSize: 512, deterministicLockstep: false, lockstepMaxSteps: 1 });
-      const c = addon.pt_ctx_create(opts.device);
+      // the devices of the context: opts.devices, else PT_DEVICES ("0,1,2,3"; a device may repeat),
+      // else opts.device - with several, every draw fans out over them inside libpt (pt.h)
+      const devs = opts.devices || (process.env.PT_DEVICES ? process.env.PT_DEVICES.split(',').map((d) => parseInt(d, 10)) : null);
+      const c = devs ? addon.pt_ctx_create_devices(devs) : addon.pt_ctx_create(opts.device);
       if (typeof c === 'number') throw new Error('pt_ctx_create: ' + (ERR[c] || c));
       this._pt = c;
       this._renderLoop = null;

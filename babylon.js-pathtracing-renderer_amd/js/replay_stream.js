@@ -4,6 +4,7 @@
 // This is the JavaScript host path on machines that have the GPU but not the reference scripts.
 //
 // usage: node replay_stream.js <stream.json> <payload_dir> <out_prefix> [frames]
+//   (PT_DEVICES="0,0" etc. renders through a multi-part context: the frame split over the parts)
 //   payload_dir holds bluenoise.u8 (256x256 RGBA8) and, for glTF streams, bvh.f32 / tri.f32
 //   (2048x2048 RGBA32F, the RawTexture payloads), and optionally maps.json (model PBR maps, below).
 'use strict';
@@ -17,7 +18,7 @@ const nFrames = framesArg ? parseInt(framesArg, 10) : meta.frames.length;
 const BABYLON = {};
 const errors = [];
 install(BABYLON, { width: meta.width, height: meta.height, onError: (m) => errors.push(m) });
-const PROGRAMS = { cornell: 3, gltf: 4, hdri: 5, sky: 6, quadric: 7 };
+const PROGRAMS = { cornell: 3, gltf: 4, hdri: 5, sky: 6, quadric: 7, skymesh: 8 };
 const SHADER_PROGRAM = { screenCopyFragmentShader: 1, screenOutputFragmentShader: 2 };
 
 const engine = new BABYLON.Engine({ width: meta.width, height: meta.height });

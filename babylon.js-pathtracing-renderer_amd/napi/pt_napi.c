@@ -97,6 +97,32 @@ static napi_value CtxCreate(napi_env env, napi_callback_info info)
     pt_ctx* c = pt_ctx_create(i32(env, a[0]), &err);
     return c ? ext(env, c) : num(env, err);
 }
+/* pt_ctx_create_devices(devices[]): a JS array of HIP device ids, one part each */
+static napi_value CtxCreateDevices(napi_env env, napi_callback_info info)
+{
+    napi_value a[MAXARGS]; if (args(env, info, a, 1) < 0) return NULL;
+    uint32_t n = 0;
+    bool isarr = false;
+    if (napi_is_array(env, a[0], &isarr) != napi_ok || !isarr || napi_get_array_length(env, a[0], &n) != napi_ok || n == 0 || n > 64) {
+        napi_throw_type_error(env, NULL, "pt_ctx_create_devices: expected a non-empty array of device ids");
+        return NULL;
+    }
+    int devs[64];
+    for (uint32_t i = 0; i < n; i++) { napi_value v; CHECK(napi_get_element(env, a[0], i, &v)); devs[i] = i32(env, v); }
+    int err = 0;
+    pt_ctx* c = pt_ctx_create_devices(devs, (int)n, &err);
+    return c ? ext(env, c) : num(env, err);
+}
+static napi_value CtxCreateMask(napi_env env, napi_callback_info info)
+{
+    napi_value a[MAXARGS]; if (args(env, info, a, 1) < 0) return NULL;
+    uint32_t m = 0; napi_get_value_uint32(env, a[0], &m);
+    int err = 0;
+    pt_ctx* c = pt_ctx_create_mask(m, &err);
+    return c ? ext(env, c) : num(env, err);
+}
+static napi_value CtxParts(napi_env env, napi_callback_info info)
+{ napi_value a[MAXARGS]; if (args(env, info, a, 1) < 0) return NULL; return num(env, pt_ctx_parts((pt_ctx*)handle(env, a[0]))); }
 static napi_value CtxDestroy(napi_env env, napi_callback_info info)
 { napi_value a[MAXARGS]; if (args(env, info, a, 1) < 0) return NULL; pt_ctx_destroy((pt_ctx*)handle(env, a[0])); return nul(env); }
 static napi_value LastError(napi_env env, napi_callback_info info)
@@ -346,7 +372,8 @@ static napi_value Version(napi_env env, napi_callback_info info)
 static napi_value Init(napi_env env, napi_value exports)
 {
     static const struct { const char* name; napi_callback fn; } F[] = {
-        { "pt_ctx_create", CtxCreate }, { "pt_ctx_destroy", CtxDestroy }, { "pt_last_error", LastError },
+        { "pt_ctx_create", CtxCreate }, { "pt_ctx_create_devices", CtxCreateDevices }, { "pt_ctx_create_mask", CtxCreateMask },
+        { "pt_ctx_parts", CtxParts }, { "pt_ctx_destroy", CtxDestroy }, { "pt_last_error", LastError },
         { "pt_sync", Sync }, { "pt_canvas_resize", CanvasResize },
         { "pt_effect_create", EffectCreate }, { "pt_effect_create_program", EffectCreateProgram },
         { "pt_effect_destroy", EffectDestroy }, { "pt_effect_program", EffectProgram },

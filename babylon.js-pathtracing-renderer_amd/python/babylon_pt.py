@@ -32,7 +32,7 @@ NEAREST, BILINEAR, TRILINEAR = 1, 2, 3
 
 # every symbol include/pt.h declares (checked by tests/test_capi_symbols.py)
 SYMBOLS = [
-    "pt_ctx_create", "pt_ctx_destroy", "pt_last_error", "pt_sync", "pt_canvas_resize",
+    "pt_ctx_create", "pt_ctx_create_mask", "pt_ctx_create_devices", "pt_ctx_parts", "pt_ctx_destroy", "pt_last_error", "pt_sync", "pt_canvas_resize",
     "pt_effect_create", "pt_effect_create_program", "pt_effect_destroy", "pt_effect_program",
     "pt_set_float", "pt_set_int", "pt_set_texture",
     "pt_texture_create_rgba32f", "pt_texture_create_rgba8", "pt_render_target_create", "pt_render_target_wrap",
@@ -56,7 +56,9 @@ def lib():
     vp, ip, i32, f32p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(ctypes.c_float)
     cpp = ctypes.POINTER(ctypes.c_char_p)
     sig = {
-        "pt_ctx_create": ([i32, ip], vp), "pt_ctx_destroy": ([vp], None), "pt_last_error": ([vp], ctypes.c_char_p),
+        "pt_ctx_create": ([i32, ip], vp), "pt_ctx_create_mask": ([ctypes.c_uint32, ip], vp),
+        "pt_ctx_create_devices": ([ctypes.POINTER(ctypes.c_int), i32, ip], vp), "pt_ctx_parts": ([vp], i32),
+        "pt_ctx_destroy": ([vp], None), "pt_last_error": ([vp], ctypes.c_char_p),
         "pt_sync": ([vp], i32), "pt_canvas_resize": ([vp, i32, i32], i32),
         "pt_effect_create": ([vp, ctypes.c_char_p, cpp, i32, cpp, i32, ip], vp),
         "pt_effect_create_program": ([vp, i32, cpp, i32, cpp, i32, ip], vp),
@@ -104,14 +106,22 @@ def _names(seq):
 
 
 class Engine:
-    """`new BABYLON.Engine(canvas)` -> one pt context (one HIP stream) on one gfx950 device."""
+    """`new BABYLON.Engine(canvas)` -> a pt context: one part (one HIP stream) on `device`, or one
+    part per entry of `devices` (a device may repeat); with several parts libpt splits every frame
+    over them into 16-row bands and gathers the canvas (include/pt.h)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, devices=None):
         err = ctypes.c_int(0)
-        self.ctx = lib().pt_ctx_create(device, ctypes.byref(err))
+        if devices is None:
+            self.ctx = lib().pt_ctx_create(device, ctypes.byref(err))
+        else:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            self.ctx = lib().pt_ctx_create_devices(arr, len(devices), ctypes.byref(err))
         if not self.ctx:
-            raise PtError("pt_ctx_create(device=%d) failed: %s" % (device, ERRORS.get(err.value, err.value)))
-        self.device = device
+            raise PtError("pt_ctx_create(%s) failed: %s" % (devices if devices is not None else device,
+                                                             ERRORS.get(err.value, err.value)))
+        self.device = device if devices is None else devices[0]
+        self.parts = lib().pt_ctx_parts(self.ctx)
         self._objs = []
 
     def check(self, rc, what=""):

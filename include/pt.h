@@ -57,8 +57,20 @@ enum pt_program {
 /* Babylon sampling-mode constants (BABYLON.Constants.TEXTURE_*_SAMPLINGMODE) */
 enum pt_sampling { PT_SAMPLING_NEAREST = 1, PT_SAMPLING_BILINEAR = 2, PT_SAMPLING_TRILINEAR = 3 };
 
-/* ---- context: replaces `new BABYLON.Engine(canvas, true)` (js/GLTF_Model_Path_Tracing.js:189) */
+/* ---- context: replaces `new BABYLON.Engine(canvas, true)` (js/GLTF_Model_Path_Tracing.js:189).
+ * A context has one or more parts, each one HIP stream on one gfx950 device. With several parts
+ * every draw fans out inside pt_render: part k shades the 16-row bands b % N == k, screenOutput
+ * pulls the +-2 halo rows from the band neighbours and part 0 gathers the RGBA8 bands into the
+ * canvas (device-to-device copies over xGMI, ordered by HIP events). Render targets
+ * stay distributed by bands; pt_read_pixels assembles them. Results are bit-identical to one part.
+ * pt_ctx_create(device): one part on `device`. */
 pt_ctx* pt_ctx_create(int device, int* err);
+/* one part per set bit of device_mask (bit d = HIP device d), in increasing device order */
+pt_ctx* pt_ctx_create_mask(uint32_t device_mask, int* err);
+/* part k on devices[k]; a device may appear more than once (several parts on one GPU: the same
+ * split, halo and gather path on a one-GPU host) */
+pt_ctx* pt_ctx_create_devices(const int* devices, int n, int* err);
+int pt_ctx_parts(const pt_ctx* ctx);
 void pt_ctx_destroy(pt_ctx* ctx);
 const char* pt_last_error(pt_ctx* ctx);
 int pt_sync(pt_ctx* ctx);
@@ -128,7 +140,9 @@ int pt_read_pixels(pt_ctx* ctx, const pt_texture* tex, void* dst, size_t bytes);
 int pt_write_pixels(pt_ctx* ctx, pt_texture* tex, const void* src, size_t bytes);
 
 /* ---- MI355X extensions (no reference counterpart) -------------------------------------------
- * Row-band sharding for multi-GPU rendering: this context's path-tracing and screenCopy passes
+ * Row-band sharding for one-part contexts driven by one process per GPU (bench.py, torch.distributed;
+ * a multi-part context shards itself and refuses these four: PT_ERR_ARG; pt_canvas_wrap then wraps
+ * the gathered canvas): this context's path-tracing and screenCopy passes
  * shade only the 16-row bands b with b % num_parts == part (bands are whole 2x2 quads, so
  * derivatives are unchanged). num_parts = 1 restores full frames. */
 int pt_set_row_partition(pt_ctx* ctx, int num_parts, int part);
