@@ -17,12 +17,13 @@ constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing
 constexpr int kStackLds = PT_STACK_LDS;        // levels kept in LDS per lane; deeper levels go to a global slab
 
 // child-pair record codes: a node's rank code from the build's rank pass (rank >= 0 of an inner
-// node, -1 - rank of a leaf) -> the 32-bit code the walk carries: the inner record's byte offset,
-// or kLeafBit | the leaf record's byte offset
+// node, -1 - rank of a leaf) -> the 32-bit code the walk carries: the record's byte offset in the
+// one record array (inner records first, the leaf records from byte leafBase on), with kLeafBit set
+// for a leaf
 constexpr uint32_t kLeafBit = 0x80000000u;
-__host__ __device__ inline uint32_t pairCode(float rankCode)
+__host__ __device__ inline uint32_t pairCode(float rankCode, uint32_t leafBase)
 {
-    return rankCode >= 0.0f ? (uint32_t)rankCode * 64u : kLeafBit | ((uint32_t)(-1.0f - rankCode) * 48u);
+    return rankCode >= 0.0f ? (uint32_t)rankCode * 64u : kLeafBit | (leafBase + (uint32_t)(-1.0f - rankCode) * 48u);
 }
 
 enum Counter { C_PATHS, C_SEGMENTS, C_NODE, C_LEAF, C_HIT, C_RGBA8, C_OVERFLOW, C_HDR, C_NUM };
@@ -108,20 +109,25 @@ struct TraceArgs {
     long long aabb_texels;
     const float4* tri;
     long long tri_texels;
-    const float4* bvh_pairs;   // child-pair inner records of tAABBTexture (PROG_PAIRS variants only)
-    const float4* bvh_leaves;  // ... and its leaf records
+    const float4* bvh_pairs;   // child-pair records of tAABBTexture (PROG_PAIRS variants only): inner, then leaf
     uint32_t bvh_root_code;    // pairCode of node 0
-    uint32_t bvh_pairs_bytes, bvh_leaves_bytes;   // sizes of the two record arrays (buffer descriptors)
+    float bvh_root_box[6];     // node 0's box (texels 0.yzw, 1.yzw as uploaded; PROG_PAIRS only): the root test of
+                               // every segment reads SGPRs instead of waiting on a load
+    uint32_t bvh_pairs_bytes;  // size of the record array (its buffer descriptor)
     float2* spill;             // megakernel BVH stack levels >= kStackLds: [level][grid lane]
     unsigned spill_stride;
     // longest-first dispatch (megakernel): order[slot] = the 16x16 tile dealt to tile slot `slot`
     // (NULL: row-major); each wave records its duration in cost[tile * 4 + quadrant]
     const unsigned* order;
     unsigned* cost;
+    unsigned prio_tiles;   // the first prio_tiles tiles of `order` (the slowest last frame) run at s_setprio 3
     Tex8 albedo, bump, metal, emissive;
     // diagnostics
     unsigned long long* counters;   // C_NUM entries, only with counting builds
     unsigned* err;                  // ErrBits
+#ifdef PT_SECPROF
+    unsigned long long* wave_log;   // experiment builds: (start, end) wall clock per workgroup
+#endif
 };
 
 // wavefront buffers (pt_wavefront.hip). Path queues are split into kShards shards of `shard_cap`

@@ -39,7 +39,8 @@ hipError_t pt_launch_persist(int prog, int count, const pt::TraceArgs* a, const 
 hipError_t pt_launch_finish(const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x, int bands, hipStream_t s);
 hipError_t pt_launch_pairs_pass(int pass, const float4* aabb, long long texels, const float4* tri, long long tri_texels,
                                 unsigned nrec, unsigned char* inner, unsigned char* leafref, unsigned* counts,
-                                float* code, float4* inner_rec, float4* leaf_rec, unsigned* bad, hipStream_t s);
+                                float* code, float4* inner_rec, float4* leaf_rec, unsigned leaf_base, unsigned* bad,
+                                hipStream_t s);
 hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x, int bands,
                                int persist_blocks, hipStream_t s);
 }
@@ -75,7 +76,8 @@ struct DevTex {
     const float4* pairs_inner = nullptr;
     const float4* pairs_leaf = nullptr;
     uint32_t pairs_root = 0;
-    uint32_t pairs_inner_bytes = 0, pairs_leaf_bytes = 0;
+    float pairs_root_box[6] = {};
+    uint32_t pairs_bytes = 0;   // inner records, then leaf records from pairs_leaf on
     const DevTex* pairs_tri = nullptr;
     unsigned long long pairs_gen = ~0ull, pairs_tri_gen = ~0ull;
     bool pairs_ok = false;
@@ -121,6 +123,7 @@ struct Dev {
     // longest-first dispatch of the megakernel (PT_LPT=0 disables): cost[] / order[] of the last
     // path-tracing draw, reused when the next draw has the same grid, target and program
     bool lpt = true;
+    unsigned prio_tiles = 0;   // longest-first: the first prio_tiles 16x16 tiles run at raised wave priority
     unsigned* lpt_mem = nullptr;            // cost[4 * ntiles] | order[ntiles]
     size_t lpt_n = 0, lpt_cap = 0;
     bool lpt_valid = false;
@@ -411,6 +414,17 @@ int gb_reserve(Dev* c, int wq, int hq)
 // when either texture's texels changed since the last build. Only for data textures (their
 // texels change only through this API) of at most 2^24 texels (node ids and ranks exact in
 // float). Returns false when the reference walk must be used. One host round trip per build.
+#ifdef PT_SECPROF
+static unsigned long long* g_wave_log = nullptr;
+static size_t g_wave_log_n = 0;
+extern "C" __attribute__((visibility("default"))) size_t pt_debug_wave_log(unsigned long long* out, size_t n)
+{
+    hipDeviceSynchronize();
+    n = n < g_wave_log_n ? n : g_wave_log_n;
+    if (g_wave_log && n) hipMemcpy(out, g_wave_log, n * 32, hipMemcpyDeviceToHost);
+    return n;
+}
+#endif
 bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
 {
     *rc = PT_OK;
@@ -439,8 +453,10 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
     const float4* aabb = (const float4*)t->d;
     const float4* trid = (const float4*)tri->d;
     const long long ttex = (long long)tri->w * tri->h;
+    unsigned leaf_base = 0;   // byte offset of the leaf records in the one record array
     auto pass = [&](int k, float4* ir, float4* lr) {
-        return pt_launch_pairs_pass(k, aabb, texels, trid, ttex, nrec, inner, leafref, counts, code, ir, lr, c->d_err + 1, c->stream);
+        return pt_launch_pairs_pass(k, aabb, texels, trid, ttex, nrec, inner, leafref, counts, code, ir, lr, leaf_base,
+                                    c->d_err + 1, c->stream);
     };
     if (e == hipSuccess) e = pass(1, nullptr, nullptr);
     if (e == hipSuccess) e = pass(2, nullptr, nullptr);
@@ -454,20 +470,23 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
             h[2 * b] = (unsigned)n_inner; h[2 * b + 1] = (unsigned)n_leaf;
             n_inner += ci; n_leaf += cl;
         }
+        leaf_base = (unsigned)al(n_inner * 64);
         e = hipMalloc(&t->pairs_mem, al(n_inner * 64) + al(n_leaf * 48) + 256);
         if (e == hipSuccess) {
             t->pairs_inner = (const float4*)t->pairs_mem;
-            t->pairs_leaf = (const float4*)((char*)t->pairs_mem + al(n_inner * 64));
+            t->pairs_leaf = (const float4*)((char*)t->pairs_mem + leaf_base);
             e = hipMemcpyAsync(counts, h.data(), h.size() * sizeof(unsigned), hipMemcpyHostToDevice, c->stream);
         }
         if (e == hipSuccess) e = pass(3, nullptr, nullptr);
         if (e == hipSuccess) e = pass(4, (float4*)t->pairs_inner, (float4*)t->pairs_leaf);
-        float root = 0.0f;
+        float root = 0.0f, node0[8] = {};
         if (e == hipSuccess) e = hipMemcpyAsync(&root, code, sizeof(float), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(node0, aabb, sizeof(node0), hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-        t->pairs_root = pt::pairCode(root);
-        t->pairs_inner_bytes = (uint32_t)(n_inner * 64);
-        t->pairs_leaf_bytes = (uint32_t)(n_leaf * 48);
+        t->pairs_root = pt::pairCode(root, leaf_base);
+        const float box6[6] = { node0[1], node0[2], node0[3], node0[5], node0[6], node0[7] };
+        std::memcpy(t->pairs_root_box, box6, sizeof(box6));
+        t->pairs_bytes = (uint32_t)(leaf_base + n_leaf * 48);
     }
     if (scratch) { hipStreamSynchronize(c->stream); hipFree(scratch); }
     if (e != hipSuccess) { *rc = hipfail(c, e, "BVH child-pair build"); return false; }
@@ -522,10 +541,9 @@ int render_trace(DevFx* fx, DevTex* target)
         int prc = PT_OK;
         if (ensure_pairs(c, bvh, tri, &prc)) {
             a.bvh_pairs = bvh->pairs_inner;
-            a.bvh_leaves = bvh->pairs_leaf;
             a.bvh_root_code = bvh->pairs_root;
-            a.bvh_pairs_bytes = bvh->pairs_inner_bytes;
-            a.bvh_leaves_bytes = bvh->pairs_leaf_bytes;
+            std::memcpy(a.bvh_root_box, bvh->pairs_root_box, sizeof(a.bvh_root_box));
+            a.bvh_pairs_bytes = bvh->pairs_bytes;
         }
         if (prc) return prc;
         c->bvh_used = a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
@@ -536,6 +554,15 @@ int render_trace(DevFx* fx, DevTex* target)
     }
     a.counters = c->d_counters;
     a.err = c->d_err;
+#ifdef PT_SECPROF
+    {   // experiment builds: the wave timeline of the last megakernel draw (pt_debug_wave_log)
+        static size_t cap = 0;
+        const size_t need = (size_t)((target->w + pt::kTile - 1) / pt::kTile) * bands_owned(c, target->h) * 4 * 4;
+        if (cap < need) { if (g_wave_log) hipFree(g_wave_log); hipMalloc(&g_wave_log, need * 8); cap = need; }
+        g_wave_log_n = need / 4;
+        a.wave_log = g_wave_log;
+    }
+#endif
     int gx = (target->w + pt::kTile - 1) / pt::kTile;
     int gy = bands_owned(c, target->h);
     const int persist = ((c->cu_count * 4 + pt::kShards - 1) / pt::kShards) * pt::kShards;
@@ -591,6 +618,7 @@ int render_trace(DevFx* fx, DevTex* target)
                 }
                 a.order = same ? c->lpt_mem + 4 * c->lpt_cap : nullptr;
                 a.cost = c->lpt_mem;
+                a.prio_tiles = a.order ? c->prio_tiles : 0u;
             }
             HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, gy, c->stream));
             if (a.cost) {
@@ -745,6 +773,7 @@ Dev* dev_ctx_create(int device, int* err)
     c->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (const char* v = std::getenv("PT_PERSIST_TILES")) c->persist_tiles = (unsigned)std::max(1, std::atoi(v));
     if (const char* v = std::getenv("PT_LPT")) c->lpt = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PT_PRIO_TILES")) c->prio_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);

@@ -296,6 +296,9 @@ struct BvhResult {
     float triID, triU, triV;
     bool lookup;
     unsigned nodes, leaves, ovf;
+#ifdef PT_SECPROF
+    unsigned steps;
+#endif
 };
 
 template <class Stk>
@@ -390,10 +393,10 @@ struct PairWalk {
     int sp;                  // stack pointer
     bool pop, lookup;
 };
-// the record arrays as buffer descriptors, built from kernel arguments and made provably
+// the record array as a buffer descriptor, built from kernel arguments and made provably
 // wave-uniform (readfirstlane) so that no waterfall loop wraps the loads
 struct PairBufs {
-    __amdgpu_buffer_rsrc_t inner, leaf;
+    __amdgpu_buffer_rsrc_t rec;
 };
 PT_D __amdgpu_buffer_rsrc_t uniformRsrc(const void* p, uint32_t bytes)
 {
@@ -404,7 +407,7 @@ PT_D __amdgpu_buffer_rsrc_t uniformRsrc(const void* p, uint32_t bytes)
 }
 PT_D PairBufs pairBufs(const TraceArgs& a)
 {
-    return PairBufs{ uniformRsrc(a.bvh_pairs, a.bvh_pairs_bytes), uniformRsrc(a.bvh_leaves, a.bvh_leaves_bytes) };
+    return PairBufs{ uniformRsrc(a.bvh_pairs, a.bvh_pairs_bytes) };
 }
 typedef unsigned int vu4 __attribute__((ext_vector_type(4)));
 typedef unsigned int vu2 __attribute__((ext_vector_type(2)));
@@ -443,9 +446,15 @@ PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv
         r.nodes++;
     }
     w.pop = true;
+    // one set of loads for either kind of record (both live in one array): a wave whose lanes sit
+    // at inner and at leaf nodes issues 4 vector-memory instructions, not 4 + 3 (the address and
+    // data units cost ~17 cycles per wave-instruction however few lanes are active).
+    // A leaf record is 48 B; its lane's fourth load reads the next record's first 8 B (or 0 past
+    // the end of the array) and is not used.
+    const uint32_t off = w.code & ~kLeafBit;
+    const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
+    const float2 r3 = ldRec2(b.rec, off + 48u);
     if (!(w.code & kLeafBit)) {
-        const float4 r0 = ldRec4(b.inner, w.code), r1 = ldRec4(b.inner, w.code + 16u), r2 = ldRec4(b.inner, w.code + 32u);
-        const float2 r3 = ldRec2(b.inner, w.code + 48u);
         r.nodes += 2;
         float tA, tB;
         if (fast) {
@@ -467,13 +476,10 @@ PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv
         }
         return true;
     }
-    const uint32_t lo = w.code & ~kLeafBit;
-    const float4 t0 = ldRec4(b.leaf, lo), t1 = ldRec4(b.leaf, lo + 16u);
-    const float2 t2 = ldRec2(b.leaf, lo + 32u);
     r.leaves++;
     float tu, tv;
-    const float d = bvhTriangleE(mk(t0.x, t0.y, t0.z), mk(t0.w, t1.x, t1.y), mk(t1.z, t1.w, t2.x), O, D, tu, tv, dbl);
-    if (d < w.hitT) { w.hitT = d; w.triID = 8.0f * t2.y; w.triU = tu; w.triV = tv; w.lookup = true; }
+    const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
+    if (d < w.hitT) { w.hitT = d; w.triID = 8.0f * r2.y; w.triU = tu; w.triV = tv; w.lookup = true; }
     return true;
 }
 template <class Stk>
@@ -484,7 +490,12 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     pairWalkBegin(w, a.bvh_root_code, curT, hitT);
     const bool fast = pairWalkFast(O, inv);
     const PairBufs b = pairBufs(a);
+#ifdef PT_SECPROF
+    r.steps = 0;
+    while (pairWalkStep(a, b, O, D, inv, dbl, fast, st, w, r)) r.steps++;
+#else
     while (pairWalkStep(a, b, O, D, inv, dbl, fast, st, w, r)) {}
+#endif
     hitT = w.hitT;
     if (w.lookup) { r.triID = w.triID; r.triU = w.triU; r.triV = w.triV; r.lookup = true; }
 }

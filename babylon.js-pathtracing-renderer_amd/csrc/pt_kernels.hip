@@ -27,6 +27,11 @@
 #include "pt_device.h"
 #include "pt_glsl.h"
 #include "pt_program.h"
+#ifdef PT_SECPROF
+#define PT_SECPROF_ON 1
+#else
+#define PT_SECPROF_ON 0
+#endif
 
 using namespace ptg;
 
@@ -100,22 +105,41 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     // the walk, and only if the mesh does not win (meshHit sets them all): fewer values live across
     // the walk, same results
     f3 sn;
+    PT_SEC(cnt, 4);
     analyticNearest<PROG>(a, rayO, rayD, h, sn);
-    if (!kHasMesh<PROG>) { analyticAttributes<PROG>(a, h, sn); return; }
+    PT_SEC(cnt, 1);
+    if (!kHasMesh<PROG>) { analyticAttributes<PROG>(a, h, sn); PT_SEC(cnt, 3); return; }
 
     // ---- BVH walk (js/GLTFModelPathTracing_FragmentShader.js:201-298), pt_device.h
     f3 O = mul(a.model, rayO, 1.0f), D = mul(a.model, rayD, 0.0f);
     f3 inv = mk(grcp(D.x), grcp(D.y), grcp(D.z));
     const bool dbl = (!a.uses_albedo && a.model_mat == TRANSPARENT);
-    float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
-    float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
     BvhResult br = { 0.0f, 0.0f, 0.0f, false, 1u, 0u, 0u };
     MegaStack<LS> st{ (lds_float2*)lds, lane_slot, (glb_float2*)a.spill, deep, a.spill_stride };
-    if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
-    else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, h.t, st, br);
+    if (kPairs<PROG>) {   // the root's box from the kernel arguments (the same floats as texels 0-1)
+        const float* rb = a.bvh_root_box;
+        const float rootT = box(mk(rb[0], rb[1], rb[2]), mk(rb[3], rb[4], rb[5]), O, inv);
+#ifdef PT_SECPROF
+        if (cnt.sec) {
+            const int ln_ = __lane_id();
+            if (ln_ == __builtin_amdgcn_readfirstlane(ln_)) cnt.sec[9] = 0;
+            bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
+            atomicMax(&cnt.sec[9], (unsigned long long)br.steps);
+            cnt.lane_steps += br.steps;
+            if (ln_ == __builtin_amdgcn_readfirstlane(ln_)) cnt.sec[10] += cnt.sec[9];
+        } else
+#endif
+        bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
+    } else {
+        float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
+        const float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
+        bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, h.t, st, br);
+    }
     if (COUNT) { cnt.node += br.nodes; cnt.leaf += br.leaves; cnt.ovf += br.ovf; }
+    PT_SEC(cnt, 2);
     if (br.lookup) meshHit<PROG, COUNT>(a, br.triID, br.triU, br.triV, h, cnt);
     else analyticAttributes<PROG>(a, h, sn);
+    PT_SEC(cnt, 3);
 }
 
 // One iteration of CalculateRadiance's loop: SceneIntersect, then the shading step
@@ -198,6 +222,9 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     const unsigned tid = threadIdx.x;
     const int lane = tid & 63;
     const unsigned long long t_start = clock64();
+#ifdef PT_SECPROF
+    const unsigned long long w0_ = wall_clock64();
+#endif
     // the 8x8 wave tile of this wave inside its 16x16 tile (grid = tiles_x * kTraceSub x bands)
     int wave, tx;
     unsigned bY, costIdx = ~0u;
@@ -213,6 +240,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         const unsigned T = min(8u, ntiles - g * 8u);
         const unsigned slot = g * 8u + r % T;
         const unsigned tile = a.order ? a.order[slot] : slot;
+        if (slot < a.prio_tiles) __builtin_amdgcn_s_setprio(3);   // the critical path: issue first
         wave = (int)(r / T);
         tx = (int)(tile % tiles_x);
         bY = tile / tiles_x;
@@ -239,14 +267,22 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     // that only complete a quad at an odd edge are shaded like GL helper invocations
     const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1);
     Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
+#ifdef PT_SECPROF
+    __shared__ unsigned long long lds_sec[16];
+    if (tid < 16) lds_sec[tid] = tid == 8 ? clock64() : 0ull;
+    cnt.sec = lds_sec;
+    cnt.lane_steps = 0;
+#endif
     GOutLds<kTraceBlock> gl{ (lds_float*)lds_gout, tid };
     gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
     f3 r = mk(0, 0, 0);
     if (active) {
         Path p;
         cameraRay(a, px, py, p);
+        PT_SEC(cnt, 0);
         r = radiance<PROG, COUNT, kTraceBlock>(a, p, gl, lds_stack, tid, deep, cnt);
     }
+    PT_SEC(cnt, 4);
     const GOut g = gl.load();
 
     // ---- 2x2 fine derivatives (js/PathTracingCommon.js:1306-1320): partner lanes ^1 (x) and ^2 (y)
@@ -266,7 +302,29 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     dCol += length(dcy) > 0.0f ? 1.0f : 0.0f;
     float colorDiff = gsmoothstep(0.0f, 0.5f, dCol);
 
-    if (COUNT && active) {
+#ifdef PT_SECPROF
+    if (!COUNT && a.wave_log) {   // wave timeline in wall-clock ticks (100 MHz), one slot per workgroup
+        atomicMax(&lds_sec[11], (unsigned long long)cnt.lane_steps);
+        if (tid == 0) {
+            const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
+            a.wave_log[4 * L] = w0_;
+            a.wave_log[4 * L + 1] = wall_clock64();
+            a.wave_log[4 * L + 2] = lds_sec[10];
+            a.wave_log[4 * L + 3] = lds_sec[11];
+        }
+    }
+    if (COUNT) {
+        PT_SEC(cnt, 5);
+        if (tid == 0) {
+            for (int k = 0; k < 5; k++) atomicAdd(&a.counters[k], lds_sec[k]);
+            const unsigned long long dur_ = clock64() - t_start;
+            atomicMax(&a.counters[5], dur_);   // the longest wave of the launch(es)
+            atomicAdd(&a.counters[7], dur_);
+            atomicAdd(&a.counters[6], 1ull);
+        }
+    }
+#endif
+    if (COUNT && active && !PT_SECPROF_ON) {
         unsigned long long* C = a.counters;
         atomicAdd(&C[C_PATHS], 1ull);
         atomicAdd(&C[C_SEGMENTS], (unsigned long long)cnt.seg);
@@ -569,7 +627,8 @@ __global__ __launch_bounds__(256) void pt_pairs_rank(const unsigned char* inner,
 __global__ __launch_bounds__(256) void pt_pairs_build(const float4* aabb, long long texels, const float4* tri,
                                                       long long tri_texels, unsigned nrec, const float* code,
                                                       float4* inner_rec, float4* leaf_rec,
-                                                      const unsigned char* inner, const unsigned char* leafref)
+                                                      const unsigned char* inner, const unsigned char* leafref,
+                                                      unsigned leaf_base)
 {
     const unsigned n = blockIdx.x * 256u + threadIdx.x;
     if (n >= nrec) return;
@@ -583,7 +642,8 @@ __global__ __launch_bounds__(256) void pt_pairs_build(const float4* aabb, long l
         o[0] = make_float4(a0.y, a0.z, a0.w, a1.y);
         o[1] = make_float4(a1.z, a1.w, b0.y, b0.z);
         o[2] = make_float4(b0.w, b1.y, b1.z, b1.w);
-        o[3] = make_float4(__uint_as_float(pairCode(code[n + 1u])), __uint_as_float(pairCode(code[(unsigned)idB])), 0.0f, 0.0f);
+        o[3] = make_float4(__uint_as_float(pairCode(code[n + 1u], leaf_base)),
+                           __uint_as_float(pairCode(code[(unsigned)idB], leaf_base)), 0.0f, 0.0f);
     } else if (leafref[n]) {
         const float hdr = fetch32(aabb, texels, fn * 2.0f).x;
         const float id = 8.0f * hdr;
@@ -693,7 +753,8 @@ hipError_t pt_launch_persist(int prog, int count, const pt::TraceArgs* a, const 
 // the four passes of the child-pair build; `offsets` is filled by the host between pass 2 and 3
 hipError_t pt_launch_pairs_pass(int pass, const float4* aabb, long long texels, const float4* tri, long long tri_texels,
                                 unsigned nrec, unsigned char* inner, unsigned char* leafref, unsigned* counts,
-                                float* code, float4* inner_rec, float4* leaf_rec, unsigned* bad, hipStream_t s)
+                                float* code, float4* inner_rec, float4* leaf_rec, unsigned leaf_base, unsigned* bad,
+                                hipStream_t s)
 {
     const dim3 nodes((nrec + 255) / 256), blocks((nrec + pt::kPairsBlock - 1) / pt::kPairsBlock), b256(256);
     switch (pass) {
@@ -702,7 +763,7 @@ hipError_t pt_launch_pairs_pass(int pass, const float4* aabb, long long texels, 
     case 3: hipLaunchKernelGGL(pt::pt_pairs_rank, blocks, b256, 0, s, inner, leafref, nrec, counts, code); break;
     case 4:
         hipLaunchKernelGGL(pt::pt_pairs_build, nodes, b256, 0, s, aabb, texels, tri, tri_texels, nrec, code, inner_rec,
-                           leaf_rec, inner, leafref);
+                           leaf_rec, inner, leafref, leaf_base);
         break;
     default: return hipErrorInvalidValue;
     }

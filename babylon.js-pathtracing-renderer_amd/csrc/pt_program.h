@@ -24,7 +24,26 @@ struct Hit {
 
 struct Cnt {
     unsigned seg, node, leaf, hit, tap, ovf, hdr;
+#ifdef PT_SECPROF
+    unsigned long long* sec;   // experiment builds: per-wave LDS slots ([0..7] section sums, [8] last mark,
+                               // [9] walk max scratch, [10] wave walk iterations, [11] longest lane's walk steps)
+    unsigned lane_steps;
+#endif
 };
+// section profile (experiment builds only, -DPT_SECPROF): the wave's shader clock between marks,
+// charged to section k by the first active lane (divergent code is charged once per wave)
+#ifdef PT_SECPROF
+#define PT_SEC(cnt, k)                                                                        \
+    do {                                                                                      \
+        const unsigned long long now_ = clock64();                                            \
+        const int ln_ = __lane_id();                                                          \
+        if (COUNT && (cnt).sec && ln_ == __builtin_amdgcn_readfirstlane(ln_)) {                \
+            (cnt).sec[k] += now_ - (cnt).sec[8]; (cnt).sec[8] = now_;                         \
+        }                                                                                     \
+    } while (0)
+#else
+#define PT_SEC(cnt, k) do {} while (0)
+#endif
 
 // CalculateRadiance's `out` parameters objectNormal / objectColor / objectID / pixelSharpness:
 // in registers (GOut) or, for the megakernel, in LDS [field][lane] (GOutLds), which takes eight

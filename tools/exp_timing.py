@@ -21,13 +21,23 @@ ap.add_argument("--backends", default="megakernel,wavefront")
 ap.add_argument("--layouts", default="pairs,reference")
 ap.add_argument("--no-mesh-variant", action="store_true", help="skip the mesh-out-of-view run")
 ap.add_argument("--dragon", action="store_true", help="the StanfordDragon stand-in mesh instead of the stream's")
+ap.add_argument("--workload", default=None, choices=sorted(H.WORKLOADS), help="a bench.py workload instead of --stream")
 a = ap.parse_args()
-meta = H.stream(a.stream)
 e = bp.Engine(0)
 mesh = None
-if meta["scene"] in ("gltf", "hdri"):
-    mesh = H.texture_payloads(meta, H.synthetic_dragon() if a.dragon else H.mesh(meta))
-p = bp.StreamPlayer(e, meta, H.bluenoise(), mesh)
+maps = None
+if a.workload:
+    meta, mesh_arrays, maps, (W, Hh) = H.workload(a.workload)
+    mesh = H.texture_payloads(meta, mesh_arrays) if mesh_arrays is not None else None
+    p = bp.StreamPlayer(e, meta, H.bluenoise(), mesh, W, Hh)
+    if maps:
+        for kind, sampler in H.PBR_SAMPLERS.items():
+            p.textures[sampler] = bp.Texture(e, maps[kind], name=kind)
+else:
+    meta = H.stream(a.stream)
+    if meta["scene"] in ("gltf", "hdri"):
+        mesh = H.texture_payloads(meta, H.synthetic_dragon() if a.dragon else H.mesh(meta))
+    p = bp.StreamPlayer(e, meta, H.bluenoise(), mesh)
 prog = meta["scene"]
 import itertools  # noqa: E402
 for backend, layout in itertools.product(a.backends.split(","), a.layouts.split(",")):
