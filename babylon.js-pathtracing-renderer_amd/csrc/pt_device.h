@@ -452,6 +452,17 @@ PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv
     // A leaf record is 48 B; its lane's fourth load reads the next record's first 8 B (or 0 past
     // the end of the array) and is not used.
     const uint32_t off = w.code & ~kLeafBit;
+#ifdef PT_SECPROF
+    if (a.counters) {   // experiment: wave-level record loads, those with one record for all lanes, lanes served
+        const uint32_t first = __builtin_amdgcn_readfirstlane(off);
+        const unsigned long long act = __ballot(1), same = __ballot(off == first);
+        if (__lane_id() == (int)__builtin_amdgcn_readfirstlane(__lane_id())) {
+            atomicAdd(&a.counters[0], 1ull);
+            if (same == act) atomicAdd(&a.counters[1], 1ull);
+            atomicAdd(&a.counters[2], (unsigned long long)__popcll(act));
+        }
+    }
+#endif
     const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
     const float2 r3 = ldRec2(b.rec, off + 48u);
     if (!(w.code & kLeafBit)) {

@@ -48,9 +48,16 @@ struct MegaStack {
     glb_float2* slab;     // the spill slab (wave-uniform base) ...
     unsigned deep;        // ... and this lane's index in it: level kStackLds, levels `stride` apart
     unsigned stride;      //     (32-bit: a 64-bit per-lane pointer costs two VGPRs for the whole path)
+#ifdef PT_SECPROF
+    mutable unsigned n_get = 0, n_get_slab = 0, n_put = 0, n_put_slab = 0;
+#define PT_SLABCOUNT(x) x
+#else
+#define PT_SLABCOUNT(x)
+#endif
     PT_D float2 get(int si) const
     {
         vf2 e;
+        PT_SLABCOUNT(n_get++; if (si >= kStackLds) n_get_slab++;)
         if (si < kStackLds) e = lds[si * LS + slot];
         else e = slab[(unsigned)(si - kStackLds) * stride + deep];
         return make_float2(e.x, e.y);
@@ -58,6 +65,7 @@ struct MegaStack {
     PT_D void put(int si, float2 e)
     {
         const vf2 v = { e.x, e.y };
+        PT_SLABCOUNT(n_put++; if (si >= kStackLds) n_put_slab++;)
         if (si < kStackLds) lds[si * LS + slot] = v;
         else slab[(unsigned)(si - kStackLds) * stride + deep] = v;
     }
@@ -136,6 +144,9 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
         bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, h.t, st, br);
     }
     if (COUNT) { cnt.node += br.nodes; cnt.leaf += br.leaves; cnt.ovf += br.ovf; }
+#ifdef PT_SECPROF
+    if (COUNT) { cnt.sget += st.n_get; cnt.sget_slab += st.n_get_slab; cnt.sput += st.n_put; cnt.sput_slab += st.n_put_slab; }
+#endif
     PT_SEC(cnt, 2);
     if (br.lookup) meshHit<PROG, COUNT>(a, br.triID, br.triU, br.triV, h, cnt);
     else analyticAttributes<PROG>(a, h, sn);
@@ -272,6 +283,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     if (tid < 16) lds_sec[tid] = tid == 8 ? clock64() : 0ull;
     cnt.sec = lds_sec;
     cnt.lane_steps = 0;
+    cnt.sget = cnt.sget_slab = cnt.sput = cnt.sput_slab = 0;
 #endif
     GOutLds<kTraceBlock> gl{ (lds_float*)lds_gout, tid };
     gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
@@ -313,15 +325,11 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
             a.wave_log[4 * L + 3] = lds_sec[11];
         }
     }
-    if (COUNT) {
-        PT_SEC(cnt, 5);
-        if (tid == 0) {
-            for (int k = 0; k < 5; k++) atomicAdd(&a.counters[k], lds_sec[k]);
-            const unsigned long long dur_ = clock64() - t_start;
-            atomicMax(&a.counters[5], dur_);   // the longest wave of the launch(es)
-            atomicAdd(&a.counters[7], dur_);
-            atomicAdd(&a.counters[6], 1ull);
-        }
+    if (COUNT && active) {   // stack traffic: pops beyond the LDS levels, pushes beyond; node fetches, leaf tests
+        atomicAdd(&a.counters[3], (unsigned long long)cnt.sget_slab);
+        atomicAdd(&a.counters[4], (unsigned long long)cnt.node);
+        atomicAdd(&a.counters[5], (unsigned long long)cnt.leaf);
+        atomicAdd(&a.counters[6], 1ull);
     }
 #endif
     if (COUNT && active && !PT_SECPROF_ON) {

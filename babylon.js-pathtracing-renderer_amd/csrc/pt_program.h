@@ -28,6 +28,7 @@ struct Cnt {
     unsigned long long* sec;   // experiment builds: per-wave LDS slots ([0..7] section sums, [8] last mark,
                                // [9] walk max scratch, [10] wave walk iterations, [11] longest lane's walk steps)
     unsigned lane_steps;
+    unsigned sget, sget_slab, sput, sput_slab;   // stack pops / pushes, and those beyond the LDS levels
 #endif
 };
 // section profile (experiment builds only, -DPT_SECPROF): the wave's shader clock between marks,

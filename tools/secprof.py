@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
-"""Section profile of the megakernel (experiment build: tools/build_variant.sh secprof -DPT_SECPROF,
-run with PT_LIBPT=build_variants/secprof/libpt.so): per workload, the share of wave clock spent in
-camera ray / analytic intersection / BVH walk / hit attributes / shading / epilogue, charged once
-per wave (divergent code counts once). The counting pass carries the marks; never bit-checked."""
+"""BVH stack traffic of the megakernel (experiment build: tools/build_variant.sh secprof -DPT_SECPROF,
+run with PT_LIBPT=build_variants/secprof/libpt.so): per workload and launch, the stack pops and
+pushes of every walk and how many of them fall beyond the LDS levels into the global slab (each
+such access is a vector-memory instruction of its wave), next to the reference-priced node fetches
+and leaf tests. The counting pass carries the counts; never bit-checked."""
 import json
 import os
 import sys
@@ -13,7 +14,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import babylon_pt as bp  # noqa: E402
 import helpers as H      # noqa: E402
 
-NAMES = ["camera", "analytic", "walk", "attributes", "shade+epilogue", "max_wave", "waves", "total"]
+NAMES = ["wave_record_loads", "uniform_wave_record_loads", "lanes_at_record_loads", "pops_slab", "node_fetches", "leaf_tests", "paths"]
 for wl in (sys.argv[1:] or ["helmet", "bunny", "dragon", "sky_dragon"]):
     meta, mesh_arrays, maps, (W, Hh) = H.workload(wl)
     e = bp.Engine(0)
@@ -28,17 +29,12 @@ for wl in (sys.argv[1:] or ["helmet", "bunny", "dragon", "sky_dragon"]):
             p.play_call(call)
     e.set_counting(True)
     e.reset_counters()
-    e.sync()
-    e.timing_begin()
-    for k in range(1):
-        for call in p.synth_frame(3 + k):
-            p.play_call(call)
-    ms, _ = e.timing_end(meta["scene"])
-    c = e.counters()
+    for call in p.synth_frame(3):
+        p.play_call(call)
+    vals = [int(v) for v in e.counters().values()]
     e.dispose()
-    vals = [int(v) for v in (c.values() if isinstance(c, dict) else c)]
-    tot = max(1, vals[7])
-    print(json.dumps({"workload": wl, "waves": vals[6], "cycles_per_wave": vals[7] / max(1, vals[6]),
-                      "max_wave_cycles": vals[5], "kernel_ms": ms,
-                      "share": {NAMES[i]: round(vals[i] / tot, 4) for i in (0, 1, 2, 3, 4)}}), flush=True)
-    e2 = None
+    d = dict(zip(NAMES, vals))
+    d["workload"] = wl
+    d["lanes_per_wave_load"] = round(vals[2] / max(1, vals[0]), 2)
+    d["uniform_share"] = round(vals[1] / max(1, vals[0]), 4)
+    print(json.dumps(d), flush=True)
