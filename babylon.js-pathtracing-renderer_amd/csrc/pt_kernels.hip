@@ -477,8 +477,14 @@ __global__ __launch_bounds__(256) void pt_copy(CopyArgs a)
 }
 
 // ------------------------------------------------------------------------------ screenOutput
+// the texel texelFetch(accumulationBuffer, ivec2(gl_FragCoord.xy + vec2(dx, dy)), 0) reads for the
+// tap at integer position (x, y) = pixel + (dx, dy) (js/PathTracingCommon.js:44-72): ivec2() of a
+// float truncates toward zero, so position -1 (fragment coordinate -0.5) reads texel 0 and -2
+// (-1.5) is outside the texture: 0 (pinned)
 PT_D float4 accAt(const OutputArgs& a, int x, int y)
 {
+    x = (int)((float)x + 0.5f);
+    y = (int)((float)y + 0.5f);
     if (x < 0 || y < 0 || x >= a.acc_w || y >= a.acc_h) return make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     return a.acc[(long long)y * a.acc_w + x];
 }

@@ -1296,8 +1296,14 @@ int pto_gbuffer(const pto_frame* f, float* gbuf, int row0, int row1, int nthread
 }
 
 /* ---------------------------------------------------------------- screenOutput */
-static void fetch_acc(const float* acc, int W, int H, int x, int y, float o[4])
+/* texelFetch(accumulationBuffer, ivec2(gl_FragCoord.xy + vec2(dx, dy)), 0) for pixel (px, py)
+ * (js/PathTracingCommon.js:44-72): ivec2() of a float truncates toward zero, so the tap one texel
+ * left of (below) the first column (row), at -0.5, reads texel 0; the one two texels out, at -1.5,
+ * is outside the texture and reads 0 (pinned). Found by the mechanical transcription of the
+ * shader (oracle/xcheck); an earlier reading here dropped both. */
+static void fetch_acc(const float* acc, int W, int H, int px, int py, int dx, int dy, float o[4])
 {
+    const int x = (int)(((float)px + 0.5f) + (float)dx), y = (int)(((float)py + 0.5f) + (float)dy);
     if (x < 0 || y < 0 || x >= W || y >= H) { o[0] = o[1] = o[2] = o[3] = 0.0f; return; }
     const float* p = acc + 4 * ((size_t)y * W + x);
     o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; o[3] = p[3];
@@ -1320,7 +1326,7 @@ int pto_screen_output(int W, int H, const float* acc, float oneOverN, float expo
     for (int y = 0; y < H; y++)
         for (int x = 0; x < W; x++) {
             float m25[25][4];
-            for (int k = 0; k < 25; k++) fetch_acc(acc, W, H, x + (k % 5) - 2, y + 2 - (k / 5), m25[k]);
+            for (int k = 0; k < 25; k++) fetch_acc(acc, W, H, x, y, (k % 5) - 2, 2 - (k / 5), m25[k]);
             float th = 1.0f;
             float cp[4] = { m25[12][0], m25[12][1], m25[12][2], m25[12][3] };
             float fr = m25[12][0], fg = m25[12][1], fb = m25[12][2];

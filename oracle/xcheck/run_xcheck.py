@@ -107,6 +107,56 @@ def compare(ref, got):
             "rmse": float(np.sqrt(np.nanmean(d[..., :3] ** 2)))}
 
 
+def quantize(c):
+    """the canvas store of a [0,1] colour: u8 = floor(255 c + 0.5) in binary32"""
+    c = np.asarray(c, np.float32)
+    return np.floor(c * np.float32(255.0) + np.float32(0.5)).astype(np.uint8)
+
+
+# screenOutput at the sample counts either side of its two bypass thresholds
+# (js/PathTracingCommon.js:293: 1/N < 0.005 for sharp pixels, 1/N < 0.0002 for all)
+OUTPUT_STREAMS = ["cornell_256", "gltf_bunny_1080p", "hdri_helmet_320x180"]
+OUTPUT_N = [1, 2, 200, 201, 4999, 5001]
+
+
+def run_output():
+    """screenCopy and screenOutput transcribed, on the oracle's accumulation of each stream."""
+    out_lib, _ = build("screen_output")
+    copy_lib, _ = build("screen_copy")
+    rpath = os.path.join(GOLD, "report.json")
+    report = json.load(open(rpath))
+    for name in OUTPUT_STREAMS:
+        w, h, frames, maps_kind = STREAMS[name]
+        meta = H.stream(name)
+        maps = H.helmet_maps() if maps_kind == "helmet" else None
+        accs, _, _ = H.oracle_replay(meta, frames, width=w, height=h, maps=maps)
+        acc = np.ascontiguousarray(accs[-1])
+        exposure = H.output_call(meta["frames"][frames - 1])["uniforms"].get("uToneMappingExposure", ["f", [1.0]])[1][0]
+        res, outs = {}, {"acc": acc}
+        for n in OUTPUT_N:
+            inv = np.float32(1.0 / n)
+            for lib, uni in ((out_lib, {"uOneOverSampleCounter": inv, "uToneMappingExposure": np.float32(exposure)}),):
+                for k, v in uni.items():
+                    vv = np.asarray([v], np.float32)
+                    lib.xc_set_uniform(k.encode(), vv.ctypes.data, 1)
+                lib.xc_set_sampler(b"accumulationBuffer", acc.ctypes.data, w, h, 1)
+                got = np.zeros((h, w, 4), np.float32)
+                lib.xc_render(w, h, got.ctypes.data, max(1, (os.cpu_count() or 4) // 4))
+            outs["out_%d" % n] = got
+            want = H.po_screen_output(acc, float(inv), exposure)
+            res[str(n)] = int((quantize(got) != want).any(-1).sum())
+        copy_lib.xc_set_sampler(b"pathTracedImageBuffer", acc.ctypes.data, w, h, 1)
+        cp = np.zeros((h, w, 4), np.float32)
+        copy_lib.xc_render(w, h, cp.ctypes.data, 1)
+        res["copy"] = int((cp.view(np.uint32) != acc.view(np.uint32)).any(-1).sum())
+        np.savez_compressed(os.path.join(GOLD, "screen_output_%s_%dx%d.npz" % (name, w, h)), **outs)
+        report.setdefault("_screen_output", {})[name] = {"width": w, "height": h, "exposure": exposure,
+                                                        "pixels": w * h, "pixels_differing_by_N": res}
+        print("screenOutput", name, res, flush=True)
+    with open(rpath, "w") as f:
+        json.dump(report, f, indent=1, sort_keys=True)
+
+
 def run(names):
     os.makedirs(GOLD, exist_ok=True)
     rpath = os.path.join(GOLD, "report.json")
@@ -140,8 +190,12 @@ def run(names):
 
 if __name__ == "__main__":
     if sys.argv[1:] == ["--build"]:
-        for sc in sorted({H.stream(n)["scene"] for n in STREAMS}):
+        for sc in sorted({H.stream(n)["scene"] for n in STREAMS}) + ["screen_copy", "screen_output"]:
             build(sc)
             print("built oracle/_ref/libxcheck_%s.so" % sc)
+    elif sys.argv[1:] == ["--output"]:
+        run_output()
     else:
         run(sys.argv[1:] or list(STREAMS))
+        if not sys.argv[1:]:
+            run_output()

@@ -24,19 +24,21 @@ C++ goes to oracle/_ref/ only (never into git): it is the reference's source in 
 Statements that hold more than one rng() / blueNoise_rand() call outside a constructor's
 braces are reported (C++ leaves their order unspecified) so that a human checks them.
 
-usage: transcribe.py SCENE OUT.cpp   with SCENE one of: cornell gltf hdri sky quadric
+usage: transcribe.py PROGRAM OUT.cpp   with PROGRAM one of: cornell gltf hdri sky quadric screen_output screen_copy
 """
 import os
 import re
 import sys
 
 REF = os.environ.get("PT_REFERENCE", "/root/reference")
-SCENES = {
-    "cornell": "BabylonPathTracing_FragmentShader.js",
-    "gltf": "GLTFModelPathTracing_FragmentShader.js",
-    "hdri": "HDRIEnvironmentPathTracing_FragmentShader.js",
-    "sky": "PhysicalSkyModel_FragmentShader.js",
-    "quadric": "TransformedQuadricGeometry_FragmentShader.js",
+SCENES = {   # program -> (file, ShadersStore key)
+    "cornell": ("BabylonPathTracing_FragmentShader.js", "pathTracingFragmentShader"),
+    "gltf": ("GLTFModelPathTracing_FragmentShader.js", "pathTracingFragmentShader"),
+    "hdri": ("HDRIEnvironmentPathTracing_FragmentShader.js", "pathTracingFragmentShader"),
+    "sky": ("PhysicalSkyModel_FragmentShader.js", "pathTracingFragmentShader"),
+    "quadric": ("TransformedQuadricGeometry_FragmentShader.js", "pathTracingFragmentShader"),
+    "screen_output": ("PathTracingCommon.js", "screenOutputFragmentShader"),
+    "screen_copy": ("PathTracingCommon.js", "screenCopyFragmentShader"),
 }
 VEC_TYPES = ["vec2", "vec3", "vec4", "ivec2", "ivec3", "ivec4", "uvec2", "uvec3", "uvec4", "mat3", "mat4"]
 SCALARS = ["float", "int", "uint", "bool"]
@@ -161,8 +163,9 @@ def array_decl(decl_type, declarator):
 
 def transcribe(scene):
     common = shader_store(os.path.join(REF, "js", "PathTracingCommon.js"))
-    scene_store = shader_store(os.path.join(REF, "js", SCENES[scene]))
-    src = expand(scene_store["pathTracingFragmentShader"], common)
+    fname, key = SCENES[scene]
+    scene_store = shader_store(os.path.join(REF, "js", fname))
+    src = expand(scene_store[key], common)
     src = strip_comments(src)
     src = "\n".join(l for l in src.split("\n") if not re.match(r"\s*(#version|precision)\b", l))
     structs = re.findall(r"\bstruct\s+(\w+)", src)
@@ -275,7 +278,7 @@ NEEDS = {"float": 1, "int": 1, "bool": 1, "vec2": 2, "vec3": 3, "vec4": 4, "mat4
 
 def generate(scene, out_path):
     code, uniforms, globals_ = transcribe(scene)
-    lines = ["// GENERATED by oracle/xcheck/transcribe.py from /root/reference/js/%s and js/PathTracingCommon.js" % SCENES[scene],
+    lines = ["// GENERATED by oracle/xcheck/transcribe.py from /root/reference/js/%s (%s) and js/PathTracingCommon.js" % SCENES[scene],
              "// (build-container artefact under oracle/_ref/: never committed)",
              '#include "glsl_shim.h"', '#include "harness.inc"', "namespace glx {", code]
     lines.append("vec4 xc_frag_color() { return glFragColor; }")
