@@ -10,6 +10,7 @@ namespace pt {
 
 constexpr int kBlock = 256;          // 4 waves; a block shades a 16x16 pixel tile
 constexpr int kTile = 16;            // tile edge == row-band height used for sharding
+constexpr int kWaveLogSlots = 12;    // experiment builds: u64 per workgroup in TraceArgs::wave_log
 constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing_FragmentShader.js:95
 #ifndef PT_STACK_LDS
 #define PT_STACK_LDS 7
@@ -126,7 +127,7 @@ struct TraceArgs {
     unsigned long long* counters;   // C_NUM entries, only with counting builds
     unsigned* err;                  // ErrBits
 #ifdef PT_SECPROF
-    unsigned long long* wave_log;   // experiment builds: (start, end) wall clock per workgroup
+    unsigned long long* wave_log;   // experiment builds: per workgroup (start, end) wall clock, walk iterations, longest lane's steps, 8 section cycle sums
 #endif
 };
 

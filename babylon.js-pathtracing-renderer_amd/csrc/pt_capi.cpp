@@ -421,7 +421,7 @@ extern "C" __attribute__((visibility("default"))) size_t pt_debug_wave_log(unsig
 {
     hipDeviceSynchronize();
     n = n < g_wave_log_n ? n : g_wave_log_n;
-    if (g_wave_log && n) hipMemcpy(out, g_wave_log, n * 32, hipMemcpyDeviceToHost);
+    if (g_wave_log && n) hipMemcpy(out, g_wave_log, n * 8 * pt::kWaveLogSlots, hipMemcpyDeviceToHost);
     return n;
 }
 #endif
@@ -557,9 +557,9 @@ int render_trace(DevFx* fx, DevTex* target)
 #ifdef PT_SECPROF
     {   // experiment builds: the wave timeline of the last megakernel draw (pt_debug_wave_log)
         static size_t cap = 0;
-        const size_t need = (size_t)((target->w + pt::kTile - 1) / pt::kTile) * bands_owned(c, target->h) * 4 * 4;
+        const size_t need = (size_t)((target->w + pt::kTile - 1) / pt::kTile) * bands_owned(c, target->h) * 4 * pt::kWaveLogSlots;
         if (cap < need) { if (g_wave_log) hipFree(g_wave_log); hipMalloc(&g_wave_log, need * 8); cap = need; }
-        g_wave_log_n = need / 4;
+        g_wave_log_n = need / pt::kWaveLogSlots;
         a.wave_log = g_wave_log;
     }
 #endif

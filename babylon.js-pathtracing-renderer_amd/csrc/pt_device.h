@@ -195,21 +195,40 @@ PT_D float box(f3 mn, f3 mx, f3 ro, f3 inv)
     return gmax(t0, 0.0f) > t1 ? kINF : t0;
 }
 // box() for a ray whose model-space origin and inverse direction are finite and nonzero and a box
-// without NaN: then no slab product is NaN, and IEEE min/max (v_min3 / v_max3) pick the same values
-// as the GLSL's y<x?y:x forms up to the sign of a zero, which only ever feeds comparisons
-// (the min/max are issued as v_min/v_max/v_min3/v_max3 directly: through fminf/fmaxf the compiler
-// adds a quieting v_max x,x per operand it cannot prove canonical, 6 per box)
-PT_D float vmin(float a, float b) { float r; asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
-PT_D float vmax(float a, float b) { float r; asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b)); return r; }
+// without NaN: then no slab product is NaN, and IEEE min/max (v_min / v_max / v_min3 / v_max3) pick
+// the same values as the GLSL's y<x?y:x forms up to the sign of a zero, which only ever feeds
+// comparisons. The min/max are issued directly: through fminf/fmaxf the compiler adds a quieting
+// v_max x,x per operand it cannot prove canonical, 6 per box.
 PT_D float vmax0(float a) { float r; asm("v_max_f32 %0, 0, %1" : "=v"(r) : "v"(a)); return r; }
-PT_D float vmin3(float a, float b, float c) { float r; asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c)); return r; }
-PT_D float vmax3(float a, float b, float c) { float r; asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c)); return r; }
+// as one inline-asm block (nr = (mn - ro) * inv, fr = (mx - ro) * inv; t0 = max3 of the three
+// min(nr, fr), t1 = min3 of the three max(nr, fr)): the compiler's hazard recognizer sees one block
+// instead of eleven and pads no s_nop between them
 PT_D float boxFast(f3 mn, f3 mx, f3 ro, f3 inv)
 {
-    f3 nr = (mn - ro) * inv;
-    f3 fr = (mx - ro) * inv;
-    float t0 = vmax3(vmin(nr.x, fr.x), vmin(nr.y, fr.y), vmin(nr.z, fr.z));
-    float t1 = vmin3(vmax(nr.x, fr.x), vmax(nr.y, fr.y), vmax(nr.z, fr.z));
+    float t0, t1, a0, a1, a2, b0, b1, b2;
+    asm("v_sub_f32 %2, %8, %14\n\t"
+        "v_sub_f32 %3, %9, %15\n\t"
+        "v_sub_f32 %4, %10, %16\n\t"
+        "v_sub_f32 %5, %11, %14\n\t"
+        "v_sub_f32 %6, %12, %15\n\t"
+        "v_sub_f32 %7, %13, %16\n\t"
+        "v_mul_f32 %2, %2, %17\n\t"
+        "v_mul_f32 %3, %3, %18\n\t"
+        "v_mul_f32 %4, %4, %19\n\t"
+        "v_mul_f32 %5, %5, %17\n\t"
+        "v_mul_f32 %6, %6, %18\n\t"
+        "v_mul_f32 %7, %7, %19\n\t"
+        "v_min_f32 %0, %2, %5\n\t"
+        "v_max_f32 %2, %2, %5\n\t"
+        "v_min_f32 %1, %3, %6\n\t"
+        "v_max_f32 %3, %3, %6\n\t"
+        "v_min_f32 %5, %4, %7\n\t"
+        "v_max_f32 %4, %4, %7\n\t"
+        "v_max3_f32 %0, %0, %1, %5\n\t"
+        "v_min3_f32 %1, %2, %3, %4"
+        : "=&v"(t0), "=&v"(t1), "=&v"(a0), "=&v"(a1), "=&v"(a2), "=&v"(b0), "=&v"(b1), "=&v"(b2)
+        : "v"(mn.x), "v"(mn.y), "v"(mn.z), "v"(mx.x), "v"(mx.y), "v"(mx.z), "v"(ro.x), "v"(ro.y), "v"(ro.z),
+          "v"(inv.x), "v"(inv.y), "v"(inv.z));
     return vmax0(t0) > t1 ? kINF : t0;
 }
 PT_D bool finite3(f3 v) { return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z); }
@@ -290,7 +309,8 @@ PT_D f3 pow22(f3 c) { return mk(gpow(c.x, 2.2f), gpow(c.y, 2.2f), gpow(c.z, 2.2f
 // order, cull with the same comparisons and test the same leaves, so they return the same hit;
 // `nodes` counts the reference's node fetches (2 texels each) either way.
 //
-// The stack policy Stk provides get(level) / put(level, float2) for levels < kStackLevels.
+// The stack policy Stk provides pop(level, sentinel) -> float2 and push(level, float2) -> bool
+// (false: beyond stackLevels[27], dropped) for any level >= 0.
 
 struct BvhResult {
     float triID, triU, triV;
@@ -304,15 +324,14 @@ struct BvhResult {
 template <class Stk>
 PT_D void stackPush(const TraceArgs& a, Stk& st, int si, float2 e, unsigned& ovf)
 {
-    if (si < kStackLevels) st.put(si, e);
-    else { ovf++; atomicOr(a.err, (unsigned)E_STACK); }   // GLSL would write out of bounds: dropped
+    if (!st.push(si, e)) { ovf++; atomicOr(a.err, (unsigned)E_STACK); }   // GLSL would write out of bounds: dropped
 }
 // a pop past stackLevels[27] (undefined in the GLSL) yields `sentinel`, whose tNear = INFINITY the
 // walk culls at once (pinned with the oracle; nothing is read out of bounds)
 template <class Stk>
 PT_D float2 stackPop(const Stk& st, int si, float2 sentinel)
 {
-    return si < kStackLevels ? st.get(si) : sentinel;
+    return st.pop(si, sentinel);
 }
 
 // The reference layout: a pushed entry is (node id, tNear); a pop re-fetches the node's two texels.
@@ -452,7 +471,7 @@ PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv
     // A leaf record is 48 B; its lane's fourth load reads the next record's first 8 B (or 0 past
     // the end of the array) and is not used.
     const uint32_t off = w.code & ~kLeafBit;
-#ifdef PT_SECPROF
+#ifdef PT_SECPROF_LOADS
     if (a.counters) {   // experiment: wave-level record loads, those with one record for all lanes, lanes served
         const uint32_t first = __builtin_amdgcn_readfirstlane(off);
         const unsigned long long act = __ballot(1), same = __ballot(off == first);
@@ -491,6 +510,9 @@ PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv
     float tu, tv;
     const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
     if (d < w.hitT) { w.hitT = d; w.triID = 8.0f * r2.y; w.triU = tu; w.triV = tv; w.lookup = true; }
+    // a use on this side too keeps the codes' load with the other three: sunk into the inner-node
+    // branch, it was issued only after a mixed wave's leaf tests (-3 % kernel time)
+    asm volatile("" ::"v"(r3.x));
     return true;
 }
 template <class Stk>

@@ -54,20 +54,30 @@ struct MegaStack {
 #else
 #define PT_SLABCOUNT(x)
 #endif
-    PT_D float2 get(int si) const
+    // the common case without branches: every lane reads LDS level min(si, kStackLds - 1); lanes
+    // deeper than the LDS levels then read the slab (or get the sentinel)
+    PT_D float2 pop(int si, float2 sentinel) const
     {
-        vf2 e;
         PT_SLABCOUNT(n_get++; if (si >= kStackLds) n_get_slab++;)
-        if (si < kStackLds) e = lds[si * LS + slot];
-        else e = slab[(unsigned)(si - kStackLds) * stride + deep];
+        vf2 e = lds[(unsigned)min(si, kStackLds - 1) * LS + slot];
+        if (si >= kStackLds) {
+            const vf2 s = { sentinel.x, sentinel.y };
+            e = si < kStackLevels ? slab[(unsigned)(si - kStackLds) * stride + deep] : s;
+        }
         return make_float2(e.x, e.y);
     }
-    PT_D void put(int si, float2 e)
+    // every lane writes LDS level min(si, kStackLds): level kStackLds is a scratch level that takes
+    // the deeper lanes' store, which then also goes to the slab (false beyond stackLevels[27])
+    PT_D bool push(int si, float2 e)
     {
         const vf2 v = { e.x, e.y };
         PT_SLABCOUNT(n_put++; if (si >= kStackLds) n_put_slab++;)
-        if (si < kStackLds) lds[si * LS + slot] = v;
-        else slab[(unsigned)(si - kStackLds) * stride + deep] = v;
+        lds[(unsigned)min(si, kStackLds) * LS + slot] = v;
+        if (si >= kStackLds) {
+            if (si >= kStackLevels) return false;
+            slab[(unsigned)(si - kStackLds) * stride + deep] = v;
+        }
+        return true;
     }
 };
 
@@ -228,7 +238,7 @@ static_assert(kTraceBlock == 64 || kTraceBlock == 256, "trace workgroups are one
 template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
 {
-    __shared__ float2 lds_stack[kStackLds * kTraceBlock];
+    __shared__ float2 lds_stack[(kStackLds + 1) * kTraceBlock];   // + the scratch level (MegaStack::push)
     __shared__ float lds_gout[8 * kTraceBlock];
     const unsigned tid = threadIdx.x;
     const int lane = tid & 63;
@@ -319,10 +329,12 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         atomicMax(&lds_sec[11], (unsigned long long)cnt.lane_steps);
         if (tid == 0) {
             const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
-            a.wave_log[4 * L] = w0_;
-            a.wave_log[4 * L + 1] = wall_clock64();
-            a.wave_log[4 * L + 2] = lds_sec[10];
-            a.wave_log[4 * L + 3] = lds_sec[11];
+            unsigned long long* wl = a.wave_log + (size_t)kWaveLogSlots * L;
+            wl[0] = w0_;
+            wl[1] = wall_clock64();
+            wl[2] = lds_sec[10];
+            wl[3] = lds_sec[11];
+            for (int k = 0; k < 8; k++) wl[4 + k] = lds_sec[k];   // section cycle sums (shader clock)
         }
     }
     if (COUNT && active) {   // stack traffic: pops beyond the LDS levels, pushes beyond; node fetches, leaf tests
@@ -387,7 +399,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_persist(TraceArgs 
                                                                        unsigned n_wave_tiles, unsigned per_wave,
                                                                        unsigned refill)
 {
-    __shared__ float2 lds_stack[kStackLds * kBlock];
+    __shared__ float2 lds_stack[(kStackLds + 1) * kBlock];   // + the scratch level (MegaStack::push)
     const unsigned tid = threadIdx.x;
     const unsigned lane = tid & 63u, wave = tid >> 6;
     const unsigned long long below = (1ull << lane) - 1ull;

@@ -38,7 +38,7 @@ struct Cnt {
     do {                                                                                      \
         const unsigned long long now_ = clock64();                                            \
         const int ln_ = __lane_id();                                                          \
-        if (COUNT && (cnt).sec && ln_ == __builtin_amdgcn_readfirstlane(ln_)) {                \
+        if ((cnt).sec && ln_ == __builtin_amdgcn_readfirstlane(ln_)) {                \
             (cnt).sec[k] += now_ - (cnt).sec[8]; (cnt).sec[8] = now_;                         \
         }                                                                                     \
     } while (0)

@@ -204,6 +204,13 @@ struct WfStack {
         if (si < kStackLds) lds[si * kBlock + slot] = v;
         else deep[(si - kStackLds) * dstride] = v;
     }
+    PT_D float2 pop(int si, float2 sentinel) const { return si < kStackLevels ? get(si) : sentinel; }
+    PT_D bool push(int si, float2 e)
+    {
+        if (si >= kStackLevels) return false;
+        put(si, e);
+        return true;
+    }
 };
 
 template <int PROG, bool COUNT>

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""BVH stack traffic of the megakernel (experiment build: tools/build_variant.sh secprof -DPT_SECPROF,
+"""BVH stack traffic of the megakernel (experiment build: tools/build_variant.sh secprof "-DPT_SECPROF -DPT_SECPROF_LOADS",
 run with PT_LIBPT=build_variants/secprof/libpt.so): per workload and launch, the stack pops and
 pushes of every walk and how many of them fall beyond the LDS levels into the global slab (each
 such access is a vector-memory instruction of its wave), next to the reference-priced node fetches

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Wave timeline of the production megakernel (experiment build: tools/build_variant.sh secprof
 -DPT_SECPROF, run with PT_LIBPT=build_variants/secprof/libpt.so): every workgroup (one wave)
-stores its (start, end) wall clock (100 MHz). Per workload: the launch span, the longest wave and
+stores its (start, end) wall clock (100 MHz) and its section cycle sums (PT_SEC marks: 0 camera ray,
+1 analytic objects, 2 BVH walk, 3 hit attributes, 4 shading). Per workload: the launch span, the longest wave and
 when it started, wave-duration percentiles, and how much of the span the last 1 % of waves cover.
 A longest wave close to the span means the launch is bound by its slowest wave, not by throughput."""
 import ctypes
@@ -17,6 +18,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import babylon_pt as bp  # noqa: E402
 import helpers as H      # noqa: E402
 
+SEC = ["camera", "analytic", "walk", "hit_attr", "shade"]
 fn = bp.lib().pt_debug_wave_log
 fn.restype = ctypes.c_size_t
 fn.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
@@ -38,7 +40,7 @@ for wl in (sys.argv[2:] or ["helmet", "bunny", "dragon", "sky_dragon"]):
     for call in p.synth_frame(10):
         p.play_call(call)
     ms, _ = e.timing_end(meta["scene"])
-    buf = np.zeros((1 << 20, 4), np.uint64)
+    buf = np.zeros((1 << 20, 12), np.uint64)
     n = fn(buf.ctypes.data, buf.shape[0])
     log = buf[:n].astype(np.int64)
     t0 = log[:, 0].min()
@@ -47,6 +49,8 @@ for wl in (sys.argv[2:] or ["helmet", "bunny", "dragon", "sky_dragon"]):
     span = en.max()
     order = np.argsort(en)
     i_long = int(np.argmax(d))
+    sec = log[:, 4:9].astype(np.float64)
+    slow = np.argsort(-d)[:max(1, n // 100)]
     np.save(os.path.join(out_dir, "wavelog_%s.npy" % wl), log)
     print(json.dumps({"workload": wl, "kernel_ms": round(ms, 4), "span_us": round(span, 1), "waves": int(n),
                       "longest_us": round(d.max(), 1), "longest_starts_us": round(s[i_long], 1),
@@ -56,5 +60,8 @@ for wl in (sys.argv[2:] or ["helmet", "bunny", "dragon", "sky_dragon"]):
                       "t_99pct_waves_done_us": round(float(en[order[int(0.99 * n)]]), 1),
                       "mean_us": round(float(d.mean()), 1),
                       "longest_wave_walk_iters": int(log[i_long, 2]), "longest_wave_max_lane_steps": int(log[i_long, 3]),
+                      "section_share": {nm: round(float(sec[:, k].sum() / max(1, sec.sum())), 4) for k, nm in enumerate(SEC)},
+                      "section_share_slowest_1pct": {nm: round(float(sec[slow, k].sum() / max(1, sec[slow].sum())), 4) for k, nm in enumerate(SEC)},
+                      "clock_ghz": round(float(sec.sum(axis=1).sum() / max(1e-9, (d * 1e3).sum())), 3),
                       "top10_iters_vs_lane": [[int(log[i, 2]), int(log[i, 3]), round(float(d[i]), 1)] for i in np.argsort(-d)[:10]]}), flush=True)
     e.dispose()
