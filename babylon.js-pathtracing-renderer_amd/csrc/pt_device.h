@@ -495,15 +495,15 @@ PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv
             tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
         }
         float cA = r3.x, cB = r3.y;   // codes as float bits: only moved, never computed on
-        if (tB < tA) {
-            float tt = tB; tB = tA; tA = tt;
-            float tc = cB; cB = cA; cA = tc;
-        }
-        if (tB < w.hitT) { w.code = __float_as_uint(cB); w.pop = false; }
-        if (tA < w.hitT) {
-            if (!w.pop) { stackPush(a, st, w.sp, make_float2(tB, cB), r.ovf); w.sp++; }
-            w.code = __float_as_uint(cA); w.pop = false;
-        }
+        // the reference's swap and two ifs as selects: the near child is next if it is hit, else the
+        // far one; the far one is pushed when both are hit
+        const bool sw = tB < tA;
+        const float tN = sw ? tB : tA, tF = sw ? tA : tB;
+        const float cN = sw ? cB : cA, cF = sw ? cA : cB;
+        const bool hitN = tN < w.hitT, hitF = tF < w.hitT;
+        if (hitN && hitF) { stackPush(a, st, w.sp, make_float2(tF, cF), r.ovf); w.sp++; }
+        w.code = __float_as_uint(hitN ? cN : hitF ? cF : __uint_as_float(w.code));
+        w.pop = !(hitN || hitF);
         return true;
     }
     r.leaves++;
