@@ -15,7 +15,13 @@ constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing
 #ifndef PT_STACK_LDS
 #define PT_STACK_LDS 7
 #endif
+// the child-pair walk of the texture-free mesh programs runs at 8 waves/SIMD (pt_device.h
+// kMinWaves), where 5 LDS levels (+ the scratch level) and the G-buffer fill the 160 KB of a CU
+#ifndef PT_STACK_LDS_PAIRS
+#define PT_STACK_LDS_PAIRS 5
+#endif
 constexpr int kStackLds = PT_STACK_LDS;        // levels kept in LDS per lane; deeper levels go to a global slab
+constexpr int kStackLdsMin = PT_STACK_LDS_PAIRS < PT_STACK_LDS ? PT_STACK_LDS_PAIRS : PT_STACK_LDS;   // sizes the slab
 
 // child-pair record codes: a node's rank code from the build's rank pass (rank >= 0 of an inner
 // node, -1 - rank of a leaf) -> the 32-bit code the walk carries: the record's byte offset in the

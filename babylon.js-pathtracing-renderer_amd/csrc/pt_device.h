@@ -51,18 +51,21 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, bool pair
     if (prog != PROG_GLTF && prog != PROG_HDRI && prog != PROG_SKYMESH) return prog;
     return prog + (textured ? PROG_TEX : 0) + (pairs ? PROG_PAIRS : 0);
 }
-// waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 80 -> 6; the
-// textured variant keeps 2 rather than spill)
-// (measured with one-wave workgroups and 7 LDS stack levels: 6 waves (80 VGPRs, 12 B of spill)
-// ~1-2 % ahead of 7 (72 VGPRs) and of 8 with 6 levels; 5 waves lose 6 %; 4-6 or 9-12 LDS levels
-// lose at 6 waves; the reference walk loses above 4)
+// waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 64 -> 8). Measured
+// with one-wave workgroups after the walk's branch-free stack (round 2): the child-pair walk at 8
+// waves with 5 LDS levels (64 VGPRs, 52 B of spill) 4 % ahead of 6 waves with 7 levels on the
+// dragon stand-in, 1 % on the bunny; 7 waves with 6 levels behind both; the textured variants
+// 1.3 % faster at 4 waves (128 VGPRs, 8 B of spill) than at 3, and slower with 5 LDS levels; the
+// reference walk loses above 4.
 #ifndef PT_MINWAVES_TEX
-#define PT_MINWAVES_TEX 2
+#define PT_MINWAVES_TEX 4
 #endif
 #ifndef PT_MINWAVES_PAIRS
-#define PT_MINWAVES_PAIRS 6
+#define PT_MINWAVES_PAIRS 8
 #endif
 template <int P> constexpr int kMinWaves = kHasTex<P> ? PT_MINWAVES_TEX : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
+// BVH stack levels in LDS per lane (the rest in the global slab): fewer for the 8-wave variants
+template <int P> constexpr int kStackLdsOf = (kPairs<P> && !kHasTex<P>) ? PT_STACK_LDS_PAIRS : kStackLds;
 
 // ------------------------------------------------------------------------------ per-lane state
 struct Path {

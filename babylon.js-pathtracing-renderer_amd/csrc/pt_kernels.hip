@@ -40,13 +40,13 @@ namespace pt {
 typedef float vf2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) vf2 lds_float2;
 typedef __attribute__((address_space(1))) vf2 glb_float2;
-// LS = lanes of the block = the stride of one stack level in LDS
-template <int LS>
+// LS = lanes of the block = the stride of one stack level in LDS; NL = stack levels in LDS
+template <int LS, int NL>
 struct MegaStack {
     lds_float2* lds;
     unsigned slot;
     glb_float2* slab;     // the spill slab (wave-uniform base) ...
-    unsigned deep;        // ... and this lane's index in it: level kStackLds, levels `stride` apart
+    unsigned deep;        // ... and this lane's index in it: level NL, levels `stride` apart
     unsigned stride;      //     (32-bit: a 64-bit per-lane pointer costs two VGPRs for the whole path)
 #ifdef PT_SECPROF
     mutable unsigned n_get = 0, n_get_slab = 0, n_put = 0, n_put_slab = 0;
@@ -54,28 +54,28 @@ struct MegaStack {
 #else
 #define PT_SLABCOUNT(x)
 #endif
-    // the common case without branches: every lane reads LDS level min(si, kStackLds - 1); lanes
+    // the common case without branches: every lane reads LDS level min(si, NL - 1); lanes
     // deeper than the LDS levels then read the slab (or get the sentinel)
     PT_D float2 pop(int si, float2 sentinel) const
     {
-        PT_SLABCOUNT(n_get++; if (si >= kStackLds) n_get_slab++;)
-        vf2 e = lds[(unsigned)min(si, kStackLds - 1) * LS + slot];
-        if (si >= kStackLds) {
+        PT_SLABCOUNT(n_get++; if (si >= NL) n_get_slab++;)
+        vf2 e = lds[(unsigned)min(si, NL - 1) * LS + slot];
+        if (si >= NL) {
             const vf2 s = { sentinel.x, sentinel.y };
-            e = si < kStackLevels ? slab[(unsigned)(si - kStackLds) * stride + deep] : s;
+            e = si < kStackLevels ? slab[(unsigned)(si - NL) * stride + deep] : s;
         }
         return make_float2(e.x, e.y);
     }
-    // every lane writes LDS level min(si, kStackLds): level kStackLds is a scratch level that takes
+    // every lane writes LDS level min(si, NL): level NL is a scratch level that takes
     // the deeper lanes' store, which then also goes to the slab (false beyond stackLevels[27])
     PT_D bool push(int si, float2 e)
     {
         const vf2 v = { e.x, e.y };
-        PT_SLABCOUNT(n_put++; if (si >= kStackLds) n_put_slab++;)
-        lds[(unsigned)min(si, kStackLds) * LS + slot] = v;
-        if (si >= kStackLds) {
+        PT_SLABCOUNT(n_put++; if (si >= NL) n_put_slab++;)
+        lds[(unsigned)min(si, NL) * LS + slot] = v;
+        if (si >= NL) {
             if (si >= kStackLevels) return false;
-            slab[(unsigned)(si - kStackLds) * stride + deep] = v;
+            slab[(unsigned)(si - NL) * stride + deep] = v;
         }
         return true;
     }
@@ -133,7 +133,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     f3 inv = mk(grcp(D.x), grcp(D.y), grcp(D.z));
     const bool dbl = (!a.uses_albedo && a.model_mat == TRANSPARENT);
     BvhResult br = { 0.0f, 0.0f, 0.0f, false, 1u, 0u, 0u };
-    MegaStack<LS> st{ (lds_float2*)lds, lane_slot, (glb_float2*)a.spill, deep, a.spill_stride };
+    MegaStack<LS, kStackLdsOf<PROG>> st{ (lds_float2*)lds, lane_slot, (glb_float2*)a.spill, deep, a.spill_stride };
     if (kPairs<PROG>) {   // the root's box from the kernel arguments (the same floats as texels 0-1)
         const float* rb = a.bvh_root_box;
         const float rootT = box(mk(rb[0], rb[1], rb[2]), mk(rb[3], rb[4], rb[5]), O, inv);
@@ -238,7 +238,7 @@ static_assert(kTraceBlock == 64 || kTraceBlock == 256, "trace workgroups are one
 template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
 {
-    __shared__ float2 lds_stack[(kStackLds + 1) * kTraceBlock];   // + the scratch level (MegaStack::push)
+    __shared__ float2 lds_stack[(kStackLdsOf<PROG> + 1) * kTraceBlock];   // + the scratch level (MegaStack::push)
     __shared__ float lds_gout[8 * kTraceBlock];
     const unsigned tid = threadIdx.x;
     const int lane = tid & 63;
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_persist(TraceArgs 
                                                                        unsigned n_wave_tiles, unsigned per_wave,
                                                                        unsigned refill)
 {
-    __shared__ float2 lds_stack[(kStackLds + 1) * kBlock];   // + the scratch level (MegaStack::push)
+    __shared__ float2 lds_stack[(kStackLdsOf<PROG> + 1) * kBlock];   // + the scratch level (MegaStack::push)
     const unsigned tid = threadIdx.x;
     const unsigned lane = tid & 63u, wave = tid >> 6;
     const unsigned long long below = (1ull << lane) - 1ull;
