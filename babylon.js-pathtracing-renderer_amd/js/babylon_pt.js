@@ -354,17 +354,21 @@ function install(BABYLON, opts) {
   set('Texture', Texture);
   set('EffectWrapper', EffectWrapper);
   set('EffectRenderer', EffectRenderer);
-  return { addon, Engine, decodePNG, decodeHDR, decodeImage, nativeBVH: () => nativeBVH(addon) };
+  return { addon, Engine, decodePNG, decodeHDR, decodeImage, nativeBVH: (device) => nativeBVH(addon, device) };
 }
 
 // BVH_Build_Iterative(workList, aabb_array) (js/BVH_Fast_Builder.js:320-406) over libpt's native
-// builder (same tree, same bits). A host installs it after loading BVH_Fast_Builder.js:
-//   globalThis.BVH_Build_Iterative = require('.../babylon_pt.js').nativeBVH(addon);
-function nativeBVH(addon) {
+// builder (same tree, same bits); with a device number, over the device build (pt_bvh_build_gpu,
+// same bits again). A host installs it after loading BVH_Fast_Builder.js:
+//   globalThis.BVH_Build_Iterative = require('.../babylon_pt.js').nativeBVH(addon[, device]);
+function nativeBVH(addon, device) {
   return function BVH_Build_Iterative(workList, aabbArray) {
     const n = workList.length;
     const out = new Float32Array(8 * (2 * n - 1));
-    const rc = addon.pt_bvh_build(aabbArray.subarray(0, 9 * n), Uint32Array.from(workList), out);
+    const work = Uint32Array.from(workList);
+    const rc = device === undefined || device === null
+      ? addon.pt_bvh_build(aabbArray.subarray(0, 9 * n), work, out)
+      : addon.pt_bvh_build_gpu(device, aabbArray, work, out);
     if (rc < 0) throw new Error('pt_bvh_build: ' + (ERR[rc] || rc));
     aabbArray.set(out, 0);
   };

@@ -362,6 +362,22 @@ static napi_value BvhBuild(napi_env env, napi_callback_info info)
     if (!aabb || !work || !out || la < (size_t)n * 36) return num(env, PT_ERR_ARG);
     return num(env, pt_bvh_build(aabb, work, n, out, (int)(lo / 32)));
 }
+/* pt_bvh_build_gpu(device, aabbIn, work, out) -> node count (the device build, same bits) */
+static napi_value BvhBuildGpu(napi_env env, napi_callback_info info)
+{
+    napi_value a[MAXARGS]; if (args(env, info, a, 4) < 0) return NULL;
+    int32_t dev = 0;
+    CHECK(napi_get_value_int32(env, a[0], &dev));
+    size_t la, lw, lo;
+    const float* aabb = (const float*)bytes_of(env, a[1], &la);
+    const uint32_t* work = (const uint32_t*)bytes_of(env, a[2], &lw);
+    float* out = (float*)bytes_of(env, a[3], &lo);
+    int n = (int)(lw / 4);
+    if (!aabb || !work || !out) return num(env, PT_ERR_ARG);
+    for (int i = 0; i < n; i++)
+        if ((size_t)work[i] * 36 + 36 > la) return num(env, PT_ERR_ARG);
+    return num(env, pt_bvh_build_gpu(dev, aabb, work, n, out, (int)(lo / 32), NULL));
+}
 static napi_value Version(napi_env env, napi_callback_info info)
 {
     napi_value r; (void)info;
@@ -386,7 +402,7 @@ static napi_value Init(napi_env env, napi_value exports)
         { "pt_bvh_layout_used", BvhLayoutUsed }, { "pt_set_stream", SetStream }, { "pt_texture_device_ptr", TexDevicePtr },
         { "pt_last_render_ms", LastRenderMs }, { "pt_timing_begin", TimingBegin }, { "pt_timing_end", TimingEnd },
         { "pt_set_counting", SetCounting }, { "pt_read_counters", ReadCounters }, { "pt_reset_counters", ResetCounters }, { "pt_queue_stats", QueueStats },
-        { "pt_bvh_build", BvhBuild }, { "pt_version", Version },
+        { "pt_bvh_build", BvhBuild }, { "pt_bvh_build_gpu", BvhBuildGpu }, { "pt_version", Version },
     };
     for (size_t i = 0; i < sizeof(F) / sizeof(F[0]); i++) {
         napi_value fn;

@@ -39,7 +39,7 @@ SYMBOLS = [
     "pt_render_target_resize", "pt_texture_size", "pt_texture_destroy",
     "pt_render", "pt_read_pixels", "pt_write_pixels",
     "pt_set_row_partition", "pt_set_output_partition", "pt_canvas_wrap", "pt_set_backend", "pt_set_bvh_layout", "pt_bvh_layout_used", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
-    "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_math_exhaustive", "pt_bvh_build", "pt_version",
+    "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_math_exhaustive", "pt_bvh_build", "pt_bvh_build_gpu", "pt_version",
 ]
 
 _lib = None
@@ -78,6 +78,7 @@ def lib():
         "pt_canvas_wrap": ([vp, i32, i32, vp], i32), "pt_set_stream": ([vp, vp], i32),
         "pt_set_bvh_layout": ([vp, i32], i32), "pt_bvh_layout_used": ([vp], i32),
         "pt_bvh_build": ([vp, vp, i32, vp, i32], i32),
+        "pt_bvh_build_gpu": ([i32, vp, vp, i32, vp, i32, f32p], i32),
         "pt_last_render_ms": ([vp, i32, f32p], i32), "pt_set_counting": ([vp, i32], i32),
         "pt_timing_begin": ([vp], i32),
         "pt_timing_end": ([vp, i32, ctypes.POINTER(ctypes.c_double), ip], i32),
@@ -402,6 +403,23 @@ def bvh_build(aabb_in, work=None):
     if rc < 0:
         raise PtError("pt_bvh_build: %s" % ERRORS.get(rc, rc))
     return out[:rc]
+
+
+def bvh_build_gpu(aabb_in, work=None, device=0):
+    """The same build on the device (pt_bvh_build_gpu, csrc/pt_bvh_gpu.hip): returns (nodes, ms of
+    device time)."""
+    aabb_in = np.ascontiguousarray(aabb_in, dtype=np.float32).reshape(-1, 9)
+    n = aabb_in.shape[0]
+    work = np.arange(n, dtype=np.uint32) if work is None else np.ascontiguousarray(work, dtype=np.uint32)
+    if len(work) and int(work.max()) >= n:
+        raise PtError("pt_bvh_build_gpu: work names a triangle beyond aabb_in")
+    out = np.zeros((max(1, 2 * len(work) - 1), 8), np.float32)
+    ms = ctypes.c_float(0.0)
+    rc = lib().pt_bvh_build_gpu(device, aabb_in.ctypes.data, work.ctypes.data, len(work), out.ctypes.data,
+                                out.shape[0], ctypes.byref(ms))
+    if rc < 0:
+        raise PtError("pt_bvh_build_gpu: %s" % ERRORS.get(rc, rc))
+    return out[:rc], ms.value
 
 
 def splitmix64_uniforms(seed, n):

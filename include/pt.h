@@ -207,6 +207,13 @@ int pt_math_exhaustive(pt_ctx* ctx, int op, uint64_t* mismatches);
  * and bits, and returns the node count (2n-1), or a negative pt_status (max_nodes too small). No
  * context or device needed. */
 int pt_bvh_build(const float* aabb_in, const uint32_t* work, int n, float* nodes_out, int max_nodes);
+/* The same build on a gfx950 device (csrc/pt_bvh_gpu.hip): level by level, every node of a depth
+ * split together, the same tree and bits as pt_bvh_build (js/BVH_Fast_Builder.js:43-406; the page
+ * runs it at js/GLTF_Model_Path_Tracing.js:456-462). aabb_in holds 9 floats for every triangle id
+ * up to the largest in work; n <= 2^24. Synchronous. Returns the node count (2n-1) or a negative
+ * pt_status; *ms_out (may be NULL) = device time of the build, uploads and read-back excluded. */
+int pt_bvh_build_gpu(int device, const float* aabb_in, const uint32_t* work, int n, float* nodes_out,
+                     int max_nodes, float* ms_out);
 /* Library identity: "libpt <version> gfx950" */
 const char* pt_version(void);
 
