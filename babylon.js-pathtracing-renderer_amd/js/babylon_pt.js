@@ -114,17 +114,19 @@ function decodePNG(buf) {
 }
 
 // ---------------------------------------------------------------------------------- JPEG (host)
-// JPEG maps (the glTF models' PBR textures) are decoded by the Python host's decoder
-// (decode_image.py: Pillow / libjpeg-turbo) in a child process; PT_PYTHON names the interpreter.
-function decodeImage(buf) {
+// JPEG maps (the glTF models' PBR textures) are decoded by libpt (pt_jpeg_decode_rgba8,
+// csrc/pt_jpeg.cpp: libjpeg-turbo's default decompression reproduced bit for bit), through the addon.
+function decodeImage(buf, addon) {
   buf = Buffer.from(buf.buffer ? Buffer.from(buf.buffer, buf.byteOffset, buf.byteLength) : buf);
   if (buf.length >= 4 && buf.readUInt32BE(0) === 0x89504e47) return decodePNG(buf);
   if (!(buf.length >= 2 && buf[0] === 0xff && buf[1] === 0xd8)) throw new Error('not a PNG or JPEG image');
-  const out = require('child_process').execFileSync(process.env.PT_PYTHON || 'python3',
-    [path.join(__dirname, 'decode_image.py')], { input: buf, maxBuffer: 1 << 30 });
-  const w = out.readUInt32LE(0), h = out.readUInt32LE(4);
-  if (out.length !== 8 + 4 * w * h) throw new Error('image decode: short output');
-  return { width: w, height: h, data: new Uint8Array(out.buffer, out.byteOffset + 8, 4 * w * h) };
+  addon = addon || loadAddon();
+  const wh = addon.pt_jpeg_size(buf);
+  if (typeof wh === 'number') throw new Error('JPEG: ' + (ERR[wh] || wh));
+  const data = new Uint8Array(4 * wh[0] * wh[1]);
+  const rc = addon.pt_jpeg_decode_rgba8(buf, data);
+  if (rc < 0) throw new Error('JPEG: ' + (ERR[rc] || rc));
+  return { width: wh[0], height: wh[1], data };
 }
 
 function install(BABYLON, opts) {
@@ -224,7 +226,7 @@ function install(BABYLON, opts) {
     const bytes = t._buffer;
     if (!bytes || typeof bytes === 'string') return;
     try {
-      const img = decodeImage(bytes);
+      const img = decodeImage(bytes, addon);
       const sm = typeof t.samplingMode === 'number' ? t.samplingMode : 3;
       const h = addon.pt_texture_create_rgba8(ctx, img.width, img.height, img.data, sm, t._invertY ? 1 : 0);
       if (typeof h !== 'number') t._ptForeign = label(h, t.name || t.url || 'texture');
@@ -280,7 +282,7 @@ function install(BABYLON, opts) {
     }
     _upload(bytes, what) {
       try {
-        const img = decodeImage(bytes);
+        const img = decodeImage(bytes, addon);
         this._size = { width: img.width, height: img.height };
         const h = addon.pt_texture_create_rgba8(this._ctx, img.width, img.height, img.data, this._sampling, this._invertY ? 1 : 0);
         if (typeof h !== 'number') this._pt = label(h, this._name || what);

@@ -378,6 +378,29 @@ static napi_value BvhBuildGpu(napi_env env, napi_callback_info info)
         if ((size_t)work[i] * 36 + 36 > la) return num(env, PT_ERR_ARG);
     return num(env, pt_bvh_build_gpu(dev, aabb, work, n, out, (int)(lo / 32), NULL));
 }
+/* pt_jpeg_size(bytes: Uint8Array) -> [width, height] or a negative pt_status */
+static napi_value JpegSize(napi_env env, napi_callback_info info)
+{
+    napi_value a[MAXARGS], r; if (args(env, info, a, 1) < 0) return NULL;
+    size_t n; const uint8_t* d = (const uint8_t*)bytes_of(env, a[0], &n);
+    int w = 0, h = 0;
+    const int rc = d ? pt_jpeg_size(d, n, &w, &h) : PT_ERR_ARG;
+    if (rc != PT_OK) return num(env, rc);
+    CHECK(napi_create_array_with_length(env, 2, &r));
+    napi_set_element(env, r, 0, num(env, w));
+    napi_set_element(env, r, 1, num(env, h));
+    return r;
+}
+/* pt_jpeg_decode_rgba8(bytes: Uint8Array, out: Uint8Array (4 * w * h)) -> status */
+static napi_value JpegDecode(napi_env env, napi_callback_info info)
+{
+    napi_value a[MAXARGS]; if (args(env, info, a, 2) < 0) return NULL;
+    size_t n, cap;
+    const uint8_t* d = (const uint8_t*)bytes_of(env, a[0], &n);
+    uint8_t* out = (uint8_t*)bytes_of(env, a[1], &cap);
+    if (!d || !out) return num(env, PT_ERR_ARG);
+    return num(env, pt_jpeg_decode_rgba8(d, n, out, cap));
+}
 static napi_value Version(napi_env env, napi_callback_info info)
 {
     napi_value r; (void)info;
@@ -402,7 +425,8 @@ static napi_value Init(napi_env env, napi_value exports)
         { "pt_bvh_layout_used", BvhLayoutUsed }, { "pt_set_stream", SetStream }, { "pt_texture_device_ptr", TexDevicePtr },
         { "pt_last_render_ms", LastRenderMs }, { "pt_timing_begin", TimingBegin }, { "pt_timing_end", TimingEnd },
         { "pt_set_counting", SetCounting }, { "pt_read_counters", ReadCounters }, { "pt_reset_counters", ResetCounters }, { "pt_queue_stats", QueueStats },
-        { "pt_bvh_build", BvhBuild }, { "pt_bvh_build_gpu", BvhBuildGpu }, { "pt_version", Version },
+        { "pt_bvh_build", BvhBuild }, { "pt_bvh_build_gpu", BvhBuildGpu },
+        { "pt_jpeg_size", JpegSize }, { "pt_jpeg_decode_rgba8", JpegDecode }, { "pt_version", Version },
     };
     for (size_t i = 0; i < sizeof(F) / sizeof(F[0]); i++) {
         napi_value fn;

@@ -39,7 +39,7 @@ SYMBOLS = [
     "pt_render_target_resize", "pt_texture_size", "pt_texture_destroy",
     "pt_render", "pt_read_pixels", "pt_write_pixels",
     "pt_set_row_partition", "pt_set_output_partition", "pt_canvas_wrap", "pt_set_backend", "pt_set_bvh_layout", "pt_bvh_layout_used", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
-    "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_math_exhaustive", "pt_bvh_build", "pt_bvh_build_gpu", "pt_version",
+    "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_math_exhaustive", "pt_bvh_build", "pt_bvh_build_gpu", "pt_jpeg_size", "pt_jpeg_decode_rgba8", "pt_version",
 ]
 
 _lib = None
@@ -79,6 +79,8 @@ def lib():
         "pt_set_bvh_layout": ([vp, i32], i32), "pt_bvh_layout_used": ([vp], i32),
         "pt_bvh_build": ([vp, vp, i32, vp, i32], i32),
         "pt_bvh_build_gpu": ([i32, vp, vp, i32, vp, i32, f32p], i32),
+        "pt_jpeg_size": ([ctypes.c_char_p, ctypes.c_size_t, ip, ip], i32),
+        "pt_jpeg_decode_rgba8": ([ctypes.c_char_p, ctypes.c_size_t, vp, ctypes.c_size_t], i32),
         "pt_last_render_ms": ([vp, i32, f32p], i32), "pt_set_counting": ([vp, i32], i32),
         "pt_timing_begin": ([vp], i32),
         "pt_timing_end": ([vp, i32, ctypes.POINTER(ctypes.c_double), ip], i32),
@@ -420,6 +422,21 @@ def bvh_build_gpu(aabb_in, work=None, device=0):
     if rc < 0:
         raise PtError("pt_bvh_build_gpu: %s" % ERRORS.get(rc, rc))
     return out[:rc], ms.value
+
+
+def decode_jpeg(data):
+    """JPEG bytes -> (h, w, 4) uint8 RGBA rows top first (pt_jpeg_decode_rgba8: libjpeg-turbo's
+    default decompression, bit for bit)."""
+    data = bytes(data)
+    w, h = ctypes.c_int(0), ctypes.c_int(0)
+    rc = lib().pt_jpeg_size(data, len(data), ctypes.byref(w), ctypes.byref(h))
+    if rc < 0:
+        raise PtError("pt_jpeg_size: %s" % ERRORS.get(rc, rc))
+    out = np.zeros((h.value, w.value, 4), np.uint8)
+    rc = lib().pt_jpeg_decode_rgba8(data, len(data), out.ctypes.data, out.size)
+    if rc < 0:
+        raise PtError("pt_jpeg_decode_rgba8: %s" % ERRORS.get(rc, rc))
+    return out
 
 
 def splitmix64_uniforms(seed, n):

@@ -214,6 +214,15 @@ int pt_bvh_build(const float* aabb_in, const uint32_t* work, int n, float* nodes
  * pt_status; *ms_out (may be NULL) = device time of the build, uploads and read-back excluded. */
 int pt_bvh_build_gpu(int device, const float* aabb_in, const uint32_t* work, int n, float* nodes_out,
                      int max_nodes, float* ms_out);
+/* JPEG decode for the hosts' texture loading: replaces the browser's decode of the glTF models'
+ * map images, which the glTF loader hands to `new BABYLON.Texture` (js/GLTF_Model_Path_Tracing.js:
+ * 252-274) and the page binds with effect.setTexture (:822-825). libjpeg-turbo's default
+ * decompression reproduced bit for bit (csrc/pt_jpeg.cpp: baseline and progressive, accurate
+ * integer IDCT, fancy upsampling, RGB output); RGBA8 rows top first, alpha 255. pt_jpeg_size reads
+ * the frame header; pt_jpeg_decode_rgba8 needs capacity >= 4 * width * height. Host code: no
+ * context or device. PT_ERR_UNSUPPORTED for arithmetic-coded, 12-bit, CMYK or stored-RGB files. */
+int pt_jpeg_size(const uint8_t* data, size_t size, int* width, int* height);
+int pt_jpeg_decode_rgba8(const uint8_t* data, size_t size, uint8_t* rgba, size_t capacity);
 /* Library identity: "libpt <version> gfx950" */
 const char* pt_version(void);
 

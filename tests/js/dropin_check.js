@@ -45,7 +45,12 @@ const mock = {
     return 0;
   },
   pt_read_pixels: () => 0,
+  // JPEG decode is host code of the real addon (no device): the glTF maps decode as in production
+  pt_jpeg_size: (...a) => realAddon().pt_jpeg_size(...a),
+  pt_jpeg_decode_rgba8: (...a) => realAddon().pt_jpeg_decode_rgba8(...a),
 };
+let real_ = null;
+const realAddon = () => real_ || (real_ = require('../../babylon.js-pathtracing-renderer_amd/js/babylon_pt.js').loadAddon());
 let raw = 0;
 const rawData = [];
 const u8 = [];   // every RGBA8 texture created (blue noise, PBR maps)

@@ -1,0 +1,85 @@
+"""libpt's JPEG decoder (pt_jpeg_decode_rgba8, csrc/pt_jpeg.cpp) against libjpeg-turbo as Pillow
+runs it (default decompression: accurate integer IDCT, fancy upsampling, RGB output): the
+DamagedHelmet's four map files the reference ships (three baseline 4:2:0, one progressive 4:4:4),
+then JPEGs that libjpeg-turbo itself encodes here over the subsamplings, progressive and
+baseline, odd sizes, grayscale and restart intervals. Host code: runs on CPU."""
+import io
+import os
+
+import numpy as np
+import pytest
+
+import helpers as H
+
+MAPS = os.path.join(H.GOLD, "helmet_maps")
+
+
+def pillow_rgba(data):
+    from PIL import Image
+    return np.asarray(Image.open(io.BytesIO(data)).convert("RGBA"), dtype=np.uint8)
+
+
+@pytest.mark.parametrize("name", ["Default_albedo", "Default_emissive", "Default_metalRoughness", "Default_normal"])
+def test_helmet_maps_decode_as_libjpeg_turbo(name):
+    import babylon_pt as bp
+    data = open(os.path.join(MAPS, name + ".jpg"), "rb").read()
+    got = bp.decode_jpeg(data)
+    assert got.shape == (2048, 2048, 4)
+    assert np.array_equal(got, pillow_rgba(data))
+
+
+def _encode(img, **kw):
+    buf = io.BytesIO()
+    img.save(buf, "JPEG", **kw)
+    return buf.getvalue()
+
+
+@pytest.mark.parametrize("size", [(64, 48), (37, 29), (1, 1), (2, 3), (17, 130)])
+@pytest.mark.parametrize("subsampling", [0, 1, 2])          # 4:4:4, 4:2:2, 4:2:0
+@pytest.mark.parametrize("progressive", [False, True])
+def test_encoded_variants_decode_as_libjpeg_turbo(size, subsampling, progressive):
+    from PIL import Image
+    import babylon_pt as bp
+    rng = np.random.default_rng(size[0] * 131 + size[1] * 7 + subsampling)
+    w, h = size
+    yy, xx = np.mgrid[0:h, 0:w]
+    base = np.stack([xx * 255 // max(1, w - 1), yy * 255 // max(1, h - 1), (xx ^ yy) & 255], -1)
+    pix = np.clip(base + rng.integers(-40, 40, (h, w, 3)), 0, 255).astype(np.uint8)
+    for q in (35, 90):
+        data = _encode(Image.fromarray(pix, "RGB"), quality=q, subsampling=subsampling, progressive=progressive)
+        assert np.array_equal(bp.decode_jpeg(data), pillow_rgba(data)), (size, subsampling, progressive, q)
+
+
+@pytest.mark.parametrize("progressive", [False, True])
+def test_grayscale_decodes_as_libjpeg_turbo(progressive):
+    from PIL import Image
+    import babylon_pt as bp
+    rng = np.random.default_rng(3)
+    pix = rng.integers(0, 256, (45, 70), dtype=np.uint8)
+    data = _encode(Image.fromarray(pix, "L"), quality=80, progressive=progressive)
+    got = bp.decode_jpeg(data)
+    assert np.array_equal(got, pillow_rgba(data))
+
+
+def test_restart_intervals_decode_as_libjpeg_turbo():
+    from PIL import Image
+    import babylon_pt as bp
+    rng = np.random.default_rng(5)
+    pix = rng.integers(0, 256, (96, 120, 3), dtype=np.uint8)
+    try:
+        data = _encode(Image.fromarray(pix, "RGB"), quality=75, restart_marker_blocks=3)
+    except TypeError:
+        pytest.skip("this Pillow has no restart_marker_blocks")
+    assert b"\xff\xdd" in data
+    assert np.array_equal(bp.decode_jpeg(data), pillow_rgba(data))
+
+
+def test_bad_input_is_a_code_not_a_crash():
+    import babylon_pt as bp
+    with pytest.raises(bp.PtError):
+        bp.decode_jpeg(b"\xff\xd8\xff\xd9")
+    with pytest.raises(bp.PtError):
+        bp.decode_jpeg(b"not a jpeg at all")
+    data = open(os.path.join(MAPS, "Default_emissive.jpg"), "rb").read()
+    with pytest.raises(bp.PtError):            # truncated: no EOI
+        bp.decode_jpeg(data[: len(data) // 2])
