@@ -128,6 +128,11 @@ struct TraceArgs {
     const unsigned* order;
     unsigned* cost;
     unsigned prio_tiles;   // the first prio_tiles tiles of `order` (the slowest last frame) run at s_setprio 3
+    // *split (written by the previous pt_order_build; a multiple of 8): the first *split tiles of
+    // `order` are shaded by 16 waves of 16 lanes (4x4 pixels) instead of 4 waves of 64 (pt_trace);
+    // the grid carries padding rows for up to split_cap of them
+    const unsigned* split;
+    unsigned ntiles;       // 16x16 tiles of the draw
     Tex8 albedo, bump, metal, emissive;
     // diagnostics
     unsigned long long* counters;   // C_NUM entries, only with counting builds

@@ -30,7 +30,8 @@
 extern "C" {
 hipError_t pt_launch_exhaustive(int op, unsigned long long* bad, hipStream_t s);
 hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s);
-hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, hipStream_t s);
+hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,
+                                 unsigned split_cap, unsigned dominance, hipStream_t s);
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
@@ -124,6 +125,9 @@ struct Dev {
     // path-tracing draw, reused when the next draw has the same grid, target and program
     bool lpt = true;
     unsigned prio_tiles = 0;   // longest-first: the first prio_tiles 16x16 tiles run at raised wave priority
+    unsigned split_tiles = 32; // longest-first: at most this many of the slowest tiles shaded by 16-lane waves
+                               // (pt_trace, pt_order_build; PT_SPLIT_TILES)
+    unsigned split_dominance = 8;   // ... when the slowest wave costs this many times the mean (PT_SPLIT_ALWAYS=1: 0)
     unsigned* lpt_mem = nullptr;            // cost[4 * ntiles] | order[ntiles]
     size_t lpt_n = 0, lpt_cap = 0;
     bool lpt_valid = false;
@@ -582,8 +586,17 @@ int render_trace(DevFx* fx, DevTex* target)
         if (mesh && (rc = spill_reserve(c, lanes))) return rc;
         a.spill = c->mk_spill;
         a.spill_stride = lanes;
-    } else if (c->backend == PT_BACKEND_MEGAKERNEL && mesh) {
-        const size_t lanes = (size_t)gx * gy * pt::kBlock;
+    }
+    // megakernel: the longest-first order of the last draw (if it applies) and the tiles to split;
+    // split tiles take 12 more workgroups each, in padding rows of the grid
+    const size_t n_tiles = (size_t)gx * gy;
+    const bool lpt_same = c->lpt_valid && c->lpt_n == n_tiles && c->lpt_key_target == target &&
+                          c->lpt_key_prog == fx->prog && c->lpt_key_part == c->part && c->lpt_key_parts == c->num_parts;
+    const unsigned split = (c->backend == PT_BACKEND_MEGAKERNEL && c->lpt && !c->counting && lpt_same)
+                               ? (unsigned)std::min<size_t>(c->split_tiles, n_tiles) & ~7u : 0u;   // the cap
+    const int gy_grid = gy + (int)((12u * split + 4u * gx - 1) / (4u * gx));
+    if (c->backend == PT_BACKEND_MEGAKERNEL && mesh) {
+        const size_t lanes = (size_t)gx * gy_grid * pt::kBlock;
         if (lanes * (pt::kStackLevels - pt::kStackLdsMin) > 0xffffffffull)   // 32-bit slab index
             return fail(c, PT_ERR_ARG, "render target too large for the BVH stack slab");
         int rc = spill_reserve(c, lanes);
@@ -603,13 +616,12 @@ int render_trace(DevFx* fx, DevTex* target)
             HIPCHK(c, pt_launch_finish(&a, &c->gb, gx, gy, c->stream));
         } else {
             // longest-first: the previous draw's wave durations order this one's workgroups
-            const size_t n = (size_t)gx * gy;   // 16x16 tiles
-            const bool same = c->lpt_valid && c->lpt_n == n && c->lpt_key_target == target && c->lpt_key_prog == fx->prog &&
-                              c->lpt_key_part == c->part && c->lpt_key_parts == c->num_parts;
+            const size_t n = n_tiles;   // 16x16 tiles
+            const bool same = lpt_same;
             if (c->lpt && !c->counting) {
                 if (c->lpt_cap < n) {
                     if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
-                    HIPCHK(c, hipMalloc(&c->lpt_mem, 5 * n * sizeof(unsigned)));
+                    HIPCHK(c, hipMalloc(&c->lpt_mem, (5 * n + 1) * sizeof(unsigned)));   // cost | order | split
                     HIPCHK(c, hipMemsetAsync(c->lpt_mem, 0, 4 * n * sizeof(unsigned), c->stream));
                     c->lpt_cap = n;
                     c->lpt_valid = false;
@@ -619,10 +631,14 @@ int render_trace(DevFx* fx, DevTex* target)
                 a.order = same ? c->lpt_mem + 4 * c->lpt_cap : nullptr;
                 a.cost = c->lpt_mem;
                 a.prio_tiles = a.order ? c->prio_tiles : 0u;
+                a.split = (a.order && split) ? c->lpt_mem + 5 * c->lpt_cap : nullptr;
             }
-            HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, gy, c->stream));
+            a.ntiles = (unsigned)n;
+            HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, c->stream));
             if (a.cost) {
-                HIPCHK(c, pt_launch_order_build((unsigned)n, a.cost, c->lpt_mem + 4 * c->lpt_cap, c->stream));
+                HIPCHK(c, pt_launch_order_build((unsigned)n, a.cost, c->lpt_mem + 4 * c->lpt_cap,
+                                                c->lpt_mem + 5 * c->lpt_cap, (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u,
+                                                c->split_dominance, c->stream));
                 c->lpt_valid = true; c->lpt_n = n; c->lpt_key_target = target; c->lpt_key_prog = fx->prog;
                 c->lpt_key_part = c->part; c->lpt_key_parts = c->num_parts;
             }
@@ -774,6 +790,8 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_PERSIST_TILES")) c->persist_tiles = (unsigned)std::max(1, std::atoi(v));
     if (const char* v = std::getenv("PT_LPT")) c->lpt = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_PRIO_TILES")) c->prio_tiles = (unsigned)std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("PT_SPLIT_ALWAYS")) c->split_dominance = std::atoi(v) ? 0u : 8u;
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
@@ -1158,9 +1176,11 @@ int dev_queue_stats(Dev* c, uint32_t out[16])
 {
     if (!c || !out) return PT_ERR_ARG;
     std::memset(out, 0, 16 * sizeof(uint32_t));
-    if (!c->wf_mem) return PT_OK;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->lpt_mem && c->lpt_valid)   // the tiles the next megakernel draw of the same grid splits
+        HIPCHK(c, hipMemcpy(&out[7], c->lpt_mem + 5 * c->lpt_cap, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (!c->wf_mem) return PT_OK;
     std::vector<unsigned> h(16 * pt::kShards);
     HIPCHK(c, hipMemcpy(h.data(), c->wf.cnt, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));
     for (int b = 0; b < 7; b++)

@@ -199,18 +199,43 @@ PT_D int costBucket(unsigned dur)
 // frame-to-frame noise of 64 random paths; measured 1-2 % better than the last frame alone) (one block): a tile weighs as its slowest quadrant wave; tiles are dealt
 // bucket by bucket, slowest bucket first; within a bucket the order is whatever the LDS atomics
 // give - any permutation renders the same bits, only the schedule changes.
-__global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const unsigned* cost, unsigned* order)
+__global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const unsigned* cost, unsigned* order,
+                                                        unsigned* split, unsigned split_cap, unsigned dominance)
 {
     __shared__ unsigned cnt[kCostBuckets];
+    __shared__ unsigned long long total;
+    __shared__ unsigned slowest;
     for (int b = threadIdx.x; b < kCostBuckets; b += blockDim.x) cnt[b] = 0;
+    if (threadIdx.x == 0) { total = 0; slowest = 0; }
     __syncthreads();
-    auto tileBucket = [&](unsigned t) {
+    auto tileCost = [&](unsigned t) {
         const unsigned* c = cost + 4u * t;
-        return costBucket(max(max(c[0], c[1]), max(c[2], c[3])));
+        return max(max(c[0], c[1]), max(c[2], c[3]));
     };
-    for (unsigned t = threadIdx.x; t < ntiles; t += blockDim.x) atomicAdd(&cnt[tileBucket(t)], 1u);
+    auto tileBucket = [&](unsigned t) { return costBucket(tileCost(t)); };
+    unsigned long long part = 0;
+    unsigned mx = 0;
+    for (unsigned t = threadIdx.x; t < ntiles; t += blockDim.x) {
+        atomicAdd(&cnt[tileBucket(t)], 1u);
+        const unsigned* c = cost + 4u * t;
+        part += (unsigned long long)c[0] + c[1] + c[2] + c[3];
+        mx = max(mx, tileCost(t));
+    }
+    atomicAdd(&total, part);
+    atomicMax(&slowest, mx);
     __syncthreads();
     if (threadIdx.x == 0) {
+        // tiles to split (pt_trace): when the slowest wave costs at least `dominance` (8) x the mean (a few tiles
+        // bound the launch, as the helmet's do: ~10x; the dragon stand-in and the bunny, bound by
+        // throughput, stay near 4x), those within 3 buckets (~0.77x) of the slowest, if at most
+        // split_cap of them
+        int top = kCostBuckets - 1;
+        while (top > 0 && cnt[top] == 0) top--;
+        unsigned near = 0;
+        for (int b = top; b >= 0 && b > top - 3; b--) near += cnt[b];
+        const unsigned k = (near + 7u) & ~7u;   // split_cap: a multiple of 8, <= ntiles
+        const bool dominated = (unsigned long long)slowest * 4ull * ntiles >= dominance * total && total > 0;
+        *split = (dominated && k <= split_cap) ? k : 0u;
         unsigned acc = 0;
         for (int b = kCostBuckets - 1; b >= 0; b--) { const unsigned v = cnt[b]; cnt[b] = acc; acc += v; }
     }
@@ -247,7 +272,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     const unsigned long long w0_ = wall_clock64();
 #endif
     // the 8x8 wave tile of this wave inside its 16x16 tile (grid = tiles_x * kTraceSub x bands)
-    int wave, tx;
+    int wave, tx, part = -1;
     unsigned bY, costIdx = ~0u;
     if (kTraceSub == 4 && PT_TILE_GROUPS) {
         // launch slots in runs of 32 workgroups = 8 tiles x 4 quadrants, quadrant-major: the
@@ -255,14 +280,31 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         // (one L2), while the runs' tiles still go round-robin over the XCDs (a short last run keeps
         // the map a bijection). The tiles come in longest-first order (the previous frame's costs,
         // pt_order_build) when a.order is set, else row-major.
-        const unsigned tiles_x = gridDim.x / 4u, ntiles = tiles_x * gridDim.y;
+        // Split tiles: the K = *a.split slowest tiles come first, each as 16 waves of 16 lanes
+        // (runs of 128 workgroups = 8 tiles x 16 parts, again 8 apart per tile). A wave ends with
+        // its slowest lane of each bounce; a 4x4 block waits on fewer of them than an 8x8 one, so
+        // the kernel's critical path (the slowest tiles' waves, which start first and end last when
+        // a few tiles dominate, as the helmet's do) shortens. Which lane shades which pixel never
+        // changes what a pixel computes: same bits.
+        const unsigned tiles_x = gridDim.x / 4u, ntiles = a.ntiles;
+        const unsigned K = (a.order && a.split) ? *a.split : 0u;   // chosen by pt_order_build
         const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
-        const unsigned g = L >> 5, r = L & 31u;
-        const unsigned T = min(8u, ntiles - g * 8u);
-        const unsigned slot = g * 8u + r % T;
+        unsigned slot;
+        if (L < 16u * K) {
+            const unsigned g = L >> 7, r = L & 127u;
+            slot = g * 8u + (r & 7u);
+            wave = (int)(r >> 5);
+            part = (int)((r >> 3) & 3u);
+        } else {
+            const unsigned L2 = L - 16u * K;
+            if (L2 >= 4u * (ntiles - K)) return;   // the grid's padding
+            const unsigned g = L2 >> 5, r = L2 & 31u;
+            const unsigned T = min(8u, ntiles - K - g * 8u);
+            slot = K + g * 8u + r % T;
+            wave = (int)(r / T);
+        }
         const unsigned tile = a.order ? a.order[slot] : slot;
         if (slot < a.prio_tiles) __builtin_amdgcn_s_setprio(3);   // the critical path: issue first
-        wave = (int)(r / T);
         tx = (int)(tile % tiles_x);
         bY = tile / tiles_x;
         costIdx = tile * 4u + (unsigned)wave;
@@ -275,8 +317,9 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         tx = (int)(blockIdx.x >> 2);
         bY = blockIdx.y;
     }
-    const int lx = (lane & 1) | ((lane >> 1) & 6);
-    const int ly = ((lane >> 1) & 1) | ((lane >> 3) & 6);
+    // lane bits (x0, y0, x1, x2, y1, y2) of an 8x8 block, or (x0, y0, x1, y1) of a split tile's 4x4
+    const int lx = part < 0 ? (lane & 1) | ((lane >> 1) & 6) : (part & 1) * 4 + ((lane & 1) | ((lane >> 1) & 2));
+    const int ly = part < 0 ? ((lane >> 1) & 1) | ((lane >> 3) & 6) : (part >> 1) * 4 + (((lane >> 1) & 1) | ((lane >> 2) & 2));
     const int band = (int)bY * a.num_parts + a.part;            // global 16-row band of this block
     const int px = tx * kTile + (wave & 1) * 8 + lx;
     const int py = band * kTile + (wave >> 1) * 8 + ly;
@@ -286,7 +329,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
 
     // lanes whose whole 2x2 quad lies beyond the (even-rounded) target do no work; quad helpers
     // that only complete a quad at an odd edge are shaded like GL helper invocations
-    const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1);
+    const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1) && (part < 0 || lane < 16);
     Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
 #ifdef PT_SECPROF
     __shared__ unsigned long long lds_sec[16];
@@ -356,10 +399,11 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         atomicAdd(&C[C_HDR], (unsigned long long)cnt.hdr);
     }
     if (a.cost && costIdx != ~0u && tid == 0) {   // this wave's duration, averaged with the tile's
-        const unsigned long long dur = min(clock64() - t_start, 0xffffffffull);   // history, for the next order
+        // history, for the next order (a split tile's four parts share their quadrant's entry)
+        const unsigned long long dur = min(clock64() - t_start, 0xffffffffull);
         a.cost[costIdx] = (unsigned)((dur + (unsigned long long)a.cost[costIdx]) >> 1);
     }
-    if (px >= a.width || py >= a.height) return;   // quad helper outside the target
+    if (!active || px >= a.width || py >= a.height) return;   // quad helper outside the target, idle lane
 
     // ---- progressive accumulation (js/PathTracingCommon.js:1326-1357)
     const long long pi = (long long)py * a.width + px;
@@ -750,9 +794,10 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
     return hipGetLastError();
 }
 
-hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, hipStream_t s)
+hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,
+                                 unsigned split_cap, unsigned dominance, hipStream_t s)
 {
-    hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(1024), 0, s, ntiles, cost, order);
+    hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(1024), 0, s, ntiles, cost, order, split, split_cap, dominance);
     return hipGetLastError();
 }
 

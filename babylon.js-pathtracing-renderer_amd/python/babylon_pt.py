@@ -208,10 +208,11 @@ class Engine:
         return {k: int(v) for k, v in zip(keys, buf)}
 
     def queue_stats(self):
-        """Wavefront queue sizes of the last draw: paths per bounce and BVH rays per bounce."""
+        """Wavefront queue sizes of the last draw (paths per bounce, BVH rays per bounce) and the
+        tiles the next megakernel draw of the same grid splits into 16-lane waves."""
         buf = (ctypes.c_uint32 * 16)()
         self.check(lib().pt_queue_stats(self.ctx, buf), "pt_queue_stats")
-        return {"paths": list(buf[0:7]), "bvh": list(buf[8:14])}
+        return {"paths": list(buf[0:7]), "bvh": list(buf[8:14]), "split_tiles": int(buf[7])}
 
     def math_probe(self, op, x, y=None):
         x = np.ascontiguousarray(x, dtype=np.float32)

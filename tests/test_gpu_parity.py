@@ -644,3 +644,39 @@ def test_helmet_real_maps_1080p_bitexact(engine):
     for i in range(3):
         assert _bits_equal(ref_acc[i], got_acc[i]), "frame %d: %s" % (i, _diff_report(ref_acc[i], got_acc[i]))
         assert _bits_equal(ref_can[i], got_can[i]), "frame %d canvas: %s" % (i, _diff_report(ref_can[i], got_can[i]))
+
+
+@pytest.mark.parametrize("name", ["gltf_helmet_320x180", "hdri_helmet_320x180", "gltf_teapot_320x180"])
+def test_split_tiles_bitexact(name, monkeypatch):
+    """Tile splitting (the slowest tiles of the longest-first order shaded by 16 waves of 16 lanes,
+    pt_trace / pt_order_build) forced on every frame after the first: the recorded stream's
+    accumulation and canvas stay bit-exact with the oracle, and the draws did split tiles."""
+    import babylon_pt as bp
+    monkeypatch.setenv("PT_SPLIT_ALWAYS", "1")
+    monkeypatch.setenv("PT_SPLIT_TILES", "64")
+    e = bp.Engine(0)
+    try:
+        meta = H.stream(name)
+        maps = _maps("seeded") if "helmet" in name else None
+        m = H.texture_payloads(meta, H.mesh(meta))
+        player = bp.StreamPlayer(e, meta, H.bluenoise(), m)
+        if maps:
+            for kind, sampler in H.PBR_SAMPLERS.items():
+                player.textures[sampler] = bp.Texture(e, maps[kind], name=kind)
+        w, h = player.width, player.height
+        e.resize_canvas(w, h)
+        n = len(meta["frames"])
+        got_acc, got_can, split = [], [], []
+        for i in range(n):
+            player.play_frame(i)
+            e.sync()
+            got_acc.append(player.textures["pathTracingRenderTarget"].read())
+            got_can.append(e.read_canvas(w, h))
+            split.append(e.queue_stats()["split_tiles"])
+        ref_acc, ref_can, _ = H.oracle_replay(meta, n, with_output=True, maps=maps)
+        for i in range(n):
+            assert _bits_equal(ref_acc[i], got_acc[i]), "frame %d: %s" % (i, _diff_report(ref_acc[i], got_acc[i]))
+            assert _bits_equal(ref_can[i], got_can[i]), "frame %d canvas: %s" % (i, _diff_report(ref_can[i], got_can[i]))
+        assert max(split) >= 8, split
+    finally:
+        e.dispose()
