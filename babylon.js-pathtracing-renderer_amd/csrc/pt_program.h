@@ -194,7 +194,13 @@ PT_D void analyticNearest(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, f3& sn)
     }
 #pragma unroll 1
     for (int i = 0; i < a.nquads; i++) {
-        float d = gmin(quadTriangle(a.qtri[2 * i], rayO, rayD), quadTriangle(a.qtri[2 * i + 1], rayO, rayD));
+        // the quad's 18 floats loaded (scalar) before the tests, one wait instead of one per use
+        // (bunny -1 %, dragon stand-in -0.3 %)
+        const TriArg A = a.qtri[2 * i], B = a.qtri[2 * i + 1];
+        asm volatile("" ::"s"(A.v0.x), "s"(A.v0.y), "s"(A.v0.z), "s"(A.e1.x), "s"(A.e1.y), "s"(A.e1.z), "s"(A.e2.x),
+                     "s"(A.e2.y), "s"(A.e2.z), "s"(B.v0.x), "s"(B.v0.y), "s"(B.v0.z), "s"(B.e1.x), "s"(B.e1.y),
+                     "s"(B.e1.z), "s"(B.e2.x), "s"(B.e2.y), "s"(B.e2.z));
+        float d = gmin(quadTriangle(A, rayO, rayD), quadTriangle(B, rayO, rayD));
         if (d < h.t) { h.t = d; h.id = q0 + i; }
     }
 }
