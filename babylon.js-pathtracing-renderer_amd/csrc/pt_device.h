@@ -70,10 +70,15 @@ template <int P> constexpr int kStackLdsOf = (kPairs<P> && !kHasTex<P>) ? PT_STA
 // ------------------------------------------------------------------------------ per-lane state
 struct Path {
     uint32_t s0, s1;       // uvec2 seed (js/PathTracingCommon.js:500)
-    float counter;         // blueNoise_rand() counter
-    float bn0, bn1;        // randVec4.r / .g (channel = mod(counter, 2) only reaches r, g)
+    // blueNoise_rand()'s state in one register: bits 0-7 / 8-15 = the blue-noise texel's r / g bytes
+    // (randVec4.r / .g: channel = mod(counter, 2) only reaches those two), bits 16-31 = counter + 1
+    // (the GLSL's float counter starts at -1.0 and only ever steps by 1.0)
+    uint32_t bn;
     f3 ro, rd;             // rayOrigin, rayDirection
 };
+PT_D float unorm8(unsigned b);
+PT_D float pathCounter(const Path& p) { return (float)(p.bn >> 16) - 1.0f; }
+PT_D void setPathCounter(Path& p, float c) { p.bn = (p.bn & 0xffffu) | ((unsigned)(c + 1.0f) << 16); }
 
 PT_D float rng(Path& p)
 {
@@ -85,9 +90,9 @@ PT_D float rng(Path& p)
 }
 PT_D float blueNoise_rand(Path& p)
 {
-    p.counter = p.counter + 1.0f;
-    int channel = (int)gmod(p.counter, 2.0f);
-    return gfract(channel == 0 ? p.bn0 : p.bn1);
+    p.bn += 1u << 16;   // counter = counter + 1.0; channel = int(mod(counter, 2.0)) of a counter >= 0
+    const unsigned channel = ((p.bn >> 16) - 1u) & 1u;
+    return gfract(unorm8((p.bn >> (8u * channel)) & 255u));
 }
 PT_D float tentFilter(float x) { return (x < 0.5f) ? gsqrt(2.0f * x) - 1.0f : 1.0f - gsqrt(2.0f - (2.0f * x)); }
 PT_D f3 onb_u(f3 nl)

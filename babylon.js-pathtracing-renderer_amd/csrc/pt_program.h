@@ -393,13 +393,12 @@ PT_D void cameraRay(const TraceArgs& a, int px, int py, Path& p)
     float fcx = (float)px + 0.5f, fcy = (float)py + 0.5f;
     p.s0 = (uint32_t)a.frame * (uint32_t)fcx;
     p.s1 = (uint32_t)(a.frame + 1.0f) * (uint32_t)fcy;
-    p.counter = -1.0f;
     int bx = (int)gmod(fcx + floorf(a.rnd[0] * 256.0f), 256.0f);
     int by = (int)gmod(fcy + floorf(a.rnd[1] * 256.0f), 256.0f);
-    p.bn0 = 0.0f; p.bn1 = 0.0f;
+    p.bn = 0u;   // counter = -1.0; randVec4 = 0 outside the texture (pinned)
     if (bx < a.bluenoise.w && by < a.bluenoise.h) {
         uchar4 b = a.bluenoise.p[by * a.bluenoise.w + bx];
-        p.bn0 = unorm8(b.x); p.bn1 = unorm8(b.y);
+        p.bn = (unsigned)b.x | ((unsigned)b.y << 8);
     }
     float ox = tentFilter(rng(p));
     float oy = tentFilter(rng(p));

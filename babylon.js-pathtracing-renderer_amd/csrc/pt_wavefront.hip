@@ -313,11 +313,10 @@ __global__ __launch_bounds__(kBlock) void wf_shade(TraceArgs a, WfBufs w, int b)
             Path p;
             p.ro = mk(A.x, A.y, A.z);
             p.rd = mk(B.x, B.y, B.z);
-            p.counter = B.w;
             p.s0 = f2u(D.x); p.s1 = f2u(D.y);
             const unsigned flags = f2u(D.z);
-            const unsigned bnb = f2u(D.w);
-            p.bn0 = unorm8(bnb & 255u); p.bn1 = unorm8((bnb >> 8) & 255u);
+            p.bn = f2u(D.w) & 0xffffu;
+            setPathCounter(p, B.w);
             PState s;
             s.mask = mk(C.x, C.y, C.z);
             s.roughness = C.w;
@@ -343,7 +342,7 @@ __global__ __launch_bounds__(kBlock) void wf_shade(TraceArgs a, WfBufs w, int b)
                                     (s.sampleLight ? F_SAMPLE_LIGHT : 0u) |
                                     ((unsigned)(s.hitType + (int)kTypeBias) << F_TYPE_SHIFT);
                 oA = make_float4(p.ro.x, p.ro.y, p.ro.z, A.w);
-                oB = make_float4(p.rd.x, p.rd.y, p.rd.z, p.counter);
+                oB = make_float4(p.rd.x, p.rd.y, p.rd.z, pathCounter(p));
                 oC = make_float4(s.mask.x, s.mask.y, s.mask.z, s.roughness);
                 oD = make_float4(u2f(p.s0), u2f(p.s1), u2f(nf), D.w);
             } else {
