@@ -11,6 +11,7 @@
 // samples, CMYK / Adobe-transform files are refused (PT_ERR_UNSUPPORTED). Host code only.
 #include <cstdint>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "../../include/pt.h"
@@ -115,6 +116,7 @@ struct Decoder {
             int code = 0, k = 0;
             for (int l = 1; l <= 16; l++) {
                 t.valoff[l] = k - code;
+                if (code + counts[l] > (1 << l)) return PT_ERR_DATA;   // more codes than the length allows
                 if (counts[l]) {
                     for (int i = 0; i < counts[l]; i++, k++, code++)
                         if (l <= 8)
@@ -139,6 +141,7 @@ struct Decoder {
         if (u8() != 8) return PT_ERR_UNSUPPORTED;
         H = u16(); W = u16(); ncomp = u8();
         if (H <= 0 || W <= 0 || (ncomp != 1 && ncomp != 3)) return PT_ERR_UNSUPPORTED;
+        if ((long long)W * H > (1ll << 28)) return PT_ERR_UNSUPPORTED;   // 16k x 16k at most
         for (int i = 0; i < ncomp; i++) {
             c[i].id = u8();
             const int hv = u8();
@@ -559,5 +562,9 @@ extern "C" int pt_jpeg_decode_rgba8(const uint8_t* data, size_t size, uint8_t* r
 {
     int w = 0, h = 0;
     if (!rgba) return PT_ERR_ARG;
-    return decodeJpeg(data, size, &w, &h, rgba, capacity, false);
+    try {
+        return decodeJpeg(data, size, &w, &h, rgba, capacity, false);
+    } catch (const std::bad_alloc&) {
+        return PT_ERR_OOM;
+    }
 }
