@@ -561,8 +561,10 @@ int render_trace(DevFx* fx, DevTex* target)
 #ifdef PT_SECPROF
     {   // experiment builds: the wave timeline of the last megakernel draw (pt_debug_wave_log)
         static size_t cap = 0;
-        const size_t need = (size_t)((target->w + pt::kTile - 1) / pt::kTile) * bands_owned(c, target->h) * 4 * pt::kWaveLogSlots;
+        const size_t tx = (size_t)((target->w + pt::kTile - 1) / pt::kTile);   // + split tiles' padding rows
+        const size_t need = (tx * bands_owned(c, target->h) * 4 + 12 * (size_t)c->split_tiles + 4 * tx) * pt::kWaveLogSlots;
         if (cap < need) { if (g_wave_log) hipFree(g_wave_log); hipMalloc(&g_wave_log, need * 8); cap = need; }
+        hipMemsetAsync(g_wave_log, 0, need * 8, c->stream);   // padding workgroups leave zero rows
         g_wave_log_n = need / pt::kWaveLogSlots;
         a.wave_log = g_wave_log;
     }
