@@ -221,8 +221,11 @@ __global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const un
         part += (unsigned long long)c[0] + c[1] + c[2] + c[3];
         mx = max(mx, tileCost(t));
     }
-    atomicAdd(&total, part);
-    atomicMax(&slowest, mx);
+    for (int o = 32; o > 0; o >>= 1) {   // one LDS atomic per wave, not per thread
+        part += __shfl_xor(part, o, 64);
+        mx = max(mx, (unsigned)__shfl_xor((int)mx, o, 64));
+    }
+    if ((threadIdx.x & 63u) == 0) { atomicAdd(&total, part); atomicMax(&slowest, mx); }
     __syncthreads();
     if (threadIdx.x == 0) {
         // tiles to split (pt_trace): when the slowest wave costs at least `dominance` (8) x the mean (a few tiles
