@@ -215,11 +215,39 @@ __global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const un
     auto tileBucket = [&](unsigned t) { return costBucket(tileCost(t)); };
     unsigned long long part = 0;
     unsigned mx = 0;
-    for (unsigned t = threadIdx.x; t < ntiles; t += blockDim.x) {
-        atomicAdd(&cnt[tileBucket(t)], 1u);
-        const unsigned* c = cost + 4u * t;
-        part += (unsigned long long)c[0] + c[1] + c[2] + c[3];
-        mx = max(mx, tileCost(t));
+    // up to kOrderHeld tiles per thread (32768: a 4K frame) go through registers: all their cost
+    // loads are issued before the first LDS atomic (a loop with the atomic inside waits one HBM
+    // round trip per iteration), and the scatter reuses the buckets instead of reloading
+    constexpr int kOrderHeld = 32, kOrderChunk = 8;
+    const bool held = ntiles <= kOrderHeld * blockDim.x;
+    unsigned bk[kOrderHeld];
+    if (held) {
+#pragma unroll
+        for (int c0 = 0; c0 < kOrderHeld; c0 += kOrderChunk) {
+            if (c0 * blockDim.x >= ntiles) break;
+            uint4 v[kOrderChunk];
+#pragma unroll
+            for (int j = 0; j < kOrderChunk; j++) {
+                const unsigned t = threadIdx.x + (c0 + j) * blockDim.x;
+                v[j] = t < ntiles ? *(const uint4*)(cost + 4u * t) : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (int j = 0; j < kOrderChunk; j++) {
+                const unsigned t = threadIdx.x + (c0 + j) * blockDim.x;
+                const unsigned m = max(max(v[j].x, v[j].y), max(v[j].z, v[j].w));
+                bk[c0 + j] = costBucket(m);
+                part += (unsigned long long)v[j].x + v[j].y + v[j].z + v[j].w;
+                mx = max(mx, m);
+                if (t < ntiles) atomicAdd(&cnt[bk[c0 + j]], 1u);
+            }
+        }
+    } else {
+        for (unsigned t = threadIdx.x; t < ntiles; t += blockDim.x) {
+            atomicAdd(&cnt[tileBucket(t)], 1u);
+            const unsigned* c = cost + 4u * t;
+            part += (unsigned long long)c[0] + c[1] + c[2] + c[3];
+            mx = max(mx, tileCost(t));
+        }
     }
     for (int o = 32; o > 0; o >>= 1) {   // one LDS atomic per wave, not per thread
         part += __shfl_xor(part, o, 64);
@@ -227,22 +255,47 @@ __global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const un
     }
     if ((threadIdx.x & 63u) == 0) { atomicAdd(&total, part); atomicMax(&slowest, mx); }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {
         // tiles to split (pt_trace): when the slowest wave costs at least `dominance` (8) x the mean (a few tiles
         // bound the launch, as the helmet's do: ~10x; the dragon stand-in and the bunny, bound by
         // throughput, stay near 4x), those within 3 buckets (~0.77x) of the slowest, if at most
-        // split_cap of them
-        int top = kCostBuckets - 1;
-        while (top > 0 && cnt[top] == 0) top--;
-        unsigned near = 0;
-        for (int b = top; b >= 0 && b > top - 3; b--) near += cnt[b];
-        const unsigned k = (near + 7u) & ~7u;   // split_cap: a multiple of 8, <= ntiles
-        const bool dominated = (unsigned long long)slowest * 4ull * ntiles >= dominance * total && total > 0;
-        *split = (dominated && k <= split_cap) ? k : 0u;
-        unsigned acc = 0;
-        for (int b = kCostBuckets - 1; b >= 0; b--) { const unsigned v = cnt[b]; cnt[b] = acc; acc += v; }
+        // split_cap of them. Wave 0 does it, two buckets a lane (a serial loop over LDS is ~6 us).
+        static_assert(kCostBuckets == 128, "two buckets per lane of one wave");
+        const int l = threadIdx.x;
+        const unsigned c0 = cnt[2 * l], c1 = cnt[2 * l + 1];
+        const unsigned long long nz = __ballot((c0 | c1) != 0u);
+        int top = 0;
+        if (nz) {
+            const int tl = 63 - __builtin_clzll(nz);
+            top = 2 * tl + ((unsigned)__shfl((int)c1, tl, 64) != 0u ? 1 : 0);
+        }
+        unsigned near = (2 * l <= top && 2 * l > top - 3 ? c0 : 0u) + (2 * l + 1 <= top && 2 * l + 1 > top - 3 ? c1 : 0u);
+        unsigned suf = c0 + c1;   // inclusive suffix sum over lanes l..63 (descending bucket order)
+        for (int o = 1; o < 64; o <<= 1) {
+            near += (unsigned)__shfl_xor((int)near, o, 64);
+            const unsigned t = (unsigned)__shfl_down((int)suf, o, 64);
+            if (l + o < 64) suf += t;
+        }
+        if (l == 0) {
+            const unsigned k = (near + 7u) & ~7u;   // split_cap: a multiple of 8, <= ntiles
+            const bool dominated = (unsigned long long)slowest * 4ull * ntiles >= dominance * total && total > 0;
+            *split = (dominated && k <= split_cap) ? k : 0u;
+        }
+        const unsigned excl = suf - c0 - c1;   // tiles in buckets above 2l + 1
+        cnt[2 * l + 1] = excl;
+        cnt[2 * l] = excl + c1;
     }
     __syncthreads();
+    if (held) {
+#pragma unroll
+        for (int j = 0; j < kOrderHeld; j++) {
+            const unsigned t = threadIdx.x + j * blockDim.x;
+            if (t >= ntiles) break;
+            const unsigned pos = atomicAdd(&cnt[bk[j]], 1u);
+            if (pos < ntiles) order[pos] = t;
+        }
+        return;
+    }
     for (unsigned t = threadIdx.x; t < ntiles; t += blockDim.x) {
         const unsigned pos = atomicAdd(&cnt[tileBucket(t)], 1u);
         if (pos < ntiles) order[pos] = t;
