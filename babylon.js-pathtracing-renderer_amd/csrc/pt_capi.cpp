@@ -31,7 +31,7 @@ extern "C" {
 hipError_t pt_launch_exhaustive(int op, unsigned long long* bad, hipStream_t s);
 hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,
-                                 unsigned split_cap, unsigned dominance, hipStream_t s);
+                                 unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s);
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
@@ -127,6 +127,7 @@ struct Dev {
     unsigned prio_tiles = 0;   // longest-first: the first prio_tiles 16x16 tiles run at raised wave priority
     unsigned split_tiles = 32; // longest-first: at most this many of the slowest tiles shaded by 16-lane waves
                                // (pt_trace, pt_order_build; PT_SPLIT_TILES)
+    int split_near = 3;             // ... those within this many cost buckets of the slowest (1/8 octave each; PT_SPLIT_NEAR)
     unsigned split_dominance = 8;   // ... when the slowest wave costs this many times the mean (PT_SPLIT_ALWAYS=1: 0)
     unsigned* lpt_mem = nullptr;            // cost[4 * ntiles] | order[ntiles]
     size_t lpt_n = 0, lpt_cap = 0;
@@ -640,7 +641,7 @@ int render_trace(DevFx* fx, DevTex* target)
             if (a.cost) {
                 HIPCHK(c, pt_launch_order_build((unsigned)n, a.cost, c->lpt_mem + 4 * c->lpt_cap,
                                                 c->lpt_mem + 5 * c->lpt_cap, (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u,
-                                                c->split_dominance, c->stream));
+                                                c->split_dominance, c->split_near, c->stream));
                 c->lpt_valid = true; c->lpt_n = n; c->lpt_key_target = target; c->lpt_key_prog = fx->prog;
                 c->lpt_key_part = c->part; c->lpt_key_parts = c->num_parts;
             }
@@ -793,6 +794,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_LPT")) c->lpt = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_PRIO_TILES")) c->prio_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("PT_SPLIT_NEAR")) c->split_near = std::max(1, std::min(128, std::atoi(v)));
     if (const char* v = std::getenv("PT_SPLIT_ALWAYS")) c->split_dominance = std::atoi(v) ? 0u : 8u;
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     hipError_t e = hipSetDevice(device);

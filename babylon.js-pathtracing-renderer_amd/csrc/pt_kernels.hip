@@ -200,7 +200,8 @@ PT_D int costBucket(unsigned dur)
 // bucket by bucket, slowest bucket first; within a bucket the order is whatever the LDS atomics
 // give - any permutation renders the same bits, only the schedule changes.
 __global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const unsigned* cost, unsigned* order,
-                                                        unsigned* split, unsigned split_cap, unsigned dominance)
+                                                        unsigned* split, unsigned split_cap, unsigned dominance,
+                                                        int near_buckets)
 {
     __shared__ unsigned cnt[kCostBuckets];
     __shared__ unsigned long long total;
@@ -258,8 +259,7 @@ __global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const un
     if (threadIdx.x < 64) {
         // tiles to split (pt_trace): when the slowest wave costs at least `dominance` (8) x the mean (a few tiles
         // bound the launch, as the helmet's do: ~10x; the dragon stand-in and the bunny, bound by
-        // throughput, stay near 4x), those within 3 buckets (~0.77x) of the slowest, if at most
-        // split_cap of them. Wave 0 does it, two buckets a lane (a serial loop over LDS is ~6 us).
+        // throughput, stay near 4x), those within near_buckets (3: ~0.77x) of the slowest, at most split_cap of them. Wave 0 does it, two buckets a lane (a serial loop over LDS is ~6 us).
         static_assert(kCostBuckets == 128, "two buckets per lane of one wave");
         const int l = threadIdx.x;
         const unsigned c0 = cnt[2 * l], c1 = cnt[2 * l + 1];
@@ -269,7 +269,8 @@ __global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const un
             const int tl = 63 - __builtin_clzll(nz);
             top = 2 * tl + ((unsigned)__shfl((int)c1, tl, 64) != 0u ? 1 : 0);
         }
-        unsigned near = (2 * l <= top && 2 * l > top - 3 ? c0 : 0u) + (2 * l + 1 <= top && 2 * l + 1 > top - 3 ? c1 : 0u);
+        unsigned near = (2 * l <= top && 2 * l > top - near_buckets ? c0 : 0u) +
+                        (2 * l + 1 <= top && 2 * l + 1 > top - near_buckets ? c1 : 0u);
         unsigned suf = c0 + c1;   // inclusive suffix sum over lanes l..63 (descending bucket order)
         for (int o = 1; o < 64; o <<= 1) {
             near += (unsigned)__shfl_xor((int)near, o, 64);
@@ -279,7 +280,7 @@ __global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const un
         if (l == 0) {
             const unsigned k = (near + 7u) & ~7u;   // split_cap: a multiple of 8, <= ntiles
             const bool dominated = (unsigned long long)slowest * 4ull * ntiles >= dominance * total && total > 0;
-            *split = (dominated && k <= split_cap) ? k : 0u;
+            *split = dominated ? min(k, split_cap) : 0u;
         }
         const unsigned excl = suf - c0 - c1;   // tiles in buckets above 2l + 1
         cnt[2 * l + 1] = excl;
@@ -888,9 +889,10 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
 }
 
 hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,
-                                 unsigned split_cap, unsigned dominance, hipStream_t s)
+                                 unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s)
 {
-    hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(1024), 0, s, ntiles, cost, order, split, split_cap, dominance);
+    hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(1024), 0, s, ntiles, cost, order, split, split_cap, dominance,
+                       near_buckets);
     return hipGetLastError();
 }
 

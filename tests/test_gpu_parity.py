@@ -680,3 +680,35 @@ def test_split_tiles_bitexact(name, monkeypatch):
         assert max(split) >= 8, split
     finally:
         e.dispose()
+
+
+@pytest.mark.gpu
+def test_order_build_beyond_register_tiles_is_a_permutation(monkeypatch):
+    """pt_order_build holds up to 32 tiles per thread (32768 16x16 tiles) in registers and loops
+    over memory beyond that. A 3840x2400 frame has 36000 tiles: four frames of the bunny workload
+    with longest-first order and forced tile splitting accumulate the same bits as without the
+    order (a duplicated or missing tile in the permutation would show)."""
+    import babylon_pt as bp
+    meta, mesh_arrays, _, _ = H.workload("bunny")
+    W, Hh = 3840, 2400
+    assert (W // 16) * (Hh // 16) > 32768
+    out = {}
+    for lpt in ("1", "0"):
+        monkeypatch.setenv("PT_LPT", lpt)
+        monkeypatch.setenv("PT_SPLIT_ALWAYS", lpt)
+        e = bp.Engine(0)
+        try:
+            p = bp.StreamPlayer(e, meta, H.bluenoise(), H.texture_payloads(meta, mesh_arrays), W, Hh)
+            e.resize_canvas(p.width, p.height)
+            split = []
+            for k in range(4):
+                for call in p.synth_frame(k):
+                    p.play_call(call)
+                e.sync()
+                split.append(e.queue_stats()["split_tiles"])
+            out[lpt] = (p.textures["pathTracingRenderTarget"].read(), e.read_canvas(W, Hh), split)
+        finally:
+            e.dispose()
+    assert _bits_equal(out["1"][0], out["0"][0]), _diff_report(out["0"][0], out["1"][0])
+    assert _bits_equal(out["1"][1], out["0"][1])
+    assert max(out["1"][2]) >= 8, out["1"][2]
