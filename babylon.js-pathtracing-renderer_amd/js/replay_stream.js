@@ -6,7 +6,8 @@
 // usage: node replay_stream.js <stream.json> <payload_dir> <out_prefix> [frames]
 //   (PT_DEVICES="0,0" etc. renders through a multi-part context: the frame split over the parts)
 //   payload_dir holds bluenoise.u8 (256x256 RGBA8) and, for glTF streams, bvh.f32 / tri.f32
-//   (2048x2048 RGBA32F, the RawTexture payloads), and optionally maps.json (model PBR maps, below).
+//   (2048x2048 RGBA32F, the RawTexture payloads), hdr.f32 for HDRI streams (the environment), and
+//   optionally maps.json (model PBR maps, below).
 'use strict';
 const fs = require('fs');
 const path = require('path');
@@ -29,7 +30,12 @@ const tex = {
   'file:BlueNoise_RGBA256.png': BABYLON.RawTexture.CreateRGBATexture(new Uint8Array(fs.readFileSync(path.join(payloadDir, 'bluenoise.u8'))), 256, 256, engine, false, false, 1, 0),
 };
 if (meta.textures) {
-  for (const [raw, kind] of Object.entries(meta.textures)) tex[raw] = BABYLON.RawTexture.CreateRGBATexture(f32(kind + '.f32'), 2048, 2048, engine, false, false, 1, 1);
+  for (const [raw, kind] of Object.entries(meta.textures)) {
+    // the HDRI scene's environment: its own size, invertY and trilinear sampling, as the script uploads it
+    tex[raw] = kind === 'hdr'
+      ? BABYLON.RawTexture.CreateRGBATexture(f32('hdr.f32'), meta.hdr.width, meta.hdr.height, engine, false, meta.hdr.invertY, 3, 1)
+      : BABYLON.RawTexture.CreateRGBATexture(f32(kind + '.f32'), 2048, 2048, engine, false, false, 1, 1);
+  }
 }
 // maps.json (optional): { texture name: image file } - model maps as Babylon's glTF loader leaves
 // them (a texture holding the image file's bytes, invertY false); the shim decodes and uploads them
