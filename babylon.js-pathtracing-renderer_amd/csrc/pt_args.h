@@ -178,6 +178,13 @@ struct OutputArgs {
     uchar4* canvas;         // RGBA8 target (NULL when writing float)
     float4* out_f;          // RGBA32F target (NULL when writing the canvas)
     float4* copy_dst;       // a deferred screenCopy of `acc` fused into this pass (NULL: none)
+    // the longest-first order build of the last megakernel draw (pt_order_build) fused into this
+    // pass as one extra block that runs beside the output tiles (NULL ob_cost: none)
+    const unsigned* ob_cost;
+    unsigned* ob_order;
+    unsigned* ob_split;
+    unsigned ob_ntiles, ob_cap, ob_dominance;
+    int ob_near;
 };
 
 struct CopyArgs {

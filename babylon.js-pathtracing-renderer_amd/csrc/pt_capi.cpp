@@ -129,6 +129,12 @@ struct Dev {
                                // (pt_trace, pt_order_build; PT_SPLIT_TILES)
     int split_near = 3;             // ... those within this many cost buckets of the slowest (1/8 octave each; PT_SPLIT_NEAR)
     unsigned split_dominance = 8;   // ... when the slowest wave costs this many times the mean (PT_SPLIT_ALWAYS=1: 0)
+    // the order build of the last megakernel draw, deferred to run as an extra block of the next
+    // screenOutput pass (pt_output) instead of a kernel of its own; any other draw, stream switch or
+    // query launches it alone first (flush_order). PT_FUSE_ORDER=0: always alone, after the draw.
+    struct { bool on; unsigned n; const unsigned* cost; unsigned* order; unsigned* split; unsigned cap, dominance; int near; }
+        pending_order = {};
+    bool fuse_order = true;
     unsigned* lpt_mem = nullptr;            // cost[4 * ntiles] | order[ntiles]
     size_t lpt_n = 0, lpt_cap = 0;
     bool lpt_valid = false;
@@ -499,9 +505,20 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
     return t->pairs_ok;
 }
 
+// launch a deferred order build now, as its own kernel
+int flush_order(Dev* c)
+{
+    if (!c->pending_order.on) return PT_OK;
+    c->pending_order.on = false;
+    const auto& po = c->pending_order;
+    HIPCHK(c, pt_launch_order_build(po.n, po.cost, po.order, po.split, po.cap, po.dominance, po.near, c->stream));
+    return PT_OK;
+}
+
 int render_trace(DevFx* fx, DevTex* target)
 {
     Dev* c = fx->ctx;
+    if (int rc = flush_order(c)) return rc;   // this draw's order (before lpt_mem could be reallocated)
     if (!target || target->kind != TEX_RT) return fail(c, PT_ERR_ARG, "path tracing draws need a render target");
     DevTex* prev = sampler(fx, "previousBuffer");
     DevTex* bn = sampler(fx, "blueNoiseTexture");
@@ -639,9 +656,9 @@ int render_trace(DevFx* fx, DevTex* target)
             a.ntiles = (unsigned)n;
             HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, c->stream));
             if (a.cost) {
-                HIPCHK(c, pt_launch_order_build((unsigned)n, a.cost, c->lpt_mem + 4 * c->lpt_cap,
-                                                c->lpt_mem + 5 * c->lpt_cap, (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u,
-                                                c->split_dominance, c->split_near, c->stream));
+                c->pending_order = { true, (unsigned)n, a.cost, c->lpt_mem + 4 * c->lpt_cap, c->lpt_mem + 5 * c->lpt_cap,
+                                     (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance, c->split_near };
+                if (!c->fuse_order) { if (int rc = flush_order(c)) return rc; }
                 c->lpt_valid = true; c->lpt_n = n; c->lpt_key_target = target; c->lpt_key_prog = fx->prog;
                 c->lpt_key_part = c->part; c->lpt_key_parts = c->num_parts;
             }
@@ -720,7 +737,15 @@ int render_output(DevFx* fx, DevTex* target)
     }
     int rc = begin_draw(c, fx->prog);
     if (rc) return rc;
-    if (a.width > 0 && a.height > 0) HIPCHK(c, pt_launch_output(&a, c->stream));
+    if (a.width > 0 && a.height > 0) {
+        if (c->pending_order.on) {   // the last megakernel draw's order build rides along as one more block
+            const auto& po = c->pending_order;
+            a.ob_cost = po.cost; a.ob_order = po.order; a.ob_split = po.split;
+            a.ob_ntiles = po.n; a.ob_cap = po.cap; a.ob_dominance = po.dominance; a.ob_near = po.near;
+            c->pending_order.on = false;
+        }
+        HIPCHK(c, pt_launch_output(&a, c->stream));
+    }
     return end_draw(c, fx->prog);
 }
 
@@ -794,6 +819,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_LPT")) c->lpt = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_PRIO_TILES")) c->prio_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_SPLIT_NEAR")) c->split_near = std::max(1, std::min(128, std::atoi(v)));
     if (const char* v = std::getenv("PT_SPLIT_ALWAYS")) c->split_dominance = std::atoi(v) ? 0u : 8u;
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
@@ -817,6 +843,7 @@ void dev_ctx_destroy(Dev* c)
     if (!c) return;
     hipSetDevice(c->device);
     c->pending_copy.on = false;   // nothing can observe its target any more
+    c->pending_order.on = false;  // ... nor a next draw the order
     if (c->stream) hipStreamSynchronize(c->stream);
     std::vector<DevFx*> fx(c->effects.begin(), c->effects.end());
     for (auto* f : fx) dev_effect_destroy(f);
@@ -1083,6 +1110,7 @@ int dev_set_stream(Dev* c, void* stream)
     if (!c) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = flush_copy(c)) return rc;
+    if (int rc = flush_order(c)) return rc;        // on the stream its draw ran on
     HIPCHK(c, hipStreamSynchronize(c->stream));   // work already queued finishes first
     c->stream = stream ? (hipStream_t)stream : c->own_stream;
     return PT_OK;
@@ -1181,6 +1209,7 @@ int dev_queue_stats(Dev* c, uint32_t out[16])
     if (!c || !out) return PT_ERR_ARG;
     std::memset(out, 0, 16 * sizeof(uint32_t));
     HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = flush_order(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (c->lpt_mem && c->lpt_valid)   // the tiles the next megakernel draw of the same grid splits
         HIPCHK(c, hipMemcpy(&out[7], c->lpt_mem + 5 * c->lpt_cap, sizeof(uint32_t), hipMemcpyDeviceToHost));

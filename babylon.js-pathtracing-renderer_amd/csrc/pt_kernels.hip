@@ -199,9 +199,9 @@ PT_D int costBucket(unsigned dur)
 // frame-to-frame noise of 64 random paths; measured 1-2 % better than the last frame alone) (one block): a tile weighs as its slowest quadrant wave; tiles are dealt
 // bucket by bucket, slowest bucket first; within a bucket the order is whatever the LDS atomics
 // give - any permutation renders the same bits, only the schedule changes.
-__global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const unsigned* cost, unsigned* order,
-                                                        unsigned* split, unsigned split_cap, unsigned dominance,
-                                                        int near_buckets)
+// (one block of 1024 threads as its own kernel, or of 256 as the extra block of pt_output)
+PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split, unsigned split_cap,
+                     unsigned dominance, int near_buckets)
 {
     __shared__ unsigned cnt[kCostBuckets];
     __shared__ unsigned long long total;
@@ -301,6 +301,13 @@ __global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const un
         const unsigned pos = atomicAdd(&cnt[tileBucket(t)], 1u);
         if (pos < ntiles) order[pos] = t;
     }
+}
+
+__global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const unsigned* cost, unsigned* order,
+                                                        unsigned* split, unsigned split_cap, unsigned dominance,
+                                                        int near_buckets)
+{
+    orderBuild(ntiles, cost, order, split, split_cap, dominance, near_buckets);
 }
 
 // Workgroups of kTraceBlock lanes. At one wave per workgroup (64, the default) every 8x8 wave tile
@@ -680,7 +687,15 @@ __global__ __launch_bounds__(256) void pt_output(OutputArgs a, int tiles_x, int 
         f0 = accAt(a, x0 + tid % 20 - 2, y0 + tid / 20 - 2);
         if (tid + 256 < 400) f1 = accAt(a, x0 + (tid + 256) % 20 - 2, y0 + (tid + 256) / 20 - 2);
     };
-    int t = blockIdx.x, x0, y0;
+    int bid = (int)blockIdx.x, nblk = (int)gridDim.x;
+    if (a.ob_cost) {   // block 0: the next megakernel draw's order (pt_order_build), beside the tiles
+        if (bid == 0) {
+            orderBuild(a.ob_ntiles, a.ob_cost, a.ob_order, a.ob_split, a.ob_cap, a.ob_dominance, a.ob_near);
+            return;
+        }
+        bid--; nblk--;
+    }
+    int t = bid, x0, y0;
     if (t >= ntiles) return;
     origin(t, x0, y0);
     float4 f0, f1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -689,7 +704,7 @@ __global__ __launch_bounds__(256) void pt_output(OutputArgs a, int tiles_x, int 
     if (tid + 256 < 400) tile[0][tid + 256] = f1;
     __syncthreads();
     for (int cur = 0; t < ntiles; cur ^= 1) {
-        const int tn = t + (int)gridDim.x;
+        const int tn = t + nblk;
         int nx0 = 0, ny0 = 0;
         if (tn < ntiles) { origin(tn, nx0, ny0); load(nx0, ny0, f0, f1); }
         const int x = x0 + lx, y = y0 + ly;
@@ -946,9 +961,15 @@ hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s)
 {
     const int nb = (a->height + 15) / 16;
     dim3 grid((a->width + 15) / 16, a->part < nb ? (nb - a->part + a->num_parts - 1) / a->num_parts : 0);
-    if (grid.y == 0) return hipSuccess;
+    if (grid.y == 0) {   // no band of this part: a fused order build runs on its own
+        if (a->ob_cost)
+            hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(1024), 0, s, a->ob_ntiles, a->ob_cost, a->ob_order,
+                               a->ob_split, a->ob_cap, a->ob_dominance, a->ob_near);
+        return hipGetLastError();
+    }
     const int ntiles = (int)(grid.x * grid.y), blocks = 2048;
-    hipLaunchKernelGGL(pt::pt_output, dim3(ntiles < blocks ? ntiles : blocks), dim3(256), 0, s, *a, (int)grid.x, ntiles);
+    hipLaunchKernelGGL(pt::pt_output, dim3((ntiles < blocks ? ntiles : blocks) + (a->ob_cost ? 1 : 0)), dim3(256), 0, s, *a,
+                       (int)grid.x, ntiles);
     return hipGetLastError();
 }
 
