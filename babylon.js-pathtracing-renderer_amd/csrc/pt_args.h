@@ -169,6 +169,7 @@ struct WfBufs {
     int wq, hq;             // quad-rounded frame size
 };
 
+constexpr unsigned kOrderHeld = 128;   // pt_order_build: tiles per thread kept in registers (a byte each)
 struct OutputArgs {
     int width, height;      // output (canvas or render target) size
     int num_parts, part;    // with an output partition: only 16-row bands b % num_parts == part
@@ -180,6 +181,7 @@ struct OutputArgs {
     float4* copy_dst;       // a deferred screenCopy of `acc` fused into this pass (NULL: none)
     // the longest-first order build of the last megakernel draw (pt_order_build) fused into this
     // pass as one extra block that runs beside the output tiles (NULL ob_cost: none)
+    // (fused only while each of its 256 threads holds its tiles in registers: ntiles <= kOrderHeld * 256)
     const unsigned* ob_cost;
     unsigned* ob_order;
     unsigned* ob_split;

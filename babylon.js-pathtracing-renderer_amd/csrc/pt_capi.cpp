@@ -735,6 +735,10 @@ int render_output(DevFx* fx, DevTex* target)
         }
         a.width = c->cw; a.height = c->ch; a.canvas = c->canvas;
     }
+    // the order build rides along only up to 32768 tiles (4K): beyond, the block's 256 threads would
+    // loop over memory and outlast the pass, so it runs alone first (1024 threads)
+    if (c->pending_order.on && c->pending_order.n > pt::kOrderHeld * 256u)
+        if (int frc = flush_order(c)) return frc;
     int rc = begin_draw(c, fx->prog);
     if (rc) return rc;
     if (a.width > 0 && a.height > 0) {

@@ -216,16 +216,17 @@ PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, uns
     auto tileBucket = [&](unsigned t) { return costBucket(tileCost(t)); };
     unsigned long long part = 0;
     unsigned mx = 0;
-    // up to kOrderHeld tiles per thread (32768: a 4K frame) go through registers: all their cost
-    // loads are issued before the first LDS atomic (a loop with the atomic inside waits one HBM
-    // round trip per iteration), and the scatter reuses the buckets instead of reloading
-    constexpr int kOrderHeld = 32, kOrderChunk = 8;
+    // up to kOrderHeld tiles per thread (128: a 4K frame with 256 threads) go through registers,
+    // their buckets four to a register: all the cost loads of a chunk are issued before its LDS
+    // atomics (a loop with the atomic inside waits one HBM round trip per iteration), and the
+    // scatter reuses the buckets instead of reloading
+    constexpr int kOrderChunk = 8;
     const bool held = ntiles <= kOrderHeld * blockDim.x;
-    unsigned bk[kOrderHeld];
+    unsigned bk[(int)kOrderHeld / 4];
     if (held) {
 #pragma unroll
-        for (int c0 = 0; c0 < kOrderHeld; c0 += kOrderChunk) {
-            if (c0 * blockDim.x >= ntiles) break;
+        for (int c0 = 0; c0 < (int)kOrderHeld; c0 += kOrderChunk) {
+            if (c0 * blockDim.x >= ntiles) continue;   // (no break: the loop must unroll, bk[] stays in registers)
             uint4 v[kOrderChunk];
 #pragma unroll
             for (int j = 0; j < kOrderChunk; j++) {
@@ -236,10 +237,12 @@ PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, uns
             for (int j = 0; j < kOrderChunk; j++) {
                 const unsigned t = threadIdx.x + (c0 + j) * blockDim.x;
                 const unsigned m = max(max(v[j].x, v[j].y), max(v[j].z, v[j].w));
-                bk[c0 + j] = costBucket(m);
+                const unsigned b = (unsigned)costBucket(m);
+                const int k = c0 + j;
+                bk[k >> 2] = (k & 3) ? (bk[k >> 2] | (b << (8 * (k & 3)))) : b;
                 part += (unsigned long long)v[j].x + v[j].y + v[j].z + v[j].w;
                 mx = max(mx, m);
-                if (t < ntiles) atomicAdd(&cnt[bk[c0 + j]], 1u);
+                if (t < ntiles) atomicAdd(&cnt[b], 1u);
             }
         }
     } else {
@@ -289,11 +292,12 @@ PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, uns
     __syncthreads();
     if (held) {
 #pragma unroll
-        for (int j = 0; j < kOrderHeld; j++) {
+        for (int j = 0; j < (int)kOrderHeld; j++) {
             const unsigned t = threadIdx.x + j * blockDim.x;
-            if (t >= ntiles) break;
-            const unsigned pos = atomicAdd(&cnt[bk[j]], 1u);
-            if (pos < ntiles) order[pos] = t;
+            if (t < ntiles) {
+                const unsigned pos = atomicAdd(&cnt[(bk[j >> 2] >> (8 * (j & 3))) & 255u], 1u);
+                if (pos < ntiles) order[pos] = t;
+            }
         }
         return;
     }
