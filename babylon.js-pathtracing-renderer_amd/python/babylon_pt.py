@@ -657,6 +657,12 @@ class PipelinedBandGather:
         for b in sorted((b for b in range(2) if self.work[b] is not None), key=lambda b: self.frame_of[b]):
             self._finish(b)
 
+    def last_frame(self):
+        """Rank 0: the assembled canvas of the newest submitted frame (drains first)."""
+        self.drain()
+        done = [b for b in range(2) if self.frame_of[b] is not None]
+        return self.full[max(done, key=lambda b: self.frame_of[b])] if done and self.rank == 0 else None
+
 
 def halo_buffers(acc_padded, world):
     """Send/receive buffers for exchange_halos (same device and dtype as the accumulation)."""

@@ -216,6 +216,9 @@ def main():
     ap.add_argument("--workload", choices=("dragon", "bunny", "helmet", "sky_dragon"), default="dragon",
                     help="dragon (default): BASELINE.json's metric on the StanfordDragon stand-in; bunny: configs[1]; "
                          "helmet: configs[2] (real PBR maps); sky_dragon: configs[4] (physical sky + dragon, 4K)")
+    ap.add_argument("--dump-canvas", default=None, metavar="PATH",
+                    help="rank 0 saves the last timed frame's RGBA8 canvas (.npy) - e.g. to compare an N-rank "
+                         "frame with a one-rank render of the same size")
     ap.add_argument("--size", default=None,
                     help="WxH frame size (e.g. 3840x2160 for the 4K configs); at N > 1 the same frame is split over "
                          "the GPUs (strong scaling, BASELINE configs[3]: --gpus 8 --size 3840x2160)")
@@ -315,6 +318,12 @@ def main():
         step(k)
     barrier_sync()
     elapsed = time.perf_counter() - t0
+    if args.dump_canvas:
+        import numpy as np
+        if dist is None:
+            np.save(args.dump_canvas, engine.read_canvas(W, Hh))
+        elif rank == 0:
+            np.save(args.dump_canvas, gather.last_frame()[:Hh].cpu().numpy())
     pt_ms, pt_n = engine.timing_end(program)
     cp_ms, _ = engine.timing_end("screenCopy")
     out_ms, _ = engine.timing_end("screenOutput")

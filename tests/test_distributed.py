@@ -128,6 +128,10 @@ def _worker_pipeline(rank, world, port, w, h, frames, out_path):
         if rank == 0:
             np.save(out_path, np.stack([f[:h].numpy() for _, f in pipe.frames]))
             assert [i for i, _ in pipe.frames] == list(range(frames))
+            # bench.py --dump-canvas: the newest frame
+            assert torch.equal(pipe.last_frame(), pipe.frames[-1][1])
+        else:
+            assert pipe.last_frame() is None
         dist.barrier()
     finally:
         dist.destroy_process_group()
