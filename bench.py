@@ -216,6 +216,8 @@ def main():
     ap.add_argument("--workload", choices=("dragon", "bunny", "helmet", "sky_dragon"), default="dragon",
                     help="dragon (default): BASELINE.json's metric on the StanfordDragon stand-in; bunny: configs[1]; "
                          "helmet: configs[2] (real PBR maps); sky_dragon: configs[4] (physical sky + dragon, 4K)")
+    ap.add_argument("--event-every", type=int, default=10, metavar="K",
+                    help="time the kernels with HIP events around every K-th frame of the timed region")
     ap.add_argument("--dump-canvas", default=None, metavar="PATH",
                     help="rank 0 saves the last timed frame's RGBA8 canvas (.npy) - e.g. to compare an N-rank "
                          "frame with a one-rank render of the same size")
@@ -312,6 +314,10 @@ def main():
     for k in range(args.warmup):
         step(k)
     barrier_sync()
+    # kernel durations from HIP event pairs around every --event-every-th frame's draws (an event
+    # record costs ~5 us of stream time between kernels: bracketing every draw slowed the dragon
+    # stand-in's frame by 1.7 %, the bunny's by 3.8 %)
+    os.environ["PT_TIMING_EVERY"] = str(args.event_every)
     engine.timing_begin()
     t0 = time.perf_counter()
     for k in range(args.warmup, args.warmup + args.steps):
@@ -353,7 +359,7 @@ def main():
 
     paths = W * Hh * args.steps
     value = paths / elapsed / 1e6
-    avg_launch_ms = pt_ms / max(1, pt_n)
+    avg_launch_ms = max(pt_ms / max(1, pt_n), 1e-9)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
     wname = {"bunny": "bunny", "helmet": "helmet_pbr", "dragon": "dragon_standin", "sky_dragon": "dragon_standin"}
     workload = "%s_%s_%dx%d" % (program, wname[args.workload], W, Hh)
@@ -395,6 +401,7 @@ def main():
                               "of own bands, async RCCL gather of RGBA8 bands to rank 0 overlapping the next "
                               "frame") if world > 1 else None},
         "pathtrace_mpaths_per_s": round(W * Hh / (avg_launch_ms * 1e-3) / 1e6 * world, 2),
+        "kernel_timing": "HIP events around the draws of every %d-th timed frame (%d launches)" % (args.event_every, pt_n),
         "kernel_ms": {"pathtrace": round(avg_launch_ms, 4), "screen_copy": round(cp_ms / max(1, pt_n), 4),
                       "screen_output": round(out_ms / max(1, pt_n), 4)},
         "roofline": roofline,

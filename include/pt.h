@@ -177,12 +177,16 @@ int pt_set_stream(pt_ctx* ctx, void* hip_stream);
 /* Device pointer of a render target's RGBA32F storage (for RCCL collectives from the host). */
 void* pt_texture_device_ptr(pt_texture* tex);
 /* Device time of the last pt_render of each program kind, in ms (HIP events on the context
- * stream; requires pt_sync first). */
+ * stream; requires pt_sync first). Draws are bracketed by events only once this has been called
+ * (or with PT_DRAW_EVENTS=1): an event record costs ~5 us of stream time between kernels, so the
+ * first call turns them on and returns PT_ERR_ARG; the draws after it are reported. */
 int pt_last_render_ms(pt_ctx* ctx, int program, float* ms);
 /* Timing window: between pt_timing_begin and pt_timing_end every draw is bracketed by its own
  * HIP event pair (no host sync inside the window); pt_timing_end closes the window, synchronises
  * and returns the summed device time and launch count of one program kind (further pt_timing_end
- * calls report other kinds from the same window). */
+ * calls report other kinds from the same window). PT_TIMING_EVERY=k (read at pt_timing_begin)
+ * brackets only every k-th draw of each program kind, so the events barely disturb the timed
+ * stream; the launch count returned is then the bracketed draws'. */
 int pt_timing_begin(pt_ctx* ctx);
 int pt_timing_end(pt_ctx* ctx, int program, double* total_ms, int* launches);
 /* Algorithmic-byte counters: when enabled, path-tracing passes also accumulate
