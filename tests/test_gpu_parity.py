@@ -712,3 +712,37 @@ def test_order_build_beyond_register_tiles_is_a_permutation(monkeypatch):
     assert _bits_equal(out["1"][0], out["0"][0]), _diff_report(out["0"][0], out["1"][0])
     assert _bits_equal(out["1"][1], out["0"][1])
     assert max(out["1"][2]) >= 8, out["1"][2]
+
+
+def test_draw_events_opt_in_and_sampled_timing_window(engine, monkeypatch):
+    """Per-draw events cost stream time, so pt_last_render_ms turns them on at its first call (which
+    reports PT_ERR_ARG); the timing window brackets every PT_TIMING_EVERY-th draw of each kind."""
+    import babylon_pt as bp
+    meta = H.stream("gltf_teapot_320x180")
+    player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, H.mesh(meta)), 96, 64)
+    engine.resize_canvas(96, 64)
+
+    def play(k):
+        for call in player.synth_frame(k):
+            player.play_call(call)
+
+    play(0)
+    engine.sync()
+    with pytest.raises(bp.PtError):
+        engine.last_render_ms("gltf")       # no draw was bracketed yet: this call turns events on
+    play(1)
+    engine.sync()
+    assert engine.last_render_ms("gltf") > 0.0
+    monkeypatch.setenv("PT_TIMING_EVERY", "3")
+    engine.timing_begin()
+    for k in range(2, 9):                   # 7 frames: draws 0, 3, 6 of each kind are bracketed
+        play(k)
+    ms, n = engine.timing_end("gltf")
+    assert n == 3 and ms > 0.0
+    out_ms, out_n = engine.timing_end("screenOutput")
+    assert out_n == 3 and out_ms > 0.0
+    monkeypatch.setenv("PT_TIMING_EVERY", "1")
+    engine.timing_begin()
+    for k in range(9, 11):
+        play(k)
+    assert engine.timing_end("gltf")[1] == 2
