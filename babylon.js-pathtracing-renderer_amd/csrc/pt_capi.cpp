@@ -733,8 +733,12 @@ int render_output(DevFx* fx, DevTex* target)
     // frame size, same bands, and the copy target is not this pass's output
     const auto& pc = c->pending_copy;
     const int ow = target ? target->w : (c->cw || c->ch ? c->cw : acc->w), oh = target ? target->h : (c->cw || c->ch ? c->ch : acc->h);
+#ifdef PT_NO_FUSE_COPY   // experiment builds: the copy as its own kernel (what the fusion saves)
+    const bool fuse = false;
+#else
     const bool fuse = pc.on && pc.src == acc && pc.dst != target && ow == acc->w && oh == acc->h &&
                       pc.num_parts == a.num_parts && (pc.num_parts == 1 || pc.part == a.part);
+#endif
     if (fuse) { a.copy_dst = (float4*)pc.dst->d; c->pending_copy.on = false; }
     else { int frc = flush_copy(c); if (frc) return frc; }
     if (target) {

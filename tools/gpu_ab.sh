@@ -14,7 +14,7 @@ for round in $(seq $ROUNDS); do
     lib=""; [ "$d" != base ] && lib=$PWD/$d/libpt.so
     for w in $WLS; do
       PT_LIBPT=$lib timeout -k 10 200 python bench.py --workload $w --steps 100 --warmup 10 --cpu-budget 0 --no-pmc > gpurun_out/ab_tmp.json 2>>$OUT || exit $?
-      python3 -c "import json; d=json.loads(open('gpurun_out/ab_tmp.json').read().strip().splitlines()[-1]); print('$n $w r$round', d['value'], d['ms_per_step'], d['kernel_ms']['pathtrace'])" >> $OUT
+      python3 -c "import json; d=json.loads(open('gpurun_out/ab_tmp.json').read().strip().splitlines()[-1]); print('$n $w r$round', d['value'], d['ms_per_step'], d['kernel_ms']['pathtrace'], d['kernel_ms']['screen_output'], d['kernel_ms']['screen_copy'])" >> $OUT
     done
   done
 done
@@ -23,7 +23,7 @@ import sys, collections
 r = collections.defaultdict(list)
 for l in open(sys.argv[1]):
     p = l.split()
-    if len(p) == 6 and p[2].startswith('r'):
+    if len(p) >= 6 and p[2].startswith('r'):
         r[(p[0], p[1])].append(float(p[5]))
 print("summary (min kernel ms over rounds):")
 for (n, w), v in sorted(r.items(), key=lambda kv: (kv[0][1], kv[0][0])):
