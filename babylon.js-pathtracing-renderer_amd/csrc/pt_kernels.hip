@@ -971,7 +971,14 @@ hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s)
                                a->ob_split, a->ob_cap, a->ob_dominance, a->ob_near);
         return hipGetLastError();
     }
-    const int ntiles = (int)(grid.x * grid.y), blocks = 2048;
+    // persistent screenOutput blocks: about four 16x16 tiles each, 4096..8192 (1080p 4096: 37.2 ->
+    // 36.1 us; 4K 8192: 122 -> 109 us; profiles/r02i_ab_out_blocks.txt); PT_OUT_BLOCKS fixes the count
+    const int ntiles = (int)(grid.x * grid.y);
+#ifdef PT_OUT_BLOCKS
+    const int blocks = PT_OUT_BLOCKS;
+#else
+    const int blocks = ntiles / 4 < 4096 ? 4096 : ntiles / 4 > 8192 ? 8192 : ntiles / 4;
+#endif
     hipLaunchKernelGGL(pt::pt_output, dim3((ntiles < blocks ? ntiles : blocks) + (a->ob_cost ? 1 : 0)), dim3(256), 0, s, *a,
                        (int)grid.x, ntiles);
     return hipGetLastError();
