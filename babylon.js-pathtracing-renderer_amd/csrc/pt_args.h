@@ -33,6 +33,12 @@ __host__ __device__ inline uint32_t pairCode(float rankCode, uint32_t leafBase)
     return rankCode >= 0.0f ? (uint32_t)rankCode * 64u : kLeafBit | (leafBase + (uint32_t)(-1.0f - rankCode) * 48u);
 }
 
+// restart-trail walk (pt_device.h bvhWalkTrail): one trail bit per depth 1..32; a jump table of the
+// inner records at depths 0..kTopLevels, by path, after the leaf records
+constexpr int kTrailMaxDepth = 32;
+constexpr int kTopLevels = 7;
+constexpr unsigned kTopEntries = (2u << kTopLevels) - 1u;   // 255 record copies (64 B), heap order
+
 enum Counter { C_PATHS, C_SEGMENTS, C_NODE, C_LEAF, C_HIT, C_RGBA8, C_OVERFLOW, C_HDR, C_NUM };
 enum ErrBits { E_STACK = 1u };
 
@@ -121,6 +127,7 @@ struct TraceArgs {
     float bvh_root_box[6];     // node 0's box (texels 0.yzw, 1.yzw as uploaded; PROG_PAIRS only): the root test of
                                // every segment reads SGPRs instead of waiting on a load
     uint32_t bvh_pairs_bytes;  // size of the record array (its buffer descriptor)
+    uint32_t bvh_top_base;     // PROG_TRAIL: byte offset of the restart jump table (inner-record copies) in it
     float2* spill;             // megakernel BVH stack levels >= kStackLds: [level][grid lane]
     unsigned spill_stride;
     // longest-first dispatch (megakernel): order[slot] = the 16x16 tile dealt to tile slot `slot`

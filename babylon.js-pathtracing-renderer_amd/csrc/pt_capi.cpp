@@ -44,6 +44,9 @@ hipError_t pt_launch_pairs_pass(int pass, const float4* aabb, long long texels, 
                                 hipStream_t s);
 hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x, int bands,
                                int persist_blocks, hipStream_t s);
+hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, unsigned nrec, const unsigned char* inner,
+                                unsigned* parent, unsigned* refs, unsigned* flag, const float4* rec, uint32_t root,
+                                float4* top, hipStream_t s);
 }
 
 namespace {
@@ -78,7 +81,8 @@ struct DevTex {
     const float4* pairs_leaf = nullptr;
     uint32_t pairs_root = 0;
     float pairs_root_box[6] = {};
-    uint32_t pairs_bytes = 0;   // inner records, then leaf records from pairs_leaf on
+    uint32_t pairs_bytes = 0;   // inner records, then leaf records from pairs_leaf on, then the jump table
+    uint32_t pairs_top = 0;     // byte offset of the restart-trail jump table; 0: the tree is not walkable by the trail
     const DevTex* pairs_tri = nullptr;
     unsigned long long pairs_gen = ~0ull, pairs_tri_gen = ~0ull;
     bool pairs_ok = false;
@@ -452,10 +456,11 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
 {
     *rc = PT_OK;
     const long long texels = (long long)t->w * t->h;
-    if (c->bvh_layout != PT_BVH_PAIRS || t->kind != TEX_F32 || tri->kind != TEX_F32 || texels > (1ll << 24)) return false;
+    if (c->bvh_layout == PT_BVH_REFERENCE || t->kind != TEX_F32 || tri->kind != TEX_F32 || texels > (1ll << 24)) return false;
     if (t->pairs_gen == t->gen && t->pairs_tri == tri && t->pairs_tri_gen == tri->gen) return t->pairs_ok;
     if (t->pairs_mem) { hipStreamSynchronize(c->stream); hipFree(t->pairs_mem); t->pairs_mem = nullptr; }
     t->pairs_ok = false;
+    t->pairs_top = 0;
     t->pairs_gen = t->gen; t->pairs_tri = tri; t->pairs_tri_gen = tri->gen;
     const unsigned nrec = (unsigned)((texels + 1) / 2);
     const unsigned nblk = (nrec + 1023) / 1024;
@@ -463,16 +468,21 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
     unsigned char *inner = nullptr, *leafref = nullptr, *scratch = nullptr;
     unsigned* counts = nullptr;
     float* code = nullptr;
-    hipError_t e = hipMalloc(&scratch, 2 * al(nrec) + al(2 * nblk * sizeof(unsigned)) + al(nrec * sizeof(float)));
+    unsigned *parent = nullptr, *refs = nullptr;   // restart-trail checks (pt_pairs_links / _depth)
+    const size_t u4 = al(nrec * sizeof(unsigned));
+    hipError_t e = hipMalloc(&scratch, 2 * al(nrec) + al(2 * nblk * sizeof(unsigned)) + al(nrec * sizeof(float)) + 2 * u4);
     std::vector<unsigned> h(2 * nblk);
-    unsigned bad = 0;
+    unsigned bad = 0, notrail = 0;
     if (e == hipSuccess) {
         inner = scratch; leafref = scratch + al(nrec);
         counts = (unsigned*)(scratch + 2 * al(nrec));
         code = (float*)((char*)counts + al(2 * nblk * sizeof(unsigned)));
+        parent = (unsigned*)((char*)code + al(nrec * sizeof(float)));
+        refs = (unsigned*)((char*)parent + u4);
         e = hipMemsetAsync(leafref, 0, nrec, c->stream);
     }
-    if (e == hipSuccess) e = hipMemsetAsync(c->d_err + 1, 0, sizeof(unsigned), c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(refs, 0, nrec * sizeof(unsigned), c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_err + 1, 0, 2 * sizeof(unsigned), c->stream);
     const float4* aabb = (const float4*)t->d;
     const float4* trid = (const float4*)tri->d;
     const long long ttex = (long long)tri->w * tri->h;
@@ -494,7 +504,8 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
             n_inner += ci; n_leaf += cl;
         }
         leaf_base = (unsigned)al(n_inner * 64);
-        e = hipMalloc(&t->pairs_mem, al(n_inner * 64) + al(n_leaf * 48) + 256);
+        const size_t top_base = leaf_base + al(n_leaf * 48);
+        e = hipMalloc(&t->pairs_mem, top_base + pt::kTopEntries * 64 + 256);
         if (e == hipSuccess) {
             t->pairs_inner = (const float4*)t->pairs_mem;
             t->pairs_leaf = (const float4*)((char*)t->pairs_mem + leaf_base);
@@ -502,14 +513,26 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
         }
         if (e == hipSuccess) e = pass(3, nullptr, nullptr);
         if (e == hipSuccess) e = pass(4, (float4*)t->pairs_inner, (float4*)t->pairs_leaf);
+        auto tpass = [&](int k, uint32_t root) {
+            return pt_launch_trail_pass(k, aabb, texels, nrec, inner, parent, refs, c->d_err + 2, t->pairs_inner, root,
+                                        (float4*)((char*)t->pairs_mem + top_base), c->stream);
+        };
+        if (e == hipSuccess) e = tpass(1, 0);
+        if (e == hipSuccess) e = tpass(2, 0);
         float root = 0.0f, node0[8] = {};
         if (e == hipSuccess) e = hipMemcpyAsync(&root, code, sizeof(float), hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipMemcpyAsync(node0, aabb, sizeof(node0), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(&notrail, c->d_err + 2, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
         t->pairs_root = pt::pairCode(root, leaf_base);
         const float box6[6] = { node0[1], node0[2], node0[3], node0[5], node0[6], node0[7] };
         std::memcpy(t->pairs_root_box, box6, sizeof(box6));
-        t->pairs_bytes = (uint32_t)(leaf_base + n_leaf * 48);
+        t->pairs_bytes = (uint32_t)(top_base + pt::kTopEntries * 64);
+        // the restart trail's jump table, for trees it can walk (one parent per node, depth <= 32)
+        if (e == hipSuccess && !notrail) {
+            e = tpass(3, t->pairs_root);
+            if (e == hipSuccess) t->pairs_top = (uint32_t)top_base;
+        }
     }
     if (scratch) { hipStreamSynchronize(c->stream); hipFree(scratch); }
     if (e != hipSuccess) { *rc = hipfail(c, e, "BVH child-pair build"); return false; }
@@ -578,9 +601,10 @@ int render_trace(DevFx* fx, DevTex* target)
             a.bvh_root_code = bvh->pairs_root;
             std::memcpy(a.bvh_root_box, bvh->pairs_root_box, sizeof(a.bvh_root_box));
             a.bvh_pairs_bytes = bvh->pairs_bytes;
+            a.bvh_top_base = c->bvh_layout == PT_BVH_TRAIL ? bvh->pairs_top : 0u;
         }
         if (prc) return prc;
-        c->bvh_used = a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
+        c->bvh_used = a.bvh_top_base ? PT_BVH_TRAIL : a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
         a.albedo = tex8(sampler(fx, "tAlbedoTexture"));
         a.bump = tex8(sampler(fx, "tBumpTexture"));
         a.metal = tex8(sampler(fx, "tMetallicTexture"));
@@ -1147,7 +1171,7 @@ int dev_set_backend(Dev* c, int backend)
 
 int dev_set_bvh_layout(Dev* c, int layout)
 {
-    if (!c || (layout != PT_BVH_REFERENCE && layout != PT_BVH_PAIRS)) return PT_ERR_ARG;
+    if (!c || (layout != PT_BVH_REFERENCE && layout != PT_BVH_PAIRS && layout != PT_BVH_TRAIL)) return PT_ERR_ARG;
     c->bvh_layout = layout;
     return PT_OK;
 }
@@ -1169,9 +1193,9 @@ int dev_last_render_ms(Dev* c, int prog, float* ms)
     if (!c || !ms || prog < 0 || prog >= kProgSlots) return PT_ERR_ARG;
     if (!c->draw_events) {   // the first call turns the per-draw events on; later draws report
         c->draw_events = true;
-        return PT_ERR_ARG;
+        return fail(c, PT_ERR_ARG, "per-draw timing was off: it is on from now, for the next draws");
     }
-    if (!c->ev_used[prog]) return PT_ERR_ARG;
+    if (!c->ev_used[prog]) return fail(c, PT_ERR_ARG, "no timed draw of this program yet");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipEventElapsedTime(ms, c->ev0[prog], c->ev1[prog]));
     return PT_OK;

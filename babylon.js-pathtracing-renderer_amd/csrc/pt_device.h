@@ -19,8 +19,10 @@ enum { PROG_CORNELL = 3, PROG_GLTF = 4, PROG_HDRI = 5, PROG_SKY = 6, PROG_QUADRI
 // albedo or bump texture); without +PROG_TEX those branches are compiled out.
 enum { PROG_TEX = 100, PROG_GLTF_TEX = 104, PROG_HDRI_TEX = 105, PROG_SKYMESH_TEX = 108 };
 // +PROG_PAIRS: the same programs walking the child-pair BVH records (bvhWalkPairs) instead of the
-// reference's texel pairs (bvhWalkRef); chosen per draw by the host (pt_capi.cpp ensure_pairs)
-enum { PROG_PAIRS = 1000 };
+// reference's texel pairs (bvhWalkRef); chosen per draw by the host (pt_capi.cpp ensure_pairs).
+// +PROG_TRAIL: the child-pair records walked without a stack beyond an LDS ring (bvhWalkTrail: the
+// restart trail, PT_BVH_TRAIL)
+enum { PROG_PAIRS = 1000, PROG_TRAIL = 2000 };
 template <int P> constexpr int kBase = P % PROG_PAIRS;
 template <int P> constexpr int kScene = kBase<P> % PROG_TEX;
 // the programs whose SceneIntersect walks the glTF model's BVH: glTF, HDRI and the physical-sky
@@ -36,20 +38,24 @@ template <int P> constexpr bool kIsQuadric = P == PROG_QUADRIC;
 // hitObjectID layout: spheres 0-1 (quadric: shapes 0-11), then the quads, then the mesh
 // (objectCount after the quads: 8 in the glTF scene, 6 in the HDRI scene and the sky composite)
 template <int P> constexpr int kQuadId0 = kIsQuadric<P> ? 12 : 2;
-template <int P> constexpr bool kPairs = P >= PROG_PAIRS;
+template <int P> constexpr bool kPairs = P >= PROG_PAIRS;   // child-pair records (stack or trail walk)
+template <int P> constexpr bool kTrail = P >= PROG_TRAIL;
 // every instantiated program variant
 #define PT_FOR_EACH_PROG(X)                                                                           \
     X(PROG_CORNELL) X(PROG_SKY) X(PROG_QUADRIC) X(PROG_GLTF) X(PROG_GLTF_TEX) X(PROG_HDRI) X(PROG_HDRI_TEX)           \
     X(PROG_SKYMESH) X(PROG_SKYMESH_TEX)                                                                                 \
     X(PROG_PAIRS + PROG_GLTF) X(PROG_PAIRS + PROG_GLTF_TEX) X(PROG_PAIRS + PROG_HDRI) X(PROG_PAIRS + PROG_HDRI_TEX)     \
-    X(PROG_PAIRS + PROG_SKYMESH) X(PROG_PAIRS + PROG_SKYMESH_TEX)
+    X(PROG_PAIRS + PROG_SKYMESH) X(PROG_PAIRS + PROG_SKYMESH_TEX)                                                     \
+    X(PROG_TRAIL + PROG_GLTF) X(PROG_TRAIL + PROG_GLTF_TEX) X(PROG_TRAIL + PROG_HDRI) X(PROG_TRAIL + PROG_HDRI_TEX)     \
+    X(PROG_TRAIL + PROG_SKYMESH) X(PROG_TRAIL + PROG_SKYMESH_TEX)
 
 // the kernel variant of a draw: the scene program, +PROG_TEX when the model carries albedo / bump
-// maps, +PROG_PAIRS when the BVH walk uses child-pair records
-__host__ __device__ inline int resolveProgram(int prog, bool textured, bool pairs)
+// maps, +PROG_PAIRS when the BVH walk uses child-pair records with the short stack, +PROG_TRAIL when
+// it walks them with the restart trail
+__host__ __device__ inline int resolveProgram(int prog, bool textured, bool pairs, bool trail = false)
 {
     if (prog != PROG_GLTF && prog != PROG_HDRI && prog != PROG_SKYMESH) return prog;
-    return prog + (textured ? PROG_TEX : 0) + (pairs ? PROG_PAIRS : 0);
+    return prog + (textured ? PROG_TEX : 0) + (pairs ? (trail ? PROG_TRAIL : PROG_PAIRS) : 0);
 }
 // waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 64 -> 8). Measured
 // with one-wave workgroups after the walk's branch-free stack (round 2): the child-pair walk at 8
@@ -66,6 +72,22 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, bool pair
 template <int P> constexpr int kMinWaves = kHasTex<P> ? PT_MINWAVES_TEX : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
 // BVH stack levels in LDS per lane (the rest in the global slab): fewer for the 8-wave variants
 template <int P> constexpr int kStackLdsOf = (kPairs<P> && !kHasTex<P>) ? PT_STACK_LDS_PAIRS : kStackLds;
+// the restart-trail walk's LDS ring (entries per lane): the LDS of the stack walk's levels and its
+// scratch level at 8 waves/SIMD (6 x 8 B + the 32-B G-buffer = 80 B per lane = 160 KB per CU); at 4
+// waves/SIMD the textured variants have room for 14
+#ifndef PT_RING_PAIRS
+#define PT_RING_PAIRS (PT_STACK_LDS_PAIRS + 1)
+#endif
+#ifndef PT_RING_TEX
+#define PT_RING_TEX 14
+#endif
+template <int P> constexpr int kRingOf = kHasTex<P> ? PT_RING_TEX : PT_RING_PAIRS;
+// LDS float2 slots per lane a walk of program P needs: stack levels + the scratch level, or the ring
+template <int P> constexpr int kWalkSlotsOf = kTrail<P> ? kRingOf<P> : kStackLdsOf<P> + 1;
+
+typedef float vf2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) vf2 lds_float2;
+typedef __attribute__((address_space(1))) vf2 glb_float2;
 
 // ------------------------------------------------------------------------------ per-lane state
 struct Path {
@@ -325,7 +347,7 @@ struct BvhResult {
     bool lookup;
     unsigned nodes, leaves, ovf;
 #ifdef PT_SECPROF
-    unsigned steps;
+    unsigned steps, restarts;
 #endif
 };
 
@@ -536,6 +558,160 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     while (pairWalkStep(a, b, O, D, inv, dbl, fast, st, w, r)) r.steps++;
 #else
     while (pairWalkStep(a, b, O, D, inv, dbl, fast, st, w, r)) {}
+#endif
+    hitT = w.hitT;
+    if (w.lookup) { r.triID = w.triID; r.triU = w.triU; r.triV = w.triV; r.lookup = true; }
+}
+
+// ------------------------------------------------------------------------------ restart-trail walk
+// The child-pair records walked without a stack in memory (PT_BVH_TRAIL; north_star's "stackless
+// BVH traversal"): the ordered near-first walk of js/GLTFModelPathTracing_FragmentShader.js:211-298
+// keeps, per depth d of the current path (bit 32 - d of a register),
+//   trail  0: both children were hit and the near one is being walked - the far one is pending
+//             (the reference's stack entry); 1: the level's last child is being walked (the far one
+//             after its pop, the only one hit, or a far one whose push the reference drops);
+//   dir    which child the path took: 1 = B (the right link), 0 = A (the left child n + 1).
+// A pop is arithmetic on the trail: the deepest pending level at or above the current depth
+// becomes its far child, everything below it is cleared ((trail & -L) + L; a carry out of the top
+// ends the walk). The pending levels' (tNear, code) entries - the reference stack's contents - are
+// kept in a per-lane ring of R LDS slots that drops its oldest (shallowest) entry when full; when a
+// pop finds the ring empty the walk restarts: it jumps to the deepest level of a jump table of the
+// top kTopLevels levels' inner records (copies, indexed by the path's dir bits, so the jump is no
+// load of its own) and descends along the dir bits to the pending level's parent, re-testing one
+// child box per level to refill the ring with the pending levels passed on the way. The boxes are
+// the same floats tested by the same function, so a re-tested entry carries the bits it was pushed
+// with, and the walk visits the reference walk's nodes in its order: same hit, same counters
+// (restart descents are not node fetches of the reference's). The reference's overflow (stack
+// entries beyond stackLevels[27] dropped, their pops culled) is restated exactly: a push is dropped
+// when 28 levels above it are pending. Needs trees of depth <= 32 whose nodes have one parent each
+// (checked when the records are built, pt_pairs_depth; the host walks other trees with the stack).
+enum { TW_REC = 0, TW_POP = 1, TW_RESTART = 2 };
+struct TrailWalk {
+    uint32_t code;             // record to load next (TW_REC / TW_RESTART)
+    float hitT;
+    float triID, triU, triV;
+    uint32_t trail, dir;       // per depth d: bit 32 - d
+    uint32_t lvl;              // the bit of the depth of the node `code` addresses (root: 0)
+    int rtop, rcnt;            // ring: next slot, entries held
+    int mode;
+    bool lookup;
+};
+// the bit of the level below `lvl` (the root's children: the top bit)
+PT_D uint32_t childBit(uint32_t lvl) { return lvl ? lvl >> 1 : 0x80000000u; }
+template <int R>
+PT_D void ringPush(lds_float2* ring, unsigned stride, unsigned slot, TrailWalk& w, float t, float code)
+{
+    const vf2 v = { t, code };
+    ring[(unsigned)w.rtop * stride + slot] = v;
+    w.rtop = w.rtop == R - 1 ? 0 : w.rtop + 1;
+    w.rcnt = min(w.rcnt + 1, R);
+}
+// one step; false once the walk is over. A step pops (culled: the step ends there) and/or loads one
+// record: an inner node's two children, a leaf's triangle, or a restart descent's next level.
+template <int R>
+PT_D bool trailWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv, bool dbl, bool fast,
+                        lds_float2* ring, unsigned stride, unsigned slot, TrailWalk& w, BvhResult& r)
+{
+    if (w.mode == TW_POP) {
+        if (w.lvl == 0u) return false;                 // the root is done
+        w.trail = (w.trail & (0u - w.lvl)) + w.lvl;    // the deepest pending level at or above this one
+        if (w.trail == 0u) return false;               // none: the walk is over
+        w.lvl = w.trail & (0u - w.trail);
+        w.dir ^= w.lvl;                                // its far child
+        if (w.rcnt > 0) {
+            w.rtop = w.rtop == 0 ? R - 1 : w.rtop - 1;
+            w.rcnt--;
+            const vf2 e = ring[(unsigned)w.rtop * stride + slot];
+            if (e.x >= w.hitT) return true;            // culled pop
+            w.code = __float_as_uint(e.y);
+            r.nodes++;
+            w.mode = TW_REC;
+        } else {
+            // restart: the jump table's copy of the deepest ancestor it holds, then down the dir bits
+            const int p = min(kTrailMaxDepth - 1 - __builtin_ctz(w.lvl), kTopLevels);   // depth - 1, capped
+            const uint32_t idx = (1u << p) - 1u + (p ? (w.dir >> (kTrailMaxDepth - p)) : 0u);
+            w.code = a.bvh_top_base + idx * 64u;
+            w.lvl = p ? 1u << (kTrailMaxDepth - p) : 0u;
+            w.mode = TW_RESTART;
+#ifdef PT_SECPROF
+            r.restarts++;
+#endif
+        }
+    }
+    const uint32_t off = w.code & ~kLeafBit;
+    const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
+    const float2 r3 = ldRec2(b.rec, off + 48u);
+    const uint32_t bk = childBit(w.lvl);
+    if (w.mode == TW_RESTART) {
+        const bool takeB = (w.dir & bk) != 0u;
+        const bool target = (w.trail & (0u - w.trail)) == bk;   // the popped level: its far child
+        const bool boxB = target ? takeB : !takeB;               // else the pending sibling, if any
+        const f3 mn = boxB ? mk(r1.z, r1.w, r2.x) : mk(r0.x, r0.y, r0.z);
+        const f3 mx = boxB ? mk(r2.y, r2.z, r2.w) : mk(r0.w, r1.x, r1.y);
+        const float t = fast ? boxFast(mn, mx, O, inv) : box(mn, mx, O, inv);
+        w.code = __float_as_uint(takeB ? r3.y : r3.x);
+        w.lvl = bk;
+        if (target) {
+            if (!(t < w.hitT)) { w.mode = TW_POP; return true; }   // culled pop
+            r.nodes++;
+            w.mode = TW_REC;
+            return true;
+        }
+        if (!(w.trail & bk)) ringPush<R>(ring, stride, slot, w, t, takeB ? r3.x : r3.y);
+        return true;
+    }
+    if (!(w.code & kLeafBit)) {
+        r.nodes += 2;
+        float tA, tB;
+        if (fast) {
+            tA = boxFast(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
+            tB = boxFast(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+        } else {
+            tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
+            tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+        }
+        const bool sw = tB < tA;   // the reference's swap: B is the near child
+        const float tF = sw ? tA : tB;
+        const float cN = sw ? r3.y : r3.x, cF = sw ? r3.x : r3.y;
+        const bool hitN = (sw ? tB : tA) < w.hitT, hitF = tF < w.hitT;
+        if (!hitN && !hitF) { w.mode = TW_POP; return true; }
+        if (hitN && hitF) {
+            // the reference pushes the far child at stack index = the levels pending above
+            if (__builtin_popcount(~w.trail & (0u - w.lvl)) < kStackLevels) ringPush<R>(ring, stride, slot, w, tF, cF);
+            else { w.trail |= bk; r.ovf++; atomicOr(a.err, (unsigned)E_STACK); }   // dropped, as beyond stackLevels[27]
+        } else
+            w.trail |= bk;
+        w.dir = (hitN ? sw : !sw) ? (w.dir | bk) : (w.dir & ~bk);
+        w.code = __float_as_uint(hitN ? cN : cF);
+        w.lvl = bk;
+        return true;
+    }
+    r.leaves++;
+    float tu, tv;
+    const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
+    if (d < w.hitT) { w.hitT = d; w.triID = 8.0f * r2.y; w.triU = tu; w.triV = tv; w.lookup = true; }
+    asm volatile("" ::"v"(r3.x));   // keeps the codes' load with the other three (as pairWalkStep)
+    w.mode = TW_POP;
+    return true;
+}
+// ring: R float2 slots per lane at ring[k * stride + slot]
+template <int R>
+PT_D void bvhWalkTrail(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float curT, float& hitT, lds_float2* ring,
+                       unsigned stride, unsigned slot, BvhResult& r)
+{
+    TrailWalk w;
+    w.code = a.bvh_root_code; w.hitT = hitT;
+    w.triID = 0.0f; w.triU = 0.0f; w.triV = 0.0f;
+    w.trail = 0u; w.dir = 0u; w.lvl = 0u; w.rtop = 0; w.rcnt = 0;
+    w.mode = curT < hitT ? TW_REC : TW_POP;
+    w.lookup = false;
+    const bool fast = pairWalkFast(O, inv);
+    const PairBufs b = pairBufs(a);
+#ifdef PT_SECPROF
+    r.steps = 0;
+    while (trailWalkStep<R>(a, b, O, D, inv, dbl, fast, ring, stride, slot, w, r)) r.steps++;
+#else
+    while (trailWalkStep<R>(a, b, O, D, inv, dbl, fast, ring, stride, slot, w, r)) {}
 #endif
     hitT = w.hitT;
     if (w.lookup) { r.triID = w.triID; r.triU = w.triU; r.triV = w.triV; r.lookup = true; }

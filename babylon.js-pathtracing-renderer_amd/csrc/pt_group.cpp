@@ -275,6 +275,9 @@ int pt_ctx_parts(const pt_ctx* c) { return c ? c->n() : PT_ERR_ARG; }
 void pt_ctx_destroy(pt_ctx* c)
 {
     if (!c) return;
+    // every part first: with distinct devices a part's queued halo pull or the gather may still read
+    // another part's buffers over the peer link, and hipFree waits only for its own device's streams
+    for (int k = 0; k < c->n(); k++) dev_sync(c->parts[k]);
     std::vector<pt_effect*> fx(c->effects.begin(), c->effects.end());
     for (auto* f : fx) pt_effect_destroy(f);
     std::vector<pt_texture*> tx(c->textures.begin(), c->textures.end());
@@ -462,6 +465,8 @@ pt_texture* pt_render_target_wrap(pt_ctx* c, int w, int h, void* dptr, int* err)
 int pt_render_target_resize(pt_texture* t, int w, int h)
 {
     if (!t) return PT_ERR_ARG;
+    if (t->ctx->n() > 1)   // neighbours' queued halo pulls / the gather may read this target's parts
+        if (int rc = pt_sync(t->ctx)) return rc;
     for (size_t k = 0; k < t->sub.size(); k++)
         if (int rc = take(t->ctx, (int)k, dev_render_target_resize(t->sub[k], w, h))) return rc;
     t->w = w; t->h = h;
@@ -480,6 +485,7 @@ void pt_texture_destroy(pt_texture* t)
 {
     if (!t) return;
     pt_ctx* c = t->ctx;
+    if (c->n() > 1) pt_sync(c);   // as pt_render_target_resize: no queued peer read of it outlives it
     for (auto* fx : c->effects)
         for (auto& kv : fx->bound)
             if (kv.second == t) kv.second = nullptr;
@@ -538,8 +544,16 @@ int pt_read_pixels(pt_ctx* c, const pt_texture* t, void* dst, size_t bytes)
 int pt_write_pixels(pt_ctx* c, pt_texture* t, const void* src, size_t bytes)
 {
     if (!c || !t) return PT_ERR_ARG;
-    for (int k = 0; k < c->n(); k++)
+    const int N = c->n();
+    for (int k = 0; k < N; k++) {
+        if (N > 1) {   // after the neighbours' last output, whose halo pulls read this part's texels
+            GHIP(c, hipSetDevice(dev_device(c->parts[k])));
+            const int lo = (k + N - 1) % N, hi = (k + 1) % N;
+            if (int rc = wait(c, k, c->ev_out[lo], c->has_out[lo])) return rc;
+            if (int rc = wait(c, k, c->ev_out[hi], c->has_out[hi])) return rc;
+        }
         if (int rc = take(c, k, dev_write_pixels(c->parts[k], t->sub[k], src, bytes))) return rc;
+    }
     return PT_OK;
 }
 
@@ -566,12 +580,18 @@ void* pt_texture_device_ptr(pt_texture* t) { return t ? dev_texture_device_ptr(t
 int pt_last_render_ms(pt_ctx* c, int prog, float* ms)
 {
     if (!c || !ms) return PT_ERR_ARG;
+    // every part is asked (the first call turns each part's per-draw events on), then the first
+    // failure is reported
     float best = 0.0f;
+    int first = PT_OK;
+    std::string msg;
     for (int k = 0; k < c->n(); k++) {
         float v = 0.0f;
-        if (int rc = take(c, k, dev_last_render_ms(c->parts[k], prog, &v))) return rc;
+        const int rc = take(c, k, dev_last_render_ms(c->parts[k], prog, &v));
+        if (rc && !first) { first = rc; msg = c->err; }
         best = std::max(best, v);
     }
+    if (first) { c->err = msg; return first; }
     *ms = best;
     return PT_OK;
 }

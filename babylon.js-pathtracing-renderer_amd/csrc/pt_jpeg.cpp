@@ -48,7 +48,8 @@ struct Decoder {
     bool progressive = false, seenSof = false, adobe = false;
     int adobeTransform = -1;
     int restart = 0;
-    uint16_t q[4][64];      // natural order
+    uint16_t q[4][64] = {};   // natural order
+    bool qset[4] = {};        // tables a DQT segment defined
     Huff dc[4], ac[4];
     Comp c[4];
     // bit reader (F.2.2.5): 0xFF00 -> 0xFF; a marker ends the entropy data (zeros are fed after it)
@@ -112,6 +113,11 @@ struct Decoder {
             if (total > 256 || len < 17 + total) return PT_ERR_DATA;
             Huff& t = cls ? ac[id] : dc[id];
             for (int i = 0; i < total; i++) t.vals[i] = (uint8_t)u8();
+            // DC symbols are magnitude categories: libjpeg-turbo (jpeg_make_d_derived_tbl) rejects any
+            // above 15, which would shift by 16 or more bits in bits() / extend()
+            if (!cls)
+                for (int i = 0; i < total; i++)
+                    if (t.vals[i] > 15) return PT_ERR_DATA;
             memset(t.look, 0, sizeof t.look);
             int code = 0, k = 0;
             for (int l = 1; l <= 16; l++) {
@@ -317,9 +323,11 @@ struct Decoder {
             else if (marker == 0xDB) {
                 int n = len - 2;
                 while (n > 0) {
+                    if (n < 65) return PT_ERR_DATA;   // a table cut short by its segment
                     const int pq = u8();
                     if ((pq >> 4) != 0 || (pq & 15) > 3) return PT_ERR_UNSUPPORTED;   // 16-bit tables
                     for (int i = 0; i < 64; i++) q[pq & 15][kZigzag[i]] = (uint16_t)u8();
+                    qset[pq & 15] = true;
                     n -= 65;
                 }
             } else if (marker == 0xDD) restart = u16();
@@ -510,6 +518,8 @@ int decodeJpeg(const uint8_t* data, size_t size, int* w, int* h, uint8_t* rgba, 
     }
     int rc = d.parse();
     if (rc != PT_OK) return rc;
+    for (int i = 0; i < d.ncomp; i++)   // libjpeg-turbo: JERR_NO_QUANT_TABLE
+        if (!d.qset[d.c[i].tq]) return PT_ERR_DATA;
     *w = d.W; *h = d.H;
     if (!rgba) return PT_OK;
     if (cap < (size_t)d.W * d.H * 4) return PT_ERR_ARG;

@@ -37,9 +37,6 @@ using namespace ptg;
 
 namespace pt {
 
-typedef float vf2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) vf2 lds_float2;
-typedef __attribute__((address_space(1))) vf2 glb_float2;
 // LS = lanes of the block = the stride of one stack level in LDS; NL = stack levels in LDS
 template <int LS, int NL>
 struct MegaStack {
@@ -137,17 +134,21 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     if (kPairs<PROG>) {   // the root's box from the kernel arguments (the same floats as texels 0-1)
         const float* rb = a.bvh_root_box;
         const float rootT = box(mk(rb[0], rb[1], rb[2]), mk(rb[3], rb[4], rb[5]), O, inv);
+        auto walk = [&]() {
+            if (kTrail<PROG>) bvhWalkTrail<kRingOf<PROG>>(a, O, D, inv, dbl, rootT, h.t, (lds_float2*)lds, LS, lane_slot, br);
+            else bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
+        };
 #ifdef PT_SECPROF
         if (cnt.sec) {
             const int ln_ = __lane_id();
             if (ln_ == __builtin_amdgcn_readfirstlane(ln_)) cnt.sec[9] = 0;
-            bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
+            walk();
             atomicMax(&cnt.sec[9], (unsigned long long)br.steps);
             cnt.lane_steps += br.steps;
             if (ln_ == __builtin_amdgcn_readfirstlane(ln_)) cnt.sec[10] += cnt.sec[9];
         } else
 #endif
-        bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
+        walk();
     } else {
         float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
         const float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
@@ -155,7 +156,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     }
     if (COUNT) { cnt.node += br.nodes; cnt.leaf += br.leaves; cnt.ovf += br.ovf; }
 #ifdef PT_SECPROF
-    if (COUNT) { cnt.sget += st.n_get; cnt.sget_slab += st.n_get_slab; cnt.sput += st.n_put; cnt.sput_slab += st.n_put_slab; }
+    if (COUNT) { cnt.sget += st.n_get; cnt.sget_slab += st.n_get_slab + br.restarts; cnt.sput += st.n_put; cnt.sput_slab += st.n_put_slab; }
 #endif
     PT_SEC(cnt, 2);
     if (br.lookup) meshHit<PROG, COUNT>(a, br.triID, br.triU, br.triV, h, cnt);
@@ -331,7 +332,7 @@ static_assert(kTraceBlock == 64 || kTraceBlock == 256, "trace workgroups are one
 template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
 {
-    __shared__ float2 lds_stack[(kStackLdsOf<PROG> + 1) * kTraceBlock];   // + the scratch level (MegaStack::push)
+    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];   // stack levels + the scratch level, or the trail walk's ring
     __shared__ float lds_gout[8 * kTraceBlock];
     const unsigned tid = threadIdx.x;
     const int lane = tid & 63;
@@ -517,7 +518,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_persist(TraceArgs 
                                                                        unsigned n_wave_tiles, unsigned per_wave,
                                                                        unsigned refill)
 {
-    __shared__ float2 lds_stack[(kStackLdsOf<PROG> + 1) * kBlock];   // + the scratch level (MegaStack::push)
+    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kBlock];   // stack levels + the scratch level, or the trail walk's ring
     const unsigned tid = threadIdx.x;
     const unsigned lane = tid & 63u, wave = tid >> 6;
     const unsigned long long below = (1ull << lane) - 1ull;
@@ -841,6 +842,58 @@ __global__ __launch_bounds__(256) void pt_pairs_build(const float4* aabb, long l
     }
 }
 
+// Restart-trail prerequisites (PROG_TRAIL, bvhWalkTrail in pt_device.h), after the records:
+//   links  every child link of an inner node counted (refs) and its parent noted; a node linked twice,
+//          or the root linked at all, is no tree -> *flag
+//   depth  every linked node climbs its parents to the root within kTrailMaxDepth steps, else *flag
+//          (the trail has one bit per depth; unreachable runs are skipped)
+//   top    the jump table: for each depth p <= kTopLevels and path (p A/B bits, heap order) the
+//          inner record the path reaches, copied (64 B); zero where the path meets a leaf first
+__global__ __launch_bounds__(256) void pt_pairs_links(const float4* aabb, long long texels, unsigned nrec,
+                                                      const unsigned char* inner, unsigned* parent, unsigned* refs,
+                                                      unsigned* flag)
+{
+    const unsigned n = blockIdx.x * 256u + threadIdx.x;
+    if (n >= nrec || !inner[n]) return;
+    const unsigned c[2] = { n + 1u, (unsigned)fetch32(aabb, texels, (float)n * 2.0f + 1.0f).x };   // exact: checked by pass 1
+    for (int k = 0; k < 2; k++) {
+        const unsigned old = atomicAdd(&refs[c[k]], 1u);
+        parent[c[k]] = n;
+        if (old != 0u || c[k] == 0u) atomicOr(flag, 1u);
+    }
+}
+
+__global__ __launch_bounds__(256) void pt_pairs_depth(unsigned nrec, const unsigned* parent, const unsigned* refs,
+                                                      unsigned* flag)
+{
+    const unsigned n = blockIdx.x * 256u + threadIdx.x;
+    if (n >= nrec || n == 0u || refs[n] == 0u) return;
+    unsigned m = n;
+    for (int d = 1; d <= kTrailMaxDepth; d++) {
+        m = parent[m];
+        if (m == 0u) return;
+        if (refs[m] == 0u) return;   // a run that is not reached from the root
+    }
+    atomicOr(flag, 1u);
+}
+
+__global__ __launch_bounds__(256) void pt_pairs_top(const float4* rec, uint32_t root, float4* top)
+{
+    const unsigned idx = threadIdx.x;
+    if (idx >= kTopEntries) return;
+    const int p = 31 - __builtin_clz(idx + 1u);
+    const unsigned prefix = idx + 1u - (1u << p);
+    uint32_t code = root;
+    bool ok = true;
+    for (int j = 0; j < p && ok; j++) {
+        if (code & kLeafBit) { ok = false; break; }
+        const float4 c = rec[code / 16u + 3u];
+        code = __float_as_uint(((prefix >> (p - 1 - j)) & 1u) ? c.y : c.x);
+    }
+    if (code & kLeafBit) ok = false;
+    for (int q = 0; q < 4; q++) top[4u * idx + q] = ok ? rec[code / 16u + q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
 // ------------------------------------------------------------------------------ self-test
 // every binary32 pattern with bits 31..24 == hi: fast device sequence vs the IEEE operation it
 // stands for (NaN == NaN); one atomic per wave with a mismatch
@@ -892,7 +945,7 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
 {
     dim3 grid(grid_x * pt::kTraceSub, grid_y), block(pt::kTraceBlock);
     // texture-free models (the bench's StanfordBunny) take the variant without PBR code
-    prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr);
+    prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr, a->bvh_top_base != 0);
 #define PT_CASE(P)                                                                                  \
     case P:                                                                                          \
         if (count) hipLaunchKernelGGL((pt::pt_trace<P, true>), grid, block, 0, s, *a);               \
@@ -918,7 +971,7 @@ hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned
 hipError_t pt_launch_persist(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x,
                              unsigned n_wave_tiles, unsigned per_wave, unsigned refill, hipStream_t s)
 {
-    prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr);
+    prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr, a->bvh_top_base != 0);
     const unsigned waves = (n_wave_tiles + per_wave - 1) / per_wave;
     dim3 grid((waves + 3) / 4), block(pt::kBlock);
 #define PT_CASE(P)                                                                                          \
@@ -950,6 +1003,21 @@ hipError_t pt_launch_pairs_pass(int pass, const float4* aabb, long long texels, 
         hipLaunchKernelGGL(pt::pt_pairs_build, nodes, b256, 0, s, aabb, texels, tri, tri_texels, nrec, code, inner_rec,
                            leaf_rec, inner, leafref, leaf_base);
         break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// the restart-trail passes: 1 links, 2 depth, 3 top (rec = the record array, top its jump table)
+hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, unsigned nrec, const unsigned char* inner,
+                                unsigned* parent, unsigned* refs, unsigned* flag, const float4* rec, uint32_t root,
+                                float4* top, hipStream_t s)
+{
+    const dim3 nodes((nrec + 255) / 256), b256(256);
+    switch (pass) {
+    case 1: hipLaunchKernelGGL(pt::pt_pairs_links, nodes, b256, 0, s, aabb, texels, nrec, inner, parent, refs, flag); break;
+    case 2: hipLaunchKernelGGL(pt::pt_pairs_depth, nodes, b256, 0, s, nrec, parent, refs, flag); break;
+    case 3: hipLaunchKernelGGL(pt::pt_pairs_top, dim3(1), b256, 0, s, rec, root, top); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -183,9 +183,6 @@ __global__ __launch_bounds__(kBlock) void wf_extend(TraceArgs a, WfBufs w, int b
 
 // ============================================================================ BVH walk
 // stack levels >= kStackLds live in a global slab indexed [level][persistent lane]
-typedef float vf2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(3))) vf2 lds_float2;
-typedef __attribute__((address_space(1))) vf2 glb_float2;
 struct WfStack {
     lds_float2* lds;
     unsigned slot;
@@ -216,7 +213,7 @@ struct WfStack {
 template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b)
 {
-    __shared__ float2 lds[kStackLds * kBlock];
+    __shared__ float2 lds[(kTrail<PROG> ? kRingOf<PROG> : kStackLds) * kBlock];   // stack levels, or the trail walk's ring
     const ShardIter it;
     const unsigned n = w.bcnt[b * kShards + it.s];
     const unsigned shard0 = it.s * w.shard_cap;
@@ -241,7 +238,8 @@ __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b
         float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
         BvhResult br = { 0.0f, 0.0f, 0.0f, false, 0u, 0u, 0u };
         WfStack st{ (lds_float2*)lds, tid, (glb_float2*)deep, dstride };
-        if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, rootT, hitT, st, br);
+        if (kTrail<PROG>) bvhWalkTrail<kRingOf<PROG>>(a, O, D, inv, dbl, rootT, hitT, (lds_float2*)lds, kBlock, tid, br);
+        else if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, rootT, hitT, st, br);
         else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, hitT, st, br);
         const unsigned nodes = br.nodes, leaves = br.leaves, ovf = br.ovf;
         const bool lookup = br.lookup;
@@ -419,7 +417,7 @@ extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceAr
                                           int tiles_x, int bands, int persist_blocks, hipStream_t s)
 {
     using namespace pt;
-    prog = resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr);
+    prog = resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr, a->bvh_top_base != 0);
     dim3 tiles(tiles_x, bands), blk(kBlock);
     if (count) hipLaunchKernelGGL((wf_raygen<true>), tiles, blk, 0, s, *a, *w);
     else hipLaunchKernelGGL((wf_raygen<false>), tiles, blk, 0, s, *a, *w);

@@ -164,10 +164,15 @@ enum pt_backend { PT_BACKEND_MEGAKERNEL = 0, PT_BACKEND_WAVEFRONT = 1, PT_BACKEN
 int pt_set_backend(pt_ctx* ctx, int backend);
 /* BVH walk of the glTF program. PT_BVH_PAIRS (default) re-packs tAABBTexture once per upload into
  * 64-byte child-pair records (both children's boxes in one line, pops without a fetch) and walks
- * those; a texture whose links are not exact in-range integers keeps PT_BVH_REFERENCE, the walk
- * over the reference's own texel pairs. Same nodes, same order, same results either way.
+ * those with the reference's short stack (LDS levels, deeper ones in a global slab); PT_BVH_TRAIL
+ * walks the same records stacklessly: a restart trail of one bit per tree level plus a per-lane LDS
+ * ring of the deepest pending entries, re-descending from a jump table of the top levels when the
+ * ring runs dry (no stack memory beyond LDS; trees deeper than 32 levels, or whose nodes have more
+ * than one parent, keep PT_BVH_PAIRS). A texture whose links are not exact in-range integers keeps
+ * PT_BVH_REFERENCE, the walk over the reference's own texel pairs. Same nodes, same order, same
+ * results every way (js/GLTFModelPathTracing_FragmentShader.js:211-298).
  * pt_bvh_layout_used reports what the last glTF draw of the context walked (-1: none yet). */
-enum pt_bvh_layout { PT_BVH_REFERENCE = 0, PT_BVH_PAIRS = 1 };
+enum pt_bvh_layout { PT_BVH_REFERENCE = 0, PT_BVH_PAIRS = 1, PT_BVH_TRAIL = 2 };
 int pt_set_bvh_layout(pt_ctx* ctx, int layout);
 int pt_bvh_layout_used(pt_ctx* ctx);
 /* Enqueue this context's work on a caller-owned HIP stream (e.g. torch.cuda.current_stream(), so

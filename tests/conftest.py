@@ -17,6 +17,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+def pytest_collection_modifyitems(config, items):
+    # oracle/_ref/ holds the build container's mechanical transcription of the reference GLSL
+    # (oracle/xcheck); it is gpurun-ignored and must never reach the GPU box, where the committed
+    # frames under tests/golden/xcheck/ stand in for it. A GPU session that finds it refuses to run.
+    if any(it.get_closest_marker("gpu") for it in items) and not os.path.isdir("/root/reference"):
+        ref = os.path.join(ROOT, "oracle", "_ref")
+        if os.path.isdir(ref) and os.listdir(ref):
+            raise pytest.UsageError("oracle/_ref/ (the transcribed reference) is present on the GPU box: "
+                                    "it must stay gpurun-ignored (.gpurunignore)")
+
+
 @pytest.fixture(scope="session")
 def gold():
     return GOLD

@@ -5,7 +5,9 @@ js/*_FragmentShader.js into C++ by syntax-only rewrites (literal suffixes, swizz
 braced constructors, out-parameter copies) over a GLSL stand-in (oracle/xcheck/glsl_shim.h) that
 shares only the pinned transcendental sequences with the oracle; oracle/xcheck/run_xcheck.py ran
 it in the build container on every recorded stream and stored its accumulation after each frame
-under tests/golden/xcheck/ (the reference is not on the GPU box). These tests pin the oracle and
+under tests/golden/xcheck/. Neither the reference nor its transcription (the git-ignored
+oracle/_ref/, also listed in .gpurunignore; tests/conftest.py refuses a GPU session that finds
+it) travels to the GPU box: there only those committed frames are read. These tests pin the oracle and
 the HIP kernels to those frames bit for bit: a misreading of the GLSL (an expression, a branch, a
 constant, the order of rng() calls) in the hand-written oracle or kernels would show here, which
 the oracle-vs-HIP tests alone cannot see. Radiance parity against a GL driver stays unpinned: the

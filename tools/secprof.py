@@ -18,6 +18,7 @@ NAMES = ["wave_record_loads", "uniform_wave_record_loads", "lanes_at_record_load
 for wl in (sys.argv[1:] or ["helmet", "bunny", "dragon", "sky_dragon"]):
     meta, mesh_arrays, maps, (W, Hh) = H.workload(wl)
     e = bp.Engine(0)
+    e.set_bvh_layout(os.environ.get("PT_BVH", "pairs"))   # trail: pops_slab counts the walk's restarts
     mesh = H.texture_payloads(meta, mesh_arrays) if mesh_arrays is not None else None
     p = bp.StreamPlayer(e, meta, H.bluenoise(), mesh, W, Hh)
     if maps:
