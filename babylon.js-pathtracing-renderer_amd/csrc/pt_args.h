@@ -33,9 +33,10 @@ __host__ __device__ inline uint32_t pairCode(float rankCode, uint32_t leafBase)
     return rankCode >= 0.0f ? (uint32_t)rankCode * 64u : kLeafBit | (leafBase + (uint32_t)(-1.0f - rankCode) * 48u);
 }
 
-// restart-trail walk (pt_device.h bvhWalkTrail): one trail bit per depth 1..32; a jump table of the
-// inner records at depths 0..kTopLevels, by path, after the leaf records
-constexpr int kTrailMaxDepth = 32;
+// restart-trail walk (pt_device.h bvhWalkTrail): one trail bit per depth 1..31 of a register; trees of
+// depth <= 28 (stackLevels[28] then never overflows); a jump table of the inner records at depths
+// 0..kTopLevels, by path, after the leaf records
+constexpr int kTrailMaxDepth = 28;
 constexpr int kTopLevels = 7;
 constexpr unsigned kTopEntries = (2u << kTopLevels) - 1u;   // 255 record copies (64 B), heap order
 

@@ -566,102 +566,68 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
 // ------------------------------------------------------------------------------ restart-trail walk
 // The child-pair records walked without a stack in memory (PT_BVH_TRAIL; north_star's "stackless
 // BVH traversal"): the ordered near-first walk of js/GLTFModelPathTracing_FragmentShader.js:211-298
-// keeps, per depth d of the current path (bit 32 - d of a register),
+// keeps, per depth d of the current path (bit 31 - d of a register; the root's bit 31 has none),
 //   trail  0: both children were hit and the near one is being walked - the far one is pending
 //             (the reference's stack entry); 1: the level's last child is being walked (the far one
-//             after its pop, the only one hit, or a far one whose push the reference drops);
+//             after its pop, or the only one hit);
 //   dir    which child the path took: 1 = B (the right link), 0 = A (the left child n + 1).
 // A pop is arithmetic on the trail: the deepest pending level at or above the current depth
-// becomes its far child, everything below it is cleared ((trail & -L) + L; a carry out of the top
-// ends the walk). The pending levels' (tNear, code) entries - the reference stack's contents - are
-// kept in a per-lane ring of R LDS slots that drops its oldest (shallowest) entry when full; when a
-// pop finds the ring empty the walk restarts: it jumps to the deepest level of a jump table of the
+// becomes its far child, everything below it is cleared ((trail & -L) + L; a carry into the root's
+// bit ends the walk). The pending levels' (tNear, code) entries - the reference stack's contents -
+// are kept in a per-lane ring of R LDS slots that drops its oldest (shallowest) entry when full; when
+// a pop finds the ring empty the walk restarts: it jumps to the deepest level of a jump table of the
 // top kTopLevels levels' inner records (copies, indexed by the path's dir bits, so the jump is no
-// load of its own) and descends along the dir bits to the pending level's parent, re-testing one
-// child box per level to refill the ring with the pending levels passed on the way. The boxes are
-// the same floats tested by the same function, so a re-tested entry carries the bits it was pushed
-// with, and the walk visits the reference walk's nodes in its order: same hit, same counters
-// (restart descents are not node fetches of the reference's). The reference's overflow (stack
-// entries beyond stackLevels[27] dropped, their pops culled) is restated exactly: a push is dropped
-// when 28 levels above it are pending. Needs trees of depth <= 32 whose nodes have one parent each
-// (checked when the records are built, pt_pairs_depth; the host walks other trees with the stack).
-enum { TW_REC = 0, TW_POP = 1, TW_RESTART = 2 };
+// load of its own) and descends along the dir bits to the pending level's parent, testing on the way
+// the pending siblings' boxes to refill the ring. The boxes are the same floats tested by the same
+// function, so a re-tested entry carries the bits it was pushed with, and the walk visits the
+// reference walk's nodes in its order: same hit, same counters (restart descents are no node fetches
+// of the reference's). The host gives it trees of depth <= 28, whose nodes have one parent each
+// (pt_pairs_depth): there at most 27 far children are ever pending, so the reference's stack
+// (stackLevels[28]) never overflows and no push is dropped; other trees keep the stack walk.
 struct TrailWalk {
-    uint32_t code;             // record to load next (TW_REC / TW_RESTART)
+    uint32_t code;             // record to load next
     float hitT;
     float triID, triU, triV;
-    uint32_t trail, dir;       // per depth d: bit 32 - d
-    uint32_t lvl;              // the bit of the depth of the node `code` addresses (root: 0)
+    uint32_t trail, dir;       // per depth d: bit 31 - d
+    uint32_t lvl;              // the bit of the depth of the node `code` addresses (root: bit 31)
     int rtop, rcnt;            // ring: next slot, entries held
-    int mode;
-    bool lookup;
+    bool pop, restart, lookup;
 };
-// the bit of the level below `lvl` (the root's children: the top bit)
-PT_D uint32_t childBit(uint32_t lvl) { return lvl ? lvl >> 1 : 0x80000000u; }
-template <int R>
-PT_D void ringPush(lds_float2* ring, unsigned stride, unsigned slot, TrailWalk& w, float t, float code)
-{
-    const vf2 v = { t, code };
-    ring[(unsigned)w.rtop * stride + slot] = v;
-    w.rtop = w.rtop == R - 1 ? 0 : w.rtop + 1;
-    w.rcnt = min(w.rcnt + 1, R);
-}
+constexpr uint32_t kRootBit = 0x80000000u;
 // one step; false once the walk is over. A step pops (culled: the step ends there) and/or loads one
 // record: an inner node's two children, a leaf's triangle, or a restart descent's next level.
 template <int R>
 PT_D bool trailWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv, bool dbl, bool fast,
                         lds_float2* ring, unsigned stride, unsigned slot, TrailWalk& w, BvhResult& r)
 {
-    if (w.mode == TW_POP) {
-        if (w.lvl == 0u) return false;                 // the root is done
+    if (w.pop) {
         w.trail = (w.trail & (0u - w.lvl)) + w.lvl;    // the deepest pending level at or above this one
-        if (w.trail == 0u) return false;               // none: the walk is over
+        if (w.trail & kRootBit) return false;          // none: the walk is over
         w.lvl = w.trail & (0u - w.trail);
         w.dir ^= w.lvl;                                // its far child
-        if (w.rcnt > 0) {
-            w.rtop = w.rtop == 0 ? R - 1 : w.rtop - 1;
-            w.rcnt--;
-            const vf2 e = ring[(unsigned)w.rtop * stride + slot];
-            if (e.x >= w.hitT) return true;            // culled pop
-            w.code = __float_as_uint(e.y);
-            r.nodes++;
-            w.mode = TW_REC;
-        } else {
+        w.rtop = (w.rtop == 0 ? R : w.rtop) - 1;       // (moving an empty ring's top is harmless)
+        const vf2 e = ring[(unsigned)w.rtop * stride + slot];
+        if (w.rcnt == 0) {
             // restart: the jump table's copy of the deepest ancestor it holds, then down the dir bits
-            const int p = min(kTrailMaxDepth - 1 - __builtin_ctz(w.lvl), kTopLevels);   // depth - 1, capped
-            const uint32_t idx = (1u << p) - 1u + (p ? (w.dir >> (kTrailMaxDepth - p)) : 0u);
-            w.code = a.bvh_top_base + idx * 64u;
-            w.lvl = p ? 1u << (kTrailMaxDepth - p) : 0u;
-            w.mode = TW_RESTART;
+            const int p = min(30 - __builtin_ctz(w.lvl), kTopLevels);   // the popped depth - 1, capped
+            w.code = a.bvh_top_base + ((1u << p) - 1u + (w.dir >> (31 - p))) * 64u;
+            w.lvl = kRootBit >> p;
+            w.restart = true;
 #ifdef PT_SECPROF
             r.restarts++;
 #endif
+        } else {
+            w.rcnt--;
+            if (e.x >= w.hitT) return true;            // culled pop
+            w.code = __float_as_uint(e.y);
+            r.nodes++;
         }
+        w.pop = false;
     }
     const uint32_t off = w.code & ~kLeafBit;
     const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
     const float2 r3 = ldRec2(b.rec, off + 48u);
-    const uint32_t bk = childBit(w.lvl);
-    if (w.mode == TW_RESTART) {
-        const bool takeB = (w.dir & bk) != 0u;
-        const bool target = (w.trail & (0u - w.trail)) == bk;   // the popped level: its far child
-        const bool boxB = target ? takeB : !takeB;               // else the pending sibling, if any
-        const f3 mn = boxB ? mk(r1.z, r1.w, r2.x) : mk(r0.x, r0.y, r0.z);
-        const f3 mx = boxB ? mk(r2.y, r2.z, r2.w) : mk(r0.w, r1.x, r1.y);
-        const float t = fast ? boxFast(mn, mx, O, inv) : box(mn, mx, O, inv);
-        w.code = __float_as_uint(takeB ? r3.y : r3.x);
-        w.lvl = bk;
-        if (target) {
-            if (!(t < w.hitT)) { w.mode = TW_POP; return true; }   // culled pop
-            r.nodes++;
-            w.mode = TW_REC;
-            return true;
-        }
-        if (!(w.trail & bk)) ringPush<R>(ring, stride, slot, w, t, takeB ? r3.x : r3.y);
-        return true;
-    }
-    if (!(w.code & kLeafBit)) {
-        r.nodes += 2;
+    if (!(w.code & kLeafBit)) {   // an inner record (restart descents visit inner records only)
         float tA, tB;
         if (fast) {
             tA = boxFast(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
@@ -670,19 +636,36 @@ PT_D bool trailWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 in
             tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
             tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
         }
+        const uint32_t bk = w.lvl >> 1;
+        // the reference step (the near child next if hit, else the far one; the far one pushed when
+        // both are hit) and a restart descent's step (the child the dir bit names; the sibling pushed
+        // if the level is pending; at the popped level its far child, culled against hitT) share one
+        // form: take child B or A, push the other
+        const bool rs = w.restart;
         const bool sw = tB < tA;   // the reference's swap: B is the near child
-        const float tF = sw ? tA : tB;
-        const float cN = sw ? r3.y : r3.x, cF = sw ? r3.x : r3.y;
-        const bool hitN = (sw ? tB : tA) < w.hitT, hitF = tF < w.hitT;
-        if (!hitN && !hitF) { w.mode = TW_POP; return true; }
-        if (hitN && hitF) {
-            // the reference pushes the far child at stack index = the levels pending above
-            if (__builtin_popcount(~w.trail & (0u - w.lvl)) < kStackLevels) ringPush<R>(ring, stride, slot, w, tF, cF);
-            else { w.trail |= bk; r.ovf++; atomicOr(a.err, (unsigned)E_STACK); }   // dropped, as beyond stackLevels[27]
-        } else
-            w.trail |= bk;
-        w.dir = (hitN ? sw : !sw) ? (w.dir | bk) : (w.dir & ~bk);
-        w.code = __float_as_uint(hitN ? cN : cF);
+        const bool hitN = (sw ? tB : tA) < w.hitT, hitF = (sw ? tA : tB) < w.hitT;
+        const bool target = rs && (w.trail & (0u - w.trail)) == bk;   // the popped level
+        const bool takeB = rs ? (w.dir & bk) != 0u : (hitN ? sw : !sw);
+        const bool push = rs ? !target && !(w.trail & bk) : hitN && hitF;
+        if (rs ? target && !((takeB ? tB : tA) < w.hitT) : !hitN && !hitF) {   // culled pop / no child hit
+            if (rs) w.lvl = bk;
+            w.restart = false;
+            w.pop = true;
+            return true;
+        }
+        r.nodes += rs ? (target ? 1u : 0u) : 2u;
+        if (target) w.restart = false;
+        if (!rs) {
+            if (!push) w.trail |= bk;
+            w.dir = takeB ? (w.dir | bk) : (w.dir & ~bk);
+        }
+        if (push) {
+            const vf2 v = { takeB ? tA : tB, takeB ? r3.x : r3.y };
+            ring[(unsigned)w.rtop * stride + slot] = v;
+            w.rtop = w.rtop == R - 1 ? 0 : w.rtop + 1;
+            w.rcnt = min(w.rcnt + 1, R);
+        }
+        w.code = __float_as_uint(takeB ? r3.y : r3.x);
         w.lvl = bk;
         return true;
     }
@@ -691,7 +674,7 @@ PT_D bool trailWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 in
     const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
     if (d < w.hitT) { w.hitT = d; w.triID = 8.0f * r2.y; w.triU = tu; w.triV = tv; w.lookup = true; }
     asm volatile("" ::"v"(r3.x));   // keeps the codes' load with the other three (as pairWalkStep)
-    w.mode = TW_POP;
+    w.pop = true;
     return true;
 }
 // ring: R float2 slots per lane at ring[k * stride + slot]
@@ -702,8 +685,9 @@ PT_D void bvhWalkTrail(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     TrailWalk w;
     w.code = a.bvh_root_code; w.hitT = hitT;
     w.triID = 0.0f; w.triU = 0.0f; w.triV = 0.0f;
-    w.trail = 0u; w.dir = 0u; w.lvl = 0u; w.rtop = 0; w.rcnt = 0;
-    w.mode = curT < hitT ? TW_REC : TW_POP;
+    w.trail = 0u; w.dir = 0u; w.lvl = kRootBit; w.rtop = 0; w.rcnt = 0;
+    w.pop = !(curT < hitT);
+    w.restart = false;
     w.lookup = false;
     const bool fast = pairWalkFast(O, inv);
     const PairBufs b = pairBufs(a);

@@ -14,21 +14,25 @@ screenOutput, as in the reference's render loop (js/GLTF_Model_Path_Tracing.js:1
 
 Multi-GPU (one process per GPU): `--gpus N` with no WORLD_SIZE in the environment launches the N
 ranks itself (torch.distributed.run, 127.0.0.1) before anything touches a GPU; under a launcher,
-WORLD_SIZE must equal --gpus. dragon / bunny / helmet scale weakly (N GPUs render N x 2.07 MP:
-1920x1080, 3840x1080, 3840x2160, 7680x2160 for N = 1, 2, 4, 8); --size or sky_dragon fix the frame
-and split it (strong scaling, BASELINE configs[3]/[4]). The frame is cut into 16-row bands dealt
+WORLD_SIZE must equal --gpus. At N > 1 the frame is BASELINE configs[3]'s 3840x2160 split over the
+GPUs (strong scaling; the N = 1 line carries the same frame on one GPU as `dragon_4k_1gpu`), or with
+--scaling weak N x 2.07 MP (1920x1080, 3840x1080, 3840x2160, 7680x2160). The frame is cut into 16-row bands dealt
 round-robin (pt_set_row_partition); per frame every rank exchanges the 2 accumulation rows above and
 below its bands with its band neighbours (RCCL P2P), runs screenOutput on its own bands into a
 canvas over a torch tensor, and the RGBA8 bands are gathered to rank 0 (RCCL, asynchronous, under
 the next frame). Every libpt draw and every torch/RCCL op of a rank is ordered on one dedicated
-torch stream (not the legacy default stream).
+torch stream (not the legacy default stream). Rank 0 then measures the same frame over the same GPUs
+through one multi-part context (`--engine multipart`: libpt's own fan-out, peer copies, no RCCL) in a
+child process and adds it to the line as `multipart`.
 
 At N = 1 the line also carries the roofline of the path-tracing kernel: algorithmic bytes per launch
 (counted exactly by a counting replay of the same frames) over the average launch
 time (HIP events in the timed region) against 8 TB/s, and the L2-to-fabric traffic of the same
 kernel measured live by two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over 5 frames of the
 same workload, and the CPU baseline (the oracle on the host's cores available to this job, pinned
-with taskset, in a child process). Prints ONE JSON line (rank 0).
+with taskset, in a child process); and, for the default dragon workload, fields measured in the same
+run: the 4K frame on one GPU (`dragon_4k_1gpu`), the scan-like stand-in (`bunny16_1080p`) and
+configs[4]'s 1024-frame converging run timed whole (`converge_1024spp`). Prints ONE JSON line (rank 0).
 """
 import argparse
 import csv
@@ -59,6 +63,7 @@ METRICS = {
     "helmet": "Mpaths/s + achieved HBM GB/s, DamagedHelmet full PBR maps + HDRI env 1080p (BASELINE configs[2])",
     "sky_dragon": "Mpaths/s + achieved HBM GB/s, Physical_Sky_Model + StanfordDragon 3840x2160 progressive "
                   "(BASELINE configs[4])",
+    "bunny16": "Mpaths/s + achieved HBM GB/s, StanfordBunny split x16 (485,408 triangles) 1080p 1spp",
 }
 DATA = {
     "dragon": "a 524,288-triangle procedural stand-in for the missing StanfordDragon.glb (native builder), "
@@ -69,6 +74,8 @@ DATA = {
               "(the .hdr files are missing from the reference)",
     "sky_dragon": "the physical-sky page's recorded stream + the glTF model uniforms (helpers.sky_mesh_stream), "
                   "the 524,288-triangle dragon stand-in",
+    "bunny16": "the reference's StanfordBunny with every triangle split x16 at edge midpoints (same surface, "
+               "485,408 triangles, native builder), the glTF page's recorded stream",
 }
 
 
@@ -198,10 +205,195 @@ def launch_check(args, world, rank):
         seen = 1
     if rank == 0:
         print(json.dumps({"check": "launch", "n_gpus": world, "ranks_seen": seen, "backend": backend if world > 1 else None,
-                          "gpus_requested": args.gpus}), flush=True)
+                          "gpus_requested": args.gpus, "workload": args.workload, **plan(args, world)}), flush=True)
     if world > 1:
         tdist.destroy_process_group()
     return 0
+
+
+def make_player(engine, workload, W, Hh, rt_ptrs=None):
+    """The workload's recorded stream, mesh and maps bound to `engine` at W x H (tests/helpers.py)."""
+    import babylon_pt as bp
+    import helpers as H
+    meta, mesh_arrays, maps, _ = H.workload(workload)
+    player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, mesh_arrays), W, Hh, rt_ptrs)
+    if maps:
+        for kind, sampler in H.PBR_SAMPLERS.items():
+            player.textures[sampler] = bp.Texture(engine, maps[kind], name=kind)
+    return player, meta["scene"], int(mesh_arrays["tri"].shape[0])
+
+
+def frame_size_for(args, world):
+    """--size, else the workload's own size at N = 1 (1080p; sky_dragon 4K); at N > 1 BASELINE
+    configs[3]'s 3840x2160 split over the GPUs (strong, the default), or N x 2.07 MP (weak)."""
+    if args.size:
+        return tuple(int(v) for v in args.size.lower().split("x"))
+    if args.workload == "sky_dragon" or (world > 1 and args.scaling == "strong"):
+        return 3840, 2160
+    return frame_size(world)
+
+
+def plan(args, world):
+    """What a run measures, from its arguments (CPU-testable): the frame, the scaling mode and the
+    kernel-timing sample rate."""
+    W, Hh = frame_size_for(args, world)
+    fixed = world > 1 and (args.scaling == "strong" or args.size is not None or args.workload == "sky_dragon")
+    return {"width": W, "height": Hh, "scaling": "strong" if fixed else "weak",
+            "event_every": args.event_every or max(1, args.steps // 10)}
+
+
+def timed_region(engine, step, first, count, event_every, barrier_sync, program):
+    """`count` steps from frame index `first`, bracketed by barrier_sync, with HIP-event windows around
+    every event_every-th draw of each kind. Returns (elapsed s, kernel_ms dict, bracketed launches)."""
+    os.environ["PT_TIMING_EVERY"] = str(event_every)
+    engine.timing_begin()
+    t0 = time.perf_counter()
+    for k in range(first, first + count):
+        step(k)
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    pt_ms, pt_n = engine.timing_end(program)
+    cp_ms, _ = engine.timing_end("screenCopy")
+    out_ms, _ = engine.timing_end("screenOutput")
+    n = max(1, pt_n)
+    return elapsed, {"pathtrace": round(pt_ms / n, 4), "screen_copy": round(cp_ms / n, 4),
+                     "screen_output": round(out_ms / n, 4)}, pt_n
+
+
+def kernel_name(layout, program, workload):
+    return "pt_trace<%s%s%s>" % ({"pairs": "PAIRS+", "trail": "TRAIL+"}.get(layout, ""), program.upper(),
+                                 "+TEX" if workload == "helmet" else "")
+
+
+def single_gpu_run(engine, workload, W, Hh, warmup, steps, event_every, from_frame_one=False):
+    """One workload at W x H on `engine`, pathTracing + screenCopy + screenOutput per step. With
+    from_frame_one the run starts at the stream's frame 1 (history cleared, the recorded frames
+    first), so the last timed frame is frame warmup + steps of a progressive run from scratch
+    (configs[4]); else it continues after the recording. Returns (player, program, triangles,
+    elapsed s, kernel_ms, bracketed launches)."""
+    player, program, tris = make_player(engine, workload, W, Hh)
+    engine.resize_canvas(W, Hh)
+    nrec = len(player.meta["frames"])
+
+    def step(k):
+        if from_frame_one and k < nrec:
+            player.play_frame(k)
+            return
+        for call in player.synth_frame(k - nrec if from_frame_one else k):
+            player.play_call(call)
+
+    for k in range(warmup):
+        step(k)
+    engine.sync()
+    elapsed, km, n = timed_region(engine, step, warmup, steps, event_every, engine.sync, program)
+    return player, program, tris, elapsed, km, n
+
+
+def run_anchors(engine, args):
+    """Fields beside the N = 1 headline, measured in the same run on the same engine:
+    dragon_4k_1gpu - the dragon stand-in at 3840x2160 (BASELINE configs[3] on one GPU: the anchor of
+                     the driver's 1 -> N strong-scaling curve, which renders that frame);
+    bunny16_1080p  - the StanfordBunny split x16 (485,408 triangles: scanned geometry at the dragon's
+                     size) at the metric's config, beside the procedural torus;
+    converge_1024spp - BASELINE configs[4] as a run: sky + dragon stand-in at 3840x2160, frames 1..1024
+                     from a cleared history, pathTracing + screenCopy + 5x5 screenOutput each, timed
+                     whole (no extrapolation); --dump-canvas PATH also saves frame 1024's canvas."""
+    out = {}
+    steps4k = max(20, args.steps // 5)
+    _, _, tris, el, km, n = single_gpu_run(engine, "dragon", 3840, 2160, 5, steps4k, max(1, steps4k // 10))
+    out["dragon_4k_1gpu"] = {"value": round(3840 * 2160 * steps4k / el / 1e6, 2), "unit": "Mpaths/s",
+                             "ms_per_step": round(el / steps4k * 1e3, 4), "steps": steps4k, "kernel_ms": km,
+                             "width": 3840, "height": 2160, "triangles": tris}
+    _, _, tris, el, km, n = single_gpu_run(engine, "bunny16", 1920, 1080, 10, args.steps, max(1, args.steps // 10))
+    out["bunny16_1080p"] = {"value": round(1920 * 1080 * args.steps / el / 1e6, 2), "unit": "Mpaths/s",
+                            "ms_per_step": round(el / args.steps * 1e3, 4), "steps": args.steps, "kernel_ms": km,
+                            "triangles": tris, "bvh_walk": engine.bvh_layout_used()}
+    _, _, tris, el, km, n = single_gpu_run(engine, "sky_dragon", 3840, 2160, 0, CONVERGED_SPP, CONVERGED_SPP // 10,
+                                           from_frame_one=True)
+    conv = {"seconds": round(el, 4), "frames": CONVERGED_SPP, "ms_per_frame": round(el / CONVERGED_SPP * 1e3, 4),
+            "mpaths_per_s": round(3840 * 2160 * CONVERGED_SPP / el / 1e6, 2), "kernel_ms": km, "measured": True,
+            "note": "frames 1..%d of the sky + dragon stand-in stream from a cleared history, 3840x2160, each "
+                    "pathTracing + screenCopy + screenOutput; wall clock of the whole run" % CONVERGED_SPP}
+    if args.dump_canvas:
+        import numpy as np
+        path = os.path.splitext(args.dump_canvas)[0] + "_sky_dragon_%dspp.npy" % CONVERGED_SPP
+        np.save(path, engine.read_canvas(3840, 2160))
+        conv["canvas"] = os.path.basename(path)
+    out["converge_%dspp" % CONVERGED_SPP] = conv
+    return out
+
+
+def multipart_devices(args):
+    if args.devices:
+        return [int(d) for d in args.devices.split(",")]
+    n = args.gpus
+    try:
+        import torch
+        visible = torch.cuda.device_count()   # counts without initialising the GPU on this image
+    except Exception:
+        visible = 1
+    return list(range(n)) if visible >= n else [0] * n
+
+
+def multipart_main(args, event_every):
+    """--engine multipart: one process, one pt_ctx_create_devices context of --gpus parts (the route
+    the Node host takes with PT_DEVICES, js/babylon_pt.js): every draw fans out inside pt_render, halo
+    rows and the canvas gather move by peer copies, no RCCL. Prints one JSON line."""
+    import babylon_pt as bp
+    devs = multipart_devices(args)
+    W, Hh = frame_size_for(args, len(devs))
+    engine = bp.Engine(devices=devs)
+    player, program, tris = make_player(engine, args.workload, W, Hh)
+    engine.resize_canvas(W, Hh)
+
+    def step(k):
+        for call in player.synth_frame(k):
+            player.play_call(call)
+
+    for k in range(args.warmup):
+        step(k)
+    engine.sync()
+    elapsed, km, n = timed_region(engine, step, args.warmup, args.steps, event_every, engine.sync, program)
+    if args.dump_canvas:
+        import numpy as np
+        np.save(args.dump_canvas, engine.read_canvas(W, Hh))
+    line = {"metric": baseline_metric() if args.workload == "dragon" else METRICS[args.workload],
+            "value": round(W * Hh * args.steps / elapsed / 1e6, 2), "unit": "Mpaths/s",
+            "n_gpus": len(set(devs)), "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "strong" if len(devs) > 1 else "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: " + DATA[args.workload], "engine": "multipart", "parts_seen": engine.parts,
+            "devices": devs,
+            "config": {"workload": "%s_%s_%dx%d" % (program, args.workload, W, Hh), "width": W, "height": Hh,
+                       "triangles": tris, "parallelism": "row-bands x%d (one context, %d parts)" % (len(devs), engine.parts),
+                       "gather": "per frame: 2-row halo pulls from band neighbours and the RGBA8 gather to part 0 "
+                                 "as peer copies inside pt_render (hipMemcpy2DAsync, event-ordered)"},
+            "kernel_timing": "HIP events around every %d-th timed frame's draws, slowest part (%d launches)" % (event_every, n),
+            "kernel_ms": km}
+    print(json.dumps(line), flush=True)
+    engine.dispose()
+    return 0
+
+
+def multipart_child(args, world, W, Hh):
+    """Rank 0 of an N-rank run: the multipart curve of the same frame over the same GPUs, in a child
+    process (the ranks keep their contexts but wait on the host meanwhile). A failure is reported,
+    never fatal to the RCCL line."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    steps = min(args.steps, 100)
+    cmd = [sys.executable, os.path.abspath(__file__), "--engine", "multipart", "--gpus", str(world),
+           "--devices", ",".join(str(d) for d in range(world)), "--size", "%dx%d" % (W, Hh), "--workload", args.workload,
+           "--steps", str(steps), "--warmup", str(min(args.warmup, 10)), "--cpu-budget", "0", "--no-pmc"]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            return {"error": "exit %d: %s" % (r.returncode, r.stderr[-300:])}
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        return {k: d[k] for k in ("value", "unit", "ms_per_step", "steps", "parts_seen", "devices", "kernel_ms")}
+    except Exception as e:   # noqa: BLE001 - reported in the line
+        return {"error": repr(e)[-300:]}
 
 
 def main():
@@ -213,19 +405,35 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 traffic passes")
     ap.add_argument("--no-output", action="store_true", help="time pathTracing+copy only (no screenOutput/gather)")
     ap.add_argument("--check-launch", action="store_true", help="start the ranks, report the world size, render nothing")
-    ap.add_argument("--workload", choices=("dragon", "bunny", "helmet", "sky_dragon"), default="dragon",
+    ap.add_argument("--workload", choices=("dragon", "bunny", "helmet", "sky_dragon", "bunny16"), default="dragon",
                     help="dragon (default): BASELINE.json's metric on the StanfordDragon stand-in; bunny: configs[1]; "
-                         "helmet: configs[2] (real PBR maps); sky_dragon: configs[4] (physical sky + dragon, 4K)")
-    ap.add_argument("--event-every", type=int, default=10, metavar="K",
-                    help="time the kernels with HIP events around every K-th frame of the timed region")
+                         "helmet: configs[2] (real PBR maps); sky_dragon: configs[4] (physical sky + dragon, 4K); "
+                         "bunny16: the StanfordBunny split x16 (485,408 triangles, the scan-like dragon-sized stand-in)")
+    ap.add_argument("--engine", choices=("ranks", "multipart"), default="ranks",
+                    help="ranks (default): one process per GPU, RCCL halos + gather; multipart: one process over a "
+                         "pt_ctx_create_devices context of --gpus parts (the Node host's route; parts share device 0 "
+                         "when fewer GPUs are visible)")
+    ap.add_argument("--devices", default=None, help="multipart: comma-separated device of each part")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="N > 1: strong (default) = one 3840x2160 frame split over the GPUs (BASELINE configs[3]); "
+                         "weak = N x 2.07 MP (1920x1080, 3840x1080, 3840x2160, 7680x2160)")
+    ap.add_argument("--no-anchors", action="store_true",
+                    help="N = 1: skip the 4K, scan-like and converged-run fields beside the headline")
+    ap.add_argument("--no-multipart", action="store_true", help="N > 1: skip the multipart curve beside the RCCL one")
+    ap.add_argument("--event-every", type=int, default=None, metavar="K",
+                    help="time the kernels with HIP events around every K-th frame of the timed region "
+                         "(default: steps // 10, so that about 10 draws are bracketed whatever --steps is)")
     ap.add_argument("--dump-canvas", default=None, metavar="PATH",
                     help="rank 0 saves the last timed frame's RGBA8 canvas (.npy) - e.g. to compare an N-rank "
                          "frame with a one-rank render of the same size")
     ap.add_argument("--size", default=None,
                     help="WxH frame size (e.g. 3840x2160 for the 4K configs); at N > 1 the same frame is split over "
-                         "the GPUs (strong scaling, BASELINE configs[3]: --gpus 8 --size 3840x2160)")
+                         "the GPUs (strong scaling)")
     args = ap.parse_args()
+    event_every = plan(args, 1)["event_every"]
 
+    if args.engine == "multipart":
+        return multipart_main(args, event_every)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return launch_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -250,17 +458,10 @@ def main():
         torch.cuda.set_stream(stream)
 
     import babylon_pt as bp
-    import helpers as H
 
-    meta, mesh_arrays, maps, (W, Hh) = H.workload(args.workload)
-    fixed = args.size is not None or args.workload == "sky_dragon"
-    if args.workload != "sky_dragon":
-        W, Hh = frame_size(world)
-    if args.size:
-        W, Hh = (int(v) for v in args.size.lower().split("x"))
+    p = plan(args, world)
+    W, Hh = p["width"], p["height"]
     engine = bp.Engine(local)
-    mesh = H.texture_payloads(meta, mesh_arrays)
-    program = meta["scene"]
 
     rt_ptrs, acc_t = None, None
     pad_bands = bp.padded_bands(Hh, world)
@@ -272,10 +473,7 @@ def main():
         rt_ptrs = {"pathTracingRenderTarget": acc_t.data_ptr(), "screenCopyRenderTarget": copy_t.data_ptr()}
         stream.synchronize()
         engine.set_stream(stream.cuda_stream)
-    player = bp.StreamPlayer(engine, meta, H.bluenoise(), mesh, W, Hh, rt_ptrs)
-    if maps:
-        for kind, sampler in H.PBR_SAMPLERS.items():
-            player.textures[sampler] = bp.Texture(engine, maps[kind], name=kind)
+    player, program, tris = make_player(engine, args.workload, W, Hh, rt_ptrs)
     engine.resize_canvas(W, Hh)
     engine.set_row_partition(world, rank)
 
@@ -314,25 +512,16 @@ def main():
     for k in range(args.warmup):
         step(k)
     barrier_sync()
-    # kernel durations from HIP event pairs around every --event-every-th frame's draws (an event
+    # kernel durations from HIP event pairs around every event_every-th frame's draws (an event
     # record costs ~5 us of stream time between kernels: bracketing every draw slowed the dragon
     # stand-in's frame by 1.7 %, the bunny's by 3.8 %)
-    os.environ["PT_TIMING_EVERY"] = str(args.event_every)
-    engine.timing_begin()
-    t0 = time.perf_counter()
-    for k in range(args.warmup, args.warmup + args.steps):
-        step(k)
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
+    elapsed, kernel_ms, pt_n = timed_region(engine, step, args.warmup, args.steps, event_every, barrier_sync, program)
     if args.dump_canvas:
         import numpy as np
         if dist is None:
             np.save(args.dump_canvas, engine.read_canvas(W, Hh))
         elif rank == 0:
             np.save(args.dump_canvas, gather.last_frame()[:Hh].cpu().numpy())
-    pt_ms, pt_n = engine.timing_end(program)
-    cp_ms, _ = engine.timing_end("screenCopy")
-    out_ms, _ = engine.timing_end("screenOutput")
 
     ranks_seen = world
     if dist is not None:
@@ -352,19 +541,28 @@ def main():
     layout = engine.bvh_layout_used()
     bytes_per_launch = algorithmic_bytes(cnt) / nc
 
+    anchors = {}
+    if world == 1 and not args.no_anchors and args.workload == "dragon" and args.size is None:
+        anchors = run_anchors(engine, args)
+
     if rank != 0:
+        if not args.no_multipart:
+            # rank 0's multipart curve runs in a child process on these GPUs meanwhile: wait on the
+            # host (the rendezvous store), not in a device-side RCCL barrier that would hold CUs
+            dist.barrier()
+            dist.distributed_c10d._get_default_store().wait(["bench_multipart_done"])
         dist.barrier()
         dist.destroy_process_group()
         return 0
 
     paths = W * Hh * args.steps
     value = paths / elapsed / 1e6
-    avg_launch_ms = max(pt_ms / max(1, pt_n), 1e-9)
+    avg_launch_ms = max(kernel_ms["pathtrace"], 1e-9)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
-    wname = {"bunny": "bunny", "helmet": "helmet_pbr", "dragon": "dragon_standin", "sky_dragon": "dragon_standin"}
+    wname = {"bunny": "bunny", "helmet": "helmet_pbr", "dragon": "dragon_standin", "sky_dragon": "dragon_standin",
+             "bunny16": "bunny_split16"}
     workload = "%s_%s_%dx%d" % (program, wname[args.workload], W, Hh)
-    kernel = "pt_trace<%s%s%s>" % ("PAIRS+" if layout == "pairs" else "", program.upper(),
-                                   "+TEX" if args.workload == "helmet" else "")
+    kernel = kernel_name(layout, program, args.workload)
     traffic, pmc_note = None, "N > 1: not collected"
     if world == 1:
         if args.no_pmc:
@@ -379,8 +577,10 @@ def main():
                 "traffic_source": ("live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over 5 frames of this workload, "
                                    "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 B per launch (gfx950 correction)")
                 if traffic else pmc_note,
-                "kernel": kernel, "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                "kernel": kernel, "bvh_walk": layout, "algorithmic_bytes_per_launch": int(bytes_per_launch),
                 "counts_per_launch": {k: v / nc for k, v in cnt.items()}}
+    ms_per_step = elapsed / args.steps * 1e3
+    ksum = sum(kernel_ms.values())
     line = {
         "metric": baseline_metric() if args.workload == "dragon" else METRICS[args.workload],
         "value": round(value, 2),
@@ -388,29 +588,38 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "strong" if fixed and world > 1 else "weak",
+        "scaling": p["scaling"],
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: " + DATA[args.workload] + "; continued with fresh uRandomVec2 per frame",
         "config": {"workload": workload, "width": W, "height": Hh, "spp_per_frame": 1, "max_bounces": 6,
-                   "triangles": int(mesh_arrays["tri"].shape[0]), "parallelism": "row-bands x%d" % world,
-                   "ranks_seen": ranks_seen,
+                   "triangles": tris, "parallelism": "row-bands x%d" % world, "ranks_seen": ranks_seen,
                    "gather": ("per frame: 2-row halo exchange with band neighbours (RCCL P2P), screenOutput "
                               "of own bands, async RCCL gather of RGBA8 bands to rank 0 overlapping the next "
                               "frame") if world > 1 else None},
         "pathtrace_mpaths_per_s": round(W * Hh / (avg_launch_ms * 1e-3) / 1e6 * world, 2),
-        "kernel_timing": "HIP events around the draws of every %d-th timed frame (%d launches)" % (args.event_every, pt_n),
-        "kernel_ms": {"pathtrace": round(avg_launch_ms, 4), "screen_copy": round(cp_ms / max(1, pt_n), 4),
-                      "screen_output": round(out_ms / max(1, pt_n), 4)},
+        "kernel_timing": "HIP events around the draws of every %d-th timed frame (%d launches)" % (event_every, pt_n),
+        "kernel_ms": kernel_ms,
+        # event windows add their own stream time around the bracketed draws: a sum above the step
+        # time flags sampled kernel times inflated by them
+        "kernel_sum_ms": round(ksum, 4),
+        "kernel_sum_exceeds_step": bool(ksum > ms_per_step),
         "roofline": roofline,
     }
+    line.update(anchors)
     if args.workload == "sky_dragon":
         line["converge_%dspp_s" % CONVERGED_SPP] = round(CONVERGED_SPP * elapsed / args.steps, 3)
         line["converge_note"] = ("%d frames timed; seconds for %d progressive frames = %s"
                                  % (args.steps, CONVERGED_SPP, "measured" if args.steps == CONVERGED_SPP
                                     else "ms_per_step x %d" % CONVERGED_SPP))
+    if world > 1 and not args.no_multipart:
+        dist.barrier()   # every rank's GPU work is done; they wait on the host while the child runs
+        try:
+            line["multipart"] = multipart_child(args, world, W, Hh)
+        finally:
+            dist.distributed_c10d._get_default_store().set("bench_multipart_done", "1")
     if args.cpu_budget > 0:
         line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_budget) if world == 1 else None
     print(json.dumps(line), flush=True)

@@ -222,6 +222,37 @@ def synthetic_dragon(nu=512, nv=512, knot=(1, 1), tube=9.0):
     return {"bvh": bp.bvh_build(aabb_in), "tri": tri, "aabb_in": aabb_in}
 
 
+def subdivided_mesh(m, levels=2):
+    """A model's triangle records split `levels` times at their edge midpoints (x4 per level: the
+    StanfordBunny's 30,338 triangles -> 485,408 at 2 levels, near the 524,288 the 2048^2 triangle
+    texture holds): the same surface - every new vertex lies on its triangle's plane, normals and UVs
+    are the vertices' linear interpolants, windings are kept - with a scan's triangle density, so a
+    BVH over real scanned geometry (depth, overlap) of the dragon's size. Float64 midpoints, float32
+    storage, per-triangle AABBs, native builder (bit-identical to BVH_Fast_Builder.js); the scale-
+    free scan-like counterpart of synthetic_dragon for the bench."""
+    import babylon_pt as bp
+    t = m["tri"].astype(np.float64)
+    n = t.shape[0]
+    pos, nor, uv = t[:, 0:9].reshape(n, 3, 3), t[:, 9:18].reshape(n, 3, 3), t[:, 18:24].reshape(n, 3, 2)
+    for _ in range(levels):
+        def mid(a, i, j):
+            return (a[:, i] + a[:, j]) * 0.5
+        def split(a):
+            ab, bc, ca = mid(a, 0, 1), mid(a, 1, 2), mid(a, 2, 0)
+            return np.stack([np.stack([a[:, 0], ab, ca], 1), np.stack([ab, a[:, 1], bc], 1),
+                             np.stack([ca, bc, a[:, 2]], 1), np.stack([ab, bc, ca], 1)], 1).reshape(-1, 3, a.shape[2])
+        pos, nor, uv = split(pos), split(nor), split(uv)
+    n = pos.shape[0]
+    tri = np.zeros((n, 32), np.float32)
+    tri[:, 0:9] = pos.reshape(n, 9)
+    tri[:, 9:18] = nor.reshape(n, 9)
+    tri[:, 18:24] = uv.reshape(n, 6)
+    p32 = tri[:, 0:9].reshape(n, 3, 3)
+    lo, hi = p32.min(1), p32.max(1)
+    aabb_in = np.concatenate([lo, hi, (lo + hi) * 0.5], 1).astype(np.float32)
+    return {"bvh": bp.bvh_build(aabb_in), "tri": tri, "aabb_in": aabb_in}
+
+
 # BASELINE configs[4]: the physical-sky page's recorded stream (sky_256) with the glTF page's model
 # uniforms and samplers added, i.e. the effect the sky shader + glTF model block composite declares
 # (DESIGN.md §1). Model transform: a 180-degree turn about y (exact +-1 entries), as the glTF page
@@ -287,6 +318,7 @@ WORKLOADS = {
     "bunny": ("gltf_bunny_1080p", None, None, (1920, 1080)),           # configs[1]
     "helmet": ("hdri_helmet_320x180", None, "helmet", (1920, 1080)),   # configs[2]
     "sky_dragon": ("skymesh", "dragon", None, (3840, 2160)),           # configs[4]
+    "bunny16": ("gltf_bunny_1080p", "bunny16", None, (1920, 1080)),    # scan-like dragon-sized stand-in
 }
 
 
@@ -294,7 +326,7 @@ def workload(name):
     """(meta, mesh arrays, maps or None, (W, H)) of a bench workload."""
     key, mesh_kind, maps_kind, size = WORKLOADS[name]
     meta = sky_mesh_stream() if key == "skymesh" else stream(key)
-    m = synthetic_dragon() if mesh_kind == "dragon" else mesh(meta)
+    m = synthetic_dragon() if mesh_kind == "dragon" else subdivided_mesh(mesh(meta)) if mesh_kind == "bunny16" else mesh(meta)
     return meta, m, (helmet_maps() if maps_kind == "helmet" else None), size
 
 

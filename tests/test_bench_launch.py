@@ -49,3 +49,57 @@ def test_cpu_baseline_uses_every_job_cpu_pinned():
     assert r["value"] and r["value"] > 0, r
     assert r["cores"] == len(cpus) == r["job_cpus"] and r["nproc"] == os.cpu_count()
     assert "taskset" in r["sample"] and r["kind"] == "port"
+
+
+def _plan(argv, world):
+    sys.path.insert(0, ROOT)
+    import bench
+    import argparse
+    ap = argparse.ArgumentParser()
+    for a, kw in (("--size", {}), ("--workload", {"default": "dragon"}), ("--scaling", {"default": "strong"}),
+                  ("--steps", {"type": int, "default": 200}), ("--event-every", {"type": int, "default": None})):
+        ap.add_argument(a, **kw)
+    return bench.plan(ap.parse_args(argv), world)
+
+
+def test_plan_headline_and_scaling_configs():
+    """N = 1: the metric's 1080p frame; N > 1 (the driver's `--gpus N`, no other flags): BASELINE
+    configs[3]'s 3840x2160 frame split over the GPUs (strong scaling), the frame the N = 1 line's
+    dragon_4k_1gpu field renders on one GPU; --scaling weak keeps N x 2.07 MP; --size and the sky
+    workload fix the frame."""
+    assert _plan([], 1) == {"width": 1920, "height": 1080, "scaling": "weak", "event_every": 20}
+    for n in (2, 4, 8):
+        p = _plan([], n)
+        assert (p["width"], p["height"], p["scaling"]) == (3840, 2160, "strong")
+    assert (_plan(["--scaling", "weak"], 8)["width"], _plan(["--scaling", "weak"], 8)["height"]) == (7680, 2160)
+    assert _plan(["--scaling", "weak"], 8)["scaling"] == "weak"
+    assert (_plan(["--size", "640x480"], 2)["width"], _plan(["--size", "640x480"], 2)["scaling"]) == (640, "strong")
+    assert (_plan(["--workload", "sky_dragon"], 1)["width"], _plan(["--workload", "sky_dragon"], 1)["height"]) == (3840, 2160)
+
+
+def test_kernel_timing_brackets_about_ten_draws():
+    """HIP-event windows bracket every (steps // 10)-th frame: ~10 draws at the driver's --steps 20
+    as at 200 (round 2 bracketed 2 at --steps 20); --event-every overrides."""
+    for steps, every in ((20, 2), (200, 20), (5, 1), (1000, 100)):
+        p = _plan(["--steps", str(steps)], 1)
+        assert p["event_every"] == every and len(range(0, steps, every)) >= min(steps, 10)
+    assert _plan(["--steps", "20", "--event-every", "7"], 1)["event_every"] == 7
+
+
+def test_gpus_n_check_launch_reports_the_4k_strong_config():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--check-launch", "--steps", "20"], env=_env(),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert (d["width"], d["height"], d["scaling"], d["event_every"], d["ranks_seen"]) == (3840, 2160, "strong", 2, 2)
+
+
+def test_multipart_devices_fall_back_to_device_zero():
+    """--engine multipart: one part per visible GPU, or every part on device 0 when fewer are visible
+    (the one-GPU rehearsal of the multi-device route); --devices fixes them."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import argparse
+    a = argparse.Namespace(devices=None, gpus=3)
+    assert bench.multipart_devices(a) == [0, 0, 0]          # no GPU visible here
+    assert bench.multipart_devices(argparse.Namespace(devices="0,1", gpus=2)) == [0, 1]

@@ -140,3 +140,50 @@ def test_node_multipart_replay_bitexact(tmp_path, devices):
     can = np.fromfile(out + ".canvas.u8", np.uint8).reshape(h, w, 4)
     ref_acc, ref_can, _ = H.oracle_replay(meta, with_output=True)
     _check(ref_acc[-1:], ref_can[-1:], [acc], [can])
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_destroy_right_after_output_without_sync(parts):
+    """pt_ctx_destroy, pt_texture_destroy and pt_render_target_resize sync every part first: a part's
+    queued halo pull or the gather may still read another part's buffers (over the peer link when
+    the devices differ; hipFree waits only for its own device). Destroyed / resized straight after a
+    screenOutput with no sync, then a fresh context renders the stream bit-exactly."""
+    import babylon_pt as bp
+    meta = H.stream("gltf_teapot_320x180")
+    for resize in (False, True):
+        e = bp.Engine(devices=[0] * parts)
+        player = bp.StreamPlayer(e, meta, H.bluenoise(), H.texture_payloads(meta, H.mesh(meta)))
+        e.resize_canvas(player.width, player.height)
+        player.play_frame(0)
+        if resize:
+            player.textures["pathTracingRenderTarget"].resize((160, 90))
+            player.textures["screenCopyRenderTarget"].dispose()
+        e.dispose()
+    e = bp.Engine(devices=[0] * parts)
+    try:
+        got = _replay(e, meta)
+    finally:
+        e.dispose()
+    ref_acc, ref_can, _ = H.oracle_replay(meta, with_output=True)
+    _check(ref_acc, ref_can, *got)
+
+
+def test_multipart_draw_events_opt_in_every_part():
+    """pt_last_render_ms over several parts: its first call turns per-draw events on for every part
+    at once (one failing call, with a message), the next reports the slowest part's draw."""
+    import babylon_pt as bp
+    meta = H.stream("gltf_teapot_320x180")
+    e = bp.Engine(devices=[0, 0, 0])
+    try:
+        player = bp.StreamPlayer(e, meta, H.bluenoise(), H.texture_payloads(meta, H.mesh(meta)), 96, 64)
+        e.resize_canvas(96, 64)
+        player.play_frame(0)
+        e.sync()
+        with pytest.raises(bp.PtError, match="per-draw timing"):
+            e.last_render_ms("gltf")
+        player.play_frame(1)
+        e.sync()
+        assert e.last_render_ms("gltf") > 0.0
+        assert e.last_render_ms("screenOutput") > 0.0
+    finally:
+        e.dispose()
