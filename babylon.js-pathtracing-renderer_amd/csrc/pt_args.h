@@ -40,6 +40,9 @@ constexpr int kTrailMaxDepth = 28;
 constexpr int kTopLevels = 7;
 constexpr unsigned kTopEntries = (2u << kTopLevels) - 1u;   // 255 record copies (64 B), heap order
 
+// the BVH walk of a mesh draw (TraceArgs::bvh_walk; the program variant's thousands digit, pt_device.h)
+enum { WALK_REF = 0, WALK_PAIRS = 1, WALK_TRAIL = 2, WALK_QUAD = 3 };
+
 enum Counter { C_PATHS, C_SEGMENTS, C_NODE, C_LEAF, C_HIT, C_RGBA8, C_OVERFLOW, C_HDR, C_NUM };
 enum ErrBits { E_STACK = 1u };
 
@@ -129,6 +132,10 @@ struct TraceArgs {
                                // every segment reads SGPRs instead of waiting on a load
     uint32_t bvh_pairs_bytes;  // size of the record array (its buffer descriptor)
     uint32_t bvh_top_base;     // PROG_TRAIL: byte offset of the restart jump table (inner-record copies) in it
+    int bvh_walk;              // WALK_REF / _PAIRS / _TRAIL / _QUAD (pt_device.h): the variant the draw takes
+    const float4* bvh_quads;   // PROG_QUAD: the two-level records (192 B per inner node)
+    uint32_t bvh_quads_bytes;
+    uint32_t bvh_quad_root;    // the root's two-level record (byte offset)
     float2* spill;             // megakernel BVH stack levels >= kStackLds: [level][grid lane]
     unsigned spill_stride;
     // longest-first dispatch (megakernel): order[slot] = the 16x16 tile dealt to tile slot `slot`

@@ -44,6 +44,9 @@ hipError_t pt_launch_pairs_pass(int pass, const float4* aabb, long long texels, 
                                 hipStream_t s);
 hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x, int bands,
                                int persist_blocks, hipStream_t s);
+hipError_t pt_launch_quads_build(const float4* aabb, long long texels, const float4* tri, long long tri_texels,
+                                 unsigned nrec, const float* code, const unsigned char* inner, float4* out,
+                                 unsigned n_inner, hipStream_t s);
 hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, unsigned nrec, const unsigned char* inner,
                                 unsigned* parent, unsigned* refs, unsigned* flag, const float4* rec, uint32_t root,
                                 float4* top, hipStream_t s);
@@ -83,6 +86,8 @@ struct DevTex {
     float pairs_root_box[6] = {};
     uint32_t pairs_bytes = 0;   // inner records, then leaf records from pairs_leaf on, then the jump table
     uint32_t pairs_top = 0;     // byte offset of the restart-trail jump table; 0: the tree is not walkable by the trail
+    void* quads_mem = nullptr;  // the two-level records (PT_BVH_QUADS; built with the pairs when that walk is asked for)
+    uint32_t quads_bytes = 0, quads_root = 0;
     const DevTex* pairs_tri = nullptr;
     unsigned long long pairs_gen = ~0ull, pairs_tri_gen = ~0ull;
     bool pairs_ok = false;
@@ -457,8 +462,12 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
     *rc = PT_OK;
     const long long texels = (long long)t->w * t->h;
     if (c->bvh_layout == PT_BVH_REFERENCE || t->kind != TEX_F32 || tri->kind != TEX_F32 || texels > (1ll << 24)) return false;
-    if (t->pairs_gen == t->gen && t->pairs_tri == tri && t->pairs_tri_gen == tri->gen) return t->pairs_ok;
+    const bool want_quads = c->bvh_layout == PT_BVH_QUADS;
+    if (t->pairs_gen == t->gen && t->pairs_tri == tri && t->pairs_tri_gen == tri->gen && (!want_quads || t->quads_mem || !t->pairs_ok))
+        return t->pairs_ok;
     if (t->pairs_mem) { hipStreamSynchronize(c->stream); hipFree(t->pairs_mem); t->pairs_mem = nullptr; }
+    if (t->quads_mem) { hipStreamSynchronize(c->stream); hipFree(t->quads_mem); t->quads_mem = nullptr; }
+    t->quads_bytes = 0;
     t->pairs_ok = false;
     t->pairs_top = 0;
     t->pairs_gen = t->gen; t->pairs_tri = tri; t->pairs_tri_gen = tri->gen;
@@ -528,10 +537,21 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
         const float box6[6] = { node0[1], node0[2], node0[3], node0[5], node0[6], node0[7] };
         std::memcpy(t->pairs_root_box, box6, sizeof(box6));
         t->pairs_bytes = (uint32_t)(top_base + pt::kTopEntries * 64);
-        // the restart trail's jump table, for trees it can walk (one parent per node, depth <= 32)
+        // the restart trail's jump table, for trees it can walk (one parent per node, depth <= 28)
         if (e == hipSuccess && !notrail) {
             e = tpass(3, t->pairs_root);
             if (e == hipSuccess) t->pairs_top = (uint32_t)top_base;
+        }
+        // the two-level records, when that walk is asked for (192 B per inner node + a leaf root's line)
+        const size_t qbytes = n_inner * 192 + 64;
+        if (e == hipSuccess && want_quads && qbytes < (1ull << 31)) {
+            e = hipMalloc(&t->quads_mem, qbytes + 256);
+            if (e == hipSuccess)
+                e = pt_launch_quads_build(aabb, texels, trid, ttex, nrec, code, inner, (float4*)t->quads_mem,
+                                          (unsigned)n_inner, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            t->quads_bytes = (uint32_t)qbytes;
+            t->quads_root = root >= 0.0f ? (uint32_t)root * 192u : pt::kLeafBit | (uint32_t)(n_inner * 192);
         }
     }
     if (scratch) { hipStreamSynchronize(c->stream); hipFree(scratch); }
@@ -602,9 +622,15 @@ int render_trace(DevFx* fx, DevTex* target)
             std::memcpy(a.bvh_root_box, bvh->pairs_root_box, sizeof(a.bvh_root_box));
             a.bvh_pairs_bytes = bvh->pairs_bytes;
             a.bvh_top_base = c->bvh_layout == PT_BVH_TRAIL ? bvh->pairs_top : 0u;
+            if (c->bvh_layout == PT_BVH_QUADS && bvh->quads_mem) {
+                a.bvh_quads = (const float4*)bvh->quads_mem;
+                a.bvh_quads_bytes = bvh->quads_bytes;
+                a.bvh_quad_root = bvh->quads_root;
+            }
         }
         if (prc) return prc;
-        c->bvh_used = a.bvh_top_base ? PT_BVH_TRAIL : a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
+        a.bvh_walk = a.bvh_quads ? pt::WALK_QUAD : a.bvh_top_base ? pt::WALK_TRAIL : a.bvh_pairs ? pt::WALK_PAIRS : pt::WALK_REF;
+        c->bvh_used = a.bvh_quads ? PT_BVH_QUADS : a.bvh_top_base ? PT_BVH_TRAIL : a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
         a.albedo = tex8(sampler(fx, "tAlbedoTexture"));
         a.bump = tex8(sampler(fx, "tBumpTexture"));
         a.metal = tex8(sampler(fx, "tMetallicTexture"));
@@ -868,7 +894,8 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_SPLIT_NEAR")) c->split_near = std::max(1, std::min(128, std::atoi(v)));
     if (const char* v = std::getenv("PT_SPLIT_ALWAYS")) c->split_dominance = std::atoi(v) ? 0u : 8u;
     if (const char* v = std::getenv("PT_BVH_LAYOUT"))   // reference | pairs | trail: the context's initial walk
-        c->bvh_layout = !std::strcmp(v, "trail") ? PT_BVH_TRAIL : !std::strcmp(v, "reference") ? PT_BVH_REFERENCE : PT_BVH_PAIRS;
+        c->bvh_layout = !std::strcmp(v, "trail") ? PT_BVH_TRAIL : !std::strcmp(v, "quads") ? PT_BVH_QUADS
+                      : !std::strcmp(v, "reference") ? PT_BVH_REFERENCE : PT_BVH_PAIRS;
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
@@ -1099,6 +1126,7 @@ void dev_texture_destroy(DevTex* t)
             if (kv.second == t) kv.second = nullptr;
     if (t->d && !t->external) { hipStreamSynchronize(c->stream); hipFree(t->d); }
     if (t->pairs_mem) { hipStreamSynchronize(c->stream); hipFree(t->pairs_mem); }
+    if (t->quads_mem) { hipStreamSynchronize(c->stream); hipFree(t->quads_mem); }
     for (auto* o : c->textures)   // records built against this triangle texture are stale
         if (o->pairs_tri == t) { o->pairs_tri = nullptr; o->pairs_gen = ~0ull; }
     c->textures.erase(t);
@@ -1173,7 +1201,7 @@ int dev_set_backend(Dev* c, int backend)
 
 int dev_set_bvh_layout(Dev* c, int layout)
 {
-    if (!c || (layout != PT_BVH_REFERENCE && layout != PT_BVH_PAIRS && layout != PT_BVH_TRAIL)) return PT_ERR_ARG;
+    if (!c || layout < PT_BVH_REFERENCE || layout > PT_BVH_QUADS) return PT_ERR_ARG;
     c->bvh_layout = layout;
     return PT_OK;
 }

@@ -18,11 +18,12 @@ enum { PROG_CORNELL = 3, PROG_GLTF = 4, PROG_HDRI = 5, PROG_SKY = 6, PROG_QUADRI
 // PROG_*_TEX: the mesh programs instantiated with their PBR / normal-map code (models with an
 // albedo or bump texture); without +PROG_TEX those branches are compiled out.
 enum { PROG_TEX = 100, PROG_GLTF_TEX = 104, PROG_HDRI_TEX = 105, PROG_SKYMESH_TEX = 108 };
-// +PROG_PAIRS: the same programs walking the child-pair BVH records (bvhWalkPairs) instead of the
-// reference's texel pairs (bvhWalkRef); chosen per draw by the host (pt_capi.cpp ensure_pairs).
-// +PROG_TRAIL: the child-pair records walked without a stack beyond an LDS ring (bvhWalkTrail: the
-// restart trail, PT_BVH_TRAIL)
-enum { PROG_PAIRS = 1000, PROG_TRAIL = 2000 };
+// BVH walks (the program variant's thousands digit, chosen per draw by the host, pt_capi.cpp):
+// +PROG_PAIRS the child-pair records (bvhWalkPairs) with the reference's short stack instead of the
+// reference's texel pairs (bvhWalkRef); +PROG_TRAIL the same records without a stack beyond an LDS ring
+// (bvhWalkTrail: the restart trail, PT_BVH_TRAIL); +PROG_QUAD two-level records, one fetch per two
+// tree levels (bvhWalkQuads, PT_BVH_QUADS)
+enum { PROG_PAIRS = 1000, PROG_TRAIL = 2000, PROG_QUAD = 3000 };   // = WALK_* (pt_args.h) x 1000
 template <int P> constexpr int kBase = P % PROG_PAIRS;
 template <int P> constexpr int kScene = kBase<P> % PROG_TEX;
 // the programs whose SceneIntersect walks the glTF model's BVH: glTF, HDRI and the physical-sky
@@ -38,24 +39,27 @@ template <int P> constexpr bool kIsQuadric = P == PROG_QUADRIC;
 // hitObjectID layout: spheres 0-1 (quadric: shapes 0-11), then the quads, then the mesh
 // (objectCount after the quads: 8 in the glTF scene, 6 in the HDRI scene and the sky composite)
 template <int P> constexpr int kQuadId0 = kIsQuadric<P> ? 12 : 2;
-template <int P> constexpr bool kPairs = P >= PROG_PAIRS;   // child-pair records (stack or trail walk)
-template <int P> constexpr bool kTrail = P >= PROG_TRAIL;
-// every instantiated program variant
-#define PT_FOR_EACH_PROG(X)                                                                           \
+template <int P> constexpr int kWalk = P / PROG_PAIRS;
+template <int P> constexpr bool kPairs = P >= PROG_PAIRS;   // child-pair records (any walk but the reference's)
+template <int P> constexpr bool kTrail = kWalk<P> == WALK_TRAIL;
+template <int P> constexpr bool kQuad = kWalk<P> == WALK_QUAD;
+// every instantiated program variant, by BVH walk (one translation unit each: pt_trace_walk*.hip)
+#define PT_FOR_EACH_PROG_REF(X)                                                                                           \
     X(PROG_CORNELL) X(PROG_SKY) X(PROG_QUADRIC) X(PROG_GLTF) X(PROG_GLTF_TEX) X(PROG_HDRI) X(PROG_HDRI_TEX)           \
-    X(PROG_SKYMESH) X(PROG_SKYMESH_TEX)                                                                                 \
-    X(PROG_PAIRS + PROG_GLTF) X(PROG_PAIRS + PROG_GLTF_TEX) X(PROG_PAIRS + PROG_HDRI) X(PROG_PAIRS + PROG_HDRI_TEX)     \
-    X(PROG_PAIRS + PROG_SKYMESH) X(PROG_PAIRS + PROG_SKYMESH_TEX)                                                     \
-    X(PROG_TRAIL + PROG_GLTF) X(PROG_TRAIL + PROG_GLTF_TEX) X(PROG_TRAIL + PROG_HDRI) X(PROG_TRAIL + PROG_HDRI_TEX)     \
-    X(PROG_TRAIL + PROG_SKYMESH) X(PROG_TRAIL + PROG_SKYMESH_TEX)
+    X(PROG_SKYMESH) X(PROG_SKYMESH_TEX)
+#define PT_FOR_EACH_MESH_PROG(X, W)                                                                                       \
+    X(W + PROG_GLTF) X(W + PROG_GLTF_TEX) X(W + PROG_HDRI) X(W + PROG_HDRI_TEX) X(W + PROG_SKYMESH) X(W + PROG_SKYMESH_TEX)
+#define PT_FOR_EACH_PROG_PAIRS(X) PT_FOR_EACH_MESH_PROG(X, PROG_PAIRS)
+#define PT_FOR_EACH_PROG_TRAIL(X) PT_FOR_EACH_MESH_PROG(X, PROG_TRAIL)
+#define PT_FOR_EACH_PROG_QUAD(X) PT_FOR_EACH_MESH_PROG(X, PROG_QUAD)
+#define PT_FOR_EACH_PROG(X) PT_FOR_EACH_PROG_REF(X) PT_FOR_EACH_PROG_PAIRS(X) PT_FOR_EACH_PROG_TRAIL(X) PT_FOR_EACH_PROG_QUAD(X)
 
 // the kernel variant of a draw: the scene program, +PROG_TEX when the model carries albedo / bump
-// maps, +PROG_PAIRS when the BVH walk uses child-pair records with the short stack, +PROG_TRAIL when
-// it walks them with the restart trail
-__host__ __device__ inline int resolveProgram(int prog, bool textured, bool pairs, bool trail = false)
+// maps, + the walk's thousands for the mesh programs
+__host__ __device__ inline int resolveProgram(int prog, bool textured, int walk)
 {
     if (prog != PROG_GLTF && prog != PROG_HDRI && prog != PROG_SKYMESH) return prog;
-    return prog + (textured ? PROG_TEX : 0) + (pairs ? (trail ? PROG_TRAIL : PROG_PAIRS) : 0);
+    return prog + (textured ? PROG_TEX : 0) + walk * PROG_PAIRS;
 }
 // waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 64 -> 8). Measured
 // with one-wave workgroups after the walk's branch-free stack (round 2): the child-pair walk at 8
@@ -69,9 +73,17 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, bool pair
 #ifndef PT_MINWAVES_PAIRS
 #define PT_MINWAVES_PAIRS 8
 #endif
-template <int P> constexpr int kMinWaves = kHasTex<P> ? PT_MINWAVES_TEX : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
+// the two-level walk holds three record lines (48 floats) live: fewer waves
+#ifndef PT_MINWAVES_QUAD
+#define PT_MINWAVES_QUAD 5
+#endif
+#ifndef PT_MINWAVES_QUAD_TEX
+#define PT_MINWAVES_QUAD_TEX 3
+#endif
+template <int P> constexpr int kMinWaves = kQuad<P> ? (kHasTex<P> ? PT_MINWAVES_QUAD_TEX : PT_MINWAVES_QUAD)
+                                         : kHasTex<P> ? PT_MINWAVES_TEX : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
 // BVH stack levels in LDS per lane (the rest in the global slab): fewer for the 8-wave variants
-template <int P> constexpr int kStackLdsOf = (kPairs<P> && !kHasTex<P>) ? PT_STACK_LDS_PAIRS : kStackLds;
+template <int P> constexpr int kStackLdsOf = (kPairs<P> && !kHasTex<P> && !kQuad<P>) ? PT_STACK_LDS_PAIRS : kStackLds;
 // the restart-trail walk's LDS ring (entries per lane): the LDS of the stack walk's levels and its
 // scratch level at 8 waves/SIMD (6 x 8 B + the 32-B G-buffer = 80 B per lane = 160 KB per CU); at 4
 // waves/SIMD the textured variants have room for 14
@@ -563,6 +575,111 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     if (w.lookup) { r.triID = w.triID; r.triU = w.triU; r.triV = w.triV; r.lookup = true; }
 }
 
+// ------------------------------------------------------------------------------ two-level records
+// PT_BVH_QUADS: one fetch per two tree levels. An inner node n's record (192 B, three 64-B lines) is
+//   line 0  n's child-pair line: A.box, B.box, codeA, codeB (A = n + 1, B = its right link)
+//   line 1  A's own line: A's child-pair line (A inner: A1.box, A2.box, codes) or A's leaf triangle
+//           (v0, e1 = v1 - v0, e2 = v2 - v0, idObject)
+//   line 2  the same for B
+// Codes: an inner node's record offset (innerRank * 192), or kLeafBit | the offset of the leaf's line
+// inside its parent's record. A step loads the three lines together, tests n's children (the
+// reference's step at n), and goes on at once with the child it takes, whose line it already holds
+// (the reference's next step): its children's boxes, or its triangle. The next fetch is that child's
+// near child's record - half the dependent round trips of the child-pair walk, with the same
+// comparisons in the same order, so the same hit and the same reference-priced counts.
+struct QuadWalk {
+    uint32_t code;
+    float hitT;
+    float triID, triU, triV;
+    int sp;
+    bool pop, lookup;
+};
+PT_D void quadLeaf(float4 l0, float4 l1, float4 l2, f3 O, f3 D, bool dbl, QuadWalk& w, BvhResult& r)
+{
+    r.leaves++;
+    float tu, tv;
+    const float d = bvhTriangleE(mk(l0.x, l0.y, l0.z), mk(l0.w, l1.x, l1.y), mk(l1.z, l1.w, l2.x), O, D, tu, tv, dbl);
+    if (d < w.hitT) { w.hitT = d; w.triID = 8.0f * l2.y; w.triU = tu; w.triV = tv; w.lookup = true; }
+}
+// one inner node's children from its line (the reference's inner step): false = neither is hit (pop)
+template <class Stk>
+PT_D bool quadInner(const TraceArgs& a, float4 l0, float4 l1, float4 l2, float2 l3, f3 O, f3 inv, bool fast, Stk& st,
+                    QuadWalk& w, BvhResult& r, uint32_t& next)
+{
+    r.nodes += 2;
+    float tA, tB;
+    if (fast) {
+        tA = boxFast(mk(l0.x, l0.y, l0.z), mk(l0.w, l1.x, l1.y), O, inv);
+        tB = boxFast(mk(l1.z, l1.w, l2.x), mk(l2.y, l2.z, l2.w), O, inv);
+    } else {
+        tA = box(mk(l0.x, l0.y, l0.z), mk(l0.w, l1.x, l1.y), O, inv);
+        tB = box(mk(l1.z, l1.w, l2.x), mk(l2.y, l2.z, l2.w), O, inv);
+    }
+    const bool sw = tB < tA;
+    const float tN = sw ? tB : tA, tF = sw ? tA : tB;
+    const float cN = sw ? l3.y : l3.x, cF = sw ? l3.x : l3.y;
+    const bool hitN = tN < w.hitT, hitF = tF < w.hitT;
+    if (hitN && hitF) { stackPush(a, st, w.sp, make_float2(tF, cF), r.ovf); w.sp++; }
+    next = __float_as_uint(hitN ? cN : cF);
+    return hitN || hitF;
+}
+template <class Stk>
+PT_D bool quadWalkStep(const TraceArgs& a, __amdgpu_buffer_rsrc_t rec, f3 O, f3 D, f3 inv, bool dbl, bool fast, Stk& st,
+                       QuadWalk& w, BvhResult& r)
+{
+    if (w.pop) {
+        w.sp--;
+        if (w.sp < 0) return false;
+        const float2 e = stackPop(st, w.sp, make_float2(kINF, 0.0f));
+        if (e.x >= w.hitT) return true;
+        w.code = __float_as_uint(e.y);
+        r.nodes++;
+    }
+    w.pop = true;
+    const uint32_t off = w.code & ~kLeafBit;
+    const float4 n0 = ldRec4(rec, off), n1 = ldRec4(rec, off + 16u), n2 = ldRec4(rec, off + 32u);
+    const float2 n3 = ldRec2(rec, off + 48u);
+    if (w.code & kLeafBit) {   // a popped leaf: its line in its parent's record
+        quadLeaf(n0, n1, n2, O, D, dbl, w, r);
+        return true;
+    }
+    const float4 a0 = ldRec4(rec, off + 64u), a1 = ldRec4(rec, off + 80u), a2 = ldRec4(rec, off + 96u);
+    const float2 a3 = ldRec2(rec, off + 112u);
+    const float4 b0 = ldRec4(rec, off + 128u), b1 = ldRec4(rec, off + 144u), b2 = ldRec4(rec, off + 160u);
+    const float2 b3 = ldRec2(rec, off + 176u);
+    uint32_t x;
+    if (!quadInner(a, n0, n1, n2, n3, O, inv, fast, st, w, r, x)) return true;
+    // the child taken: its line is line 1 (A) or line 2 (B)
+    const bool isB = x == __float_as_uint(n3.y);
+    const float4 x0 = isB ? b0 : a0, x1 = isB ? b1 : a1, x2 = isB ? b2 : a2;
+    const float2 x3 = isB ? b3 : a3;
+    if (x & kLeafBit) { quadLeaf(x0, x1, x2, O, D, dbl, w, r); return true; }
+    uint32_t y;
+    if (!quadInner(a, x0, x1, x2, x3, O, inv, fast, st, w, r, y)) return true;
+    w.code = y;
+    w.pop = false;
+    return true;
+}
+template <class Stk>
+PT_D void bvhWalkQuads(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float curT, float& hitT, Stk& st, BvhResult& r)
+{
+    QuadWalk w;
+    w.code = a.bvh_quad_root; w.hitT = hitT; w.sp = 0;
+    w.pop = !(curT < hitT);
+    w.lookup = false;
+    w.triID = 0.0f; w.triU = 0.0f; w.triV = 0.0f;
+    const bool fast = pairWalkFast(O, inv);
+    const __amdgpu_buffer_rsrc_t rec = uniformRsrc(a.bvh_quads, a.bvh_quads_bytes);
+#ifdef PT_SECPROF
+    r.steps = 0;
+    while (quadWalkStep(a, rec, O, D, inv, dbl, fast, st, w, r)) r.steps++;
+#else
+    while (quadWalkStep(a, rec, O, D, inv, dbl, fast, st, w, r)) {}
+#endif
+    hitT = w.hitT;
+    if (w.lookup) { r.triID = w.triID; r.triU = w.triU; r.triV = w.triV; r.lookup = true; }
+}
+
 // ------------------------------------------------------------------------------ restart-trail walk
 // The child-pair records walked without a stack in memory (PT_BVH_TRAIL; north_star's "stackless
 // BVH traversal"): the ordered near-first walk of js/GLTFModelPathTracing_FragmentShader.js:211-298
@@ -637,35 +754,40 @@ PT_D bool trailWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 in
             tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
         }
         const uint32_t bk = w.lvl >> 1;
-        // the reference step (the near child next if hit, else the far one; the far one pushed when
-        // both are hit) and a restart descent's step (the child the dir bit names; the sibling pushed
-        // if the level is pending; at the popped level its far child, culled against hitT) share one
-        // form: take child B or A, push the other
-        const bool rs = w.restart;
-        const bool sw = tB < tA;   // the reference's swap: B is the near child
-        const bool hitN = (sw ? tB : tA) < w.hitT, hitF = (sw ? tA : tB) < w.hitT;
-        const bool target = rs && (w.trail & (0u - w.trail)) == bk;   // the popped level
-        const bool takeB = rs ? (w.dir & bk) != 0u : (hitN ? sw : !sw);
-        const bool push = rs ? !target && !(w.trail & bk) : hitN && hitF;
-        if (rs ? target && !((takeB ? tB : tA) < w.hitT) : !hitN && !hitF) {   // culled pop / no child hit
-            if (rs) w.lvl = bk;
-            w.restart = false;
-            w.pop = true;
-            return true;
-        }
-        r.nodes += rs ? (target ? 1u : 0u) : 2u;
-        if (target) w.restart = false;
-        if (!rs) {
+        bool push;
+        float pt, pc, next;
+        if (w.restart) {   // a restart descent: the child the dir bit names
+            const bool takeB = (w.dir & bk) != 0u;
+            const bool target = (w.trail & (0u - w.trail)) == bk;   // the popped level: its far child
+            const float t = (target == takeB) ? tB : tA;            // else the pending sibling's box
+            next = takeB ? r3.y : r3.x;
+            pt = t; pc = takeB ? r3.x : r3.y;
+            push = !target && !(w.trail & bk);
+            if (target) {
+                w.restart = false;
+                if (!(t < w.hitT)) { w.lvl = bk; w.pop = true; return true; }   // culled pop
+                r.nodes++;
+            }
+        } else {   // the reference's step
+            r.nodes += 2;
+            const bool sw = tB < tA;   // the reference's swap: B is the near child
+            const float tF = sw ? tA : tB;
+            const bool hitN = (sw ? tB : tA) < w.hitT, hitF = tF < w.hitT;
+            if (!hitN && !hitF) { w.pop = true; return true; }
+            push = hitN && hitF;
+            pt = tF; pc = sw ? r3.x : r3.y;
             if (!push) w.trail |= bk;
+            const bool takeB = hitN ? sw : !sw;
             w.dir = takeB ? (w.dir | bk) : (w.dir & ~bk);
+            next = takeB ? r3.y : r3.x;
         }
         if (push) {
-            const vf2 v = { takeB ? tA : tB, takeB ? r3.x : r3.y };
+            const vf2 v = { pt, pc };
             ring[(unsigned)w.rtop * stride + slot] = v;
             w.rtop = w.rtop == R - 1 ? 0 : w.rtop + 1;
             w.rcnt = min(w.rcnt + 1, R);
         }
-        w.code = __float_as_uint(takeB ? r3.y : r3.x);
+        w.code = __float_as_uint(next);
         w.lvl = bk;
         return true;
     }

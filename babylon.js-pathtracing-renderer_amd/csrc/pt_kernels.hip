@@ -27,6 +27,7 @@
 #include "pt_device.h"
 #include "pt_glsl.h"
 #include "pt_program.h"
+#include "pt_trace.h"
 #ifdef PT_SECPROF
 #define PT_SECPROF_ON 1
 #else
@@ -36,159 +37,7 @@
 using namespace ptg;
 
 namespace pt {
-
-// LS = lanes of the block = the stride of one stack level in LDS; NL = stack levels in LDS
-template <int LS, int NL>
-struct MegaStack {
-    lds_float2* lds;
-    unsigned slot;
-    glb_float2* slab;     // the spill slab (wave-uniform base) ...
-    unsigned deep;        // ... and this lane's index in it: level NL, levels `stride` apart
-    unsigned stride;      //     (32-bit: a 64-bit per-lane pointer costs two VGPRs for the whole path)
-#ifdef PT_SECPROF
-    mutable unsigned n_get = 0, n_get_slab = 0, n_put = 0, n_put_slab = 0;
-#define PT_SLABCOUNT(x) x
-#else
-#define PT_SLABCOUNT(x)
-#endif
-    // the common case without branches: every lane reads LDS level min(si, NL - 1); lanes
-    // deeper than the LDS levels then read the slab (or get the sentinel)
-    PT_D float2 pop(int si, float2 sentinel) const
-    {
-        PT_SLABCOUNT(n_get++; if (si >= NL) n_get_slab++;)
-        vf2 e = lds[(unsigned)min(si, NL - 1) * LS + slot];
-        if (si >= NL) {
-            const vf2 s = { sentinel.x, sentinel.y };
-            e = si < kStackLevels ? slab[(unsigned)(si - NL) * stride + deep] : s;
-        }
-        return make_float2(e.x, e.y);
-    }
-    // every lane writes LDS level min(si, NL): level NL is a scratch level that takes
-    // the deeper lanes' store, which then also goes to the slab (false beyond stackLevels[27])
-    PT_D bool push(int si, float2 e)
-    {
-        const vf2 v = { e.x, e.y };
-        PT_SLABCOUNT(n_put++; if (si >= NL) n_put_slab++;)
-        lds[(unsigned)min(si, NL) * LS + slot] = v;
-        if (si >= NL) {
-            if (si >= kStackLevels) return false;
-            slab[(unsigned)(si - NL) * stride + deep] = v;
-        }
-        return true;
-    }
-};
-
-// the mesh hit's attributes (js/GLTFModelPathTracing_FragmentShader.js:300-346): interpolated
-// normal and uv from the triangle texels 2-5, optional bump map, model transform
-template <int PROG, bool COUNT>
-PT_D void meshHit(const TraceArgs& a, float triID, float triU, float triV, Hit& h, Cnt& cnt)
-{
-    float4 v2 = fetch32(a.tri, a.tri_texels, triID + 2.0f), v3 = fetch32(a.tri, a.tri_texels, triID + 3.0f),
-           v4 = fetch32(a.tri, a.tri_texels, triID + 4.0f), v5 = fetch32(a.tri, a.tri_texels, triID + 5.0f);
-    if (COUNT) cnt.hit++;
-    float triW = 1.0f - triU - triV;
-    f3 nn = normalize(mk(v2.y, v2.z, v2.w) * triW + mk(v3.x, v3.y, v3.z) * triU + mk(v3.w, v4.x, v4.y) * triV);
-    h.u = triW * v4.z + triU * v5.x + triV * v5.z;
-    h.v = triW * v4.w + triU * v5.y + triV * v5.w;
-    if (kHasTex<PROG> && a.uses_bump) {   // perturbNormal(n, vec2(1), uv), js/GLTFModelPathTracing_FragmentShader.js:72-92
-        f3 S = onb_u(nn);
-        f3 T = cross(nn, S);
-        f3 N = normalize(nn);
-        if (dot(cross(S, T), N) < 0.0f) { S = S * -1.0f; T = T * -1.0f; }
-        float tx[4];
-        texBilinear(a.bump, h.u, h.v, tx);
-        if (COUNT) cnt.tap += 4;
-        f3 mN = normalize(mk(tx[0] * 2.0f - 1.0f, tx[1] * 2.0f - 1.0f, tx[2] * 2.0f - 1.0f));
-        mN.x *= 1.0f; mN.y *= 1.0f;
-        nn = normalize(S * mN.x + T * mN.y + N * mN.z);
-    }
-    h.normal = normalize(mul3t(a.model, nn));
-    h.type = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
-    h.color = mk(1.0f, 1.0f, 1.0f);
-    h.id = meshObjectId<PROG>(a);
-}
-
-// SceneIntersect: js/BabylonPathTracing_FragmentShader.js:47-112 (Cornell),
-// js/TransformedQuadricGeometry_FragmentShader.js:77-317 (quadrics) and
-// js/GLTFModelPathTracing_FragmentShader.js:116-346 (glTF, with the BVH walk)
-template <int PROG, bool COUNT, int LS>
-PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* lds, unsigned lane_slot,
-                         unsigned deep, Cnt& cnt)
-{
-    if (COUNT) cnt.seg++;
-    // the analytic winner's t, id and object-space normal; its other attributes are resolved after
-    // the walk, and only if the mesh does not win (meshHit sets them all): fewer values live across
-    // the walk, same results
-    f3 sn;
-    PT_SEC(cnt, 4);
-    analyticNearest<PROG>(a, rayO, rayD, h, sn);
-    PT_SEC(cnt, 1);
-    if (!kHasMesh<PROG>) { analyticAttributes<PROG>(a, h, sn); PT_SEC(cnt, 3); return; }
-
-    // ---- BVH walk (js/GLTFModelPathTracing_FragmentShader.js:201-298), pt_device.h
-    f3 O = mul(a.model, rayO, 1.0f), D = mul(a.model, rayD, 0.0f);
-    f3 inv = mk(grcp(D.x), grcp(D.y), grcp(D.z));
-    const bool dbl = (!a.uses_albedo && a.model_mat == TRANSPARENT);
-    BvhResult br = { 0.0f, 0.0f, 0.0f, false, 1u, 0u, 0u };
-    MegaStack<LS, kStackLdsOf<PROG>> st{ (lds_float2*)lds, lane_slot, (glb_float2*)a.spill, deep, a.spill_stride };
-    if (kPairs<PROG>) {   // the root's box from the kernel arguments (the same floats as texels 0-1)
-        const float* rb = a.bvh_root_box;
-        const float rootT = box(mk(rb[0], rb[1], rb[2]), mk(rb[3], rb[4], rb[5]), O, inv);
-        auto walk = [&]() {
-            if (kTrail<PROG>) bvhWalkTrail<kRingOf<PROG>>(a, O, D, inv, dbl, rootT, h.t, (lds_float2*)lds, LS, lane_slot, br);
-            else bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
-        };
-#ifdef PT_SECPROF
-        if (cnt.sec) {
-            const int ln_ = __lane_id();
-            if (ln_ == __builtin_amdgcn_readfirstlane(ln_)) cnt.sec[9] = 0;
-            walk();
-            atomicMax(&cnt.sec[9], (unsigned long long)br.steps);
-            cnt.lane_steps += br.steps;
-            if (ln_ == __builtin_amdgcn_readfirstlane(ln_)) cnt.sec[10] += cnt.sec[9];
-        } else
-#endif
-        walk();
-    } else {
-        float4 c0 = fetch32(a.aabb, a.aabb_texels, 0.0f), c1 = fetch32(a.aabb, a.aabb_texels, 1.0f);
-        const float rootT = box(mk(c0.y, c0.z, c0.w), mk(c1.y, c1.z, c1.w), O, inv);
-        bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, h.t, st, br);
-    }
-    if (COUNT) { cnt.node += br.nodes; cnt.leaf += br.leaves; cnt.ovf += br.ovf; }
-#ifdef PT_SECPROF
-    if (COUNT) { cnt.sget += st.n_get; cnt.sget_slab += st.n_get_slab + br.restarts; cnt.sput += st.n_put; cnt.sput_slab += st.n_put_slab; }
-#endif
-    PT_SEC(cnt, 2);
-    if (br.lookup) meshHit<PROG, COUNT>(a, br.triID, br.triU, br.triV, h, cnt);
-    else analyticAttributes<PROG>(a, h, sn);
-    PT_SEC(cnt, 3);
-}
-
-// One iteration of CalculateRadiance's loop: SceneIntersect, then the shading step
-template <int PROG, bool COUNT, int LS, class G>
-PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, float2* lds, unsigned lane_slot,
-                     unsigned deep, Cnt& cnt)
-{
-    Hit h;
-    sceneIntersect<PROG, COUNT, LS>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt);
-    return shadeStep<PROG, COUNT, G>(a, p, s, g, accum, h, cnt);
-}
-
-template <int PROG, bool COUNT, int LS, class G>
-PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_slot, unsigned deep, Cnt& cnt)
-{
-    PState s;
-    pathBegin(s, g);
-    f3 accum = mk(0, 0, 0);
-#pragma unroll 1
-    while (bounceStep<PROG, COUNT, LS, G>(a, p, s, g, accum, lds, lane_slot, deep, cnt)) {}
-    return max3s(accum, 0.0f);
-}
-
-PT_D float xorq(float v, int m) { return __shfl_xor(v, m, 64); }
-
 // longest-first dispatch: wave durations (shader clock) in 8 log-scale buckets per octave
-constexpr int kCostBuckets = 128;
 PT_D int costBucket(unsigned dur)
 {
     const float l = __log2f((float)dur + 1.0f);   // scheduling only, never in the image
@@ -314,284 +163,6 @@ __global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const un
 {
     orderBuild(ntiles, cost, order, split, split_cap, dominance, near_buckets);
 }
-
-// Workgroups of kTraceBlock lanes. At one wave per workgroup (64, the default) every 8x8 wave tile
-// is its own workgroup: a wave that finishes frees its LDS (stack + G-buffer, 5.5 KB) at once,
-// instead of holding a 4-wave workgroup's 22.5 KB until the slowest of the four (sky next to
-// mesh) is done - LDS is what caps residency at 7 waves/SIMD.
-#ifndef PT_TRACE_BLOCK
-#define PT_TRACE_BLOCK 64
-#endif
-constexpr int kTraceBlock = PT_TRACE_BLOCK;
-#ifndef PT_TILE_GROUPS
-#define PT_TILE_GROUPS 1
-#endif
-constexpr int kTraceSub = 4 / (kTraceBlock / 64);   // workgroups per 16x16 tile
-static_assert(kTraceBlock == 64 || kTraceBlock == 256, "trace workgroups are one wave or one 16x16 tile");
-
-template <int PROG, bool COUNT>
-__global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
-{
-    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];   // stack levels + the scratch level, or the trail walk's ring
-    __shared__ float lds_gout[8 * kTraceBlock];
-    const unsigned tid = threadIdx.x;
-    const int lane = tid & 63;
-    const unsigned long long t_start = clock64();
-#ifdef PT_SECPROF
-    const unsigned long long w0_ = wall_clock64();
-#endif
-    // the 8x8 wave tile of this wave inside its 16x16 tile (grid = tiles_x * kTraceSub x bands)
-    int wave, tx, part = -1;
-    unsigned bY, costIdx = ~0u;
-    if (kTraceSub == 4 && PT_TILE_GROUPS) {
-        // launch slots in runs of 32 workgroups = 8 tiles x 4 quadrants, quadrant-major: the
-        // quadrants of one tile are workgroups 8 apart, which the dispatcher deals to the same XCD
-        // (one L2), while the runs' tiles still go round-robin over the XCDs (a short last run keeps
-        // the map a bijection). The tiles come in longest-first order (the previous frame's costs,
-        // pt_order_build) when a.order is set, else row-major.
-        // Split tiles: the K = *a.split slowest tiles come first, each as 16 waves of 16 lanes
-        // (runs of 128 workgroups = 8 tiles x 16 parts, again 8 apart per tile). A wave ends with
-        // its slowest lane of each bounce; a 4x4 block waits on fewer of them than an 8x8 one, so
-        // the kernel's critical path (the slowest tiles' waves, which start first and end last when
-        // a few tiles dominate, as the helmet's do) shortens. Which lane shades which pixel never
-        // changes what a pixel computes: same bits.
-        const unsigned tiles_x = gridDim.x / 4u, ntiles = a.ntiles;
-        const unsigned K = (a.order && a.split) ? *a.split : 0u;   // chosen by pt_order_build
-        const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
-        unsigned slot;
-        if (L < 16u * K) {
-            const unsigned g = L >> 7, r = L & 127u;
-            slot = g * 8u + (r & 7u);
-            wave = (int)(r >> 5);
-            part = (int)((r >> 3) & 3u);
-        } else {
-            const unsigned L2 = L - 16u * K;
-            if (L2 >= 4u * (ntiles - K)) return;   // the grid's padding
-            const unsigned g = L2 >> 5, r = L2 & 31u;
-            const unsigned T = min(8u, ntiles - K - g * 8u);
-            slot = K + g * 8u + r % T;
-            wave = (int)(r / T);
-        }
-        const unsigned tile = a.order ? a.order[slot] : slot;
-        if (slot < a.prio_tiles) __builtin_amdgcn_s_setprio(3);   // the critical path: issue first
-        tx = (int)(tile % tiles_x);
-        bY = tile / tiles_x;
-        costIdx = tile * 4u + (unsigned)wave;
-    } else if (kTraceSub == 1) {
-        wave = (int)(tid >> 6);
-        tx = (int)blockIdx.x;
-        bY = blockIdx.y;
-    } else {
-        wave = (int)(blockIdx.x & 3u);
-        tx = (int)(blockIdx.x >> 2);
-        bY = blockIdx.y;
-    }
-    // lane bits (x0, y0, x1, x2, y1, y2) of an 8x8 block, or (x0, y0, x1, y1) of a split tile's 4x4
-    const int lx = part < 0 ? (lane & 1) | ((lane >> 1) & 6) : (part & 1) * 4 + ((lane & 1) | ((lane >> 1) & 2));
-    const int ly = part < 0 ? ((lane >> 1) & 1) | ((lane >> 3) & 6) : (part >> 1) * 4 + (((lane >> 1) & 1) | ((lane >> 2) & 2));
-    const int band = (int)bY * a.num_parts + a.part;            // global 16-row band of this block
-    const int px = tx * kTile + (wave & 1) * 8 + lx;
-    const int py = band * kTile + (wave >> 1) * 8 + ly;
-    // stack levels >= kStackLds: a global slab [level][lane of the grid] (a private array would be
-    // scratch, which the runtime reserves for every resident wave)
-    const unsigned deep = (blockIdx.y * gridDim.x + blockIdx.x) * kTraceBlock + tid;
-
-    // lanes whose whole 2x2 quad lies beyond the (even-rounded) target do no work; quad helpers
-    // that only complete a quad at an odd edge are shaded like GL helper invocations
-    const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1) && (part < 0 || lane < 16);
-    Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
-#ifdef PT_SECPROF
-    __shared__ unsigned long long lds_sec[16];
-    if (tid < 16) lds_sec[tid] = tid == 8 ? clock64() : 0ull;
-    cnt.sec = lds_sec;
-    cnt.lane_steps = 0;
-    cnt.sget = cnt.sget_slab = cnt.sput = cnt.sput_slab = 0;
-#endif
-    GOutLds<kTraceBlock> gl{ (lds_float*)lds_gout, tid };
-    gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
-    f3 r = mk(0, 0, 0);
-    if (active) {
-        Path p;
-        cameraRay(a, px, py, p);
-        PT_SEC(cnt, 0);
-        r = radiance<PROG, COUNT, kTraceBlock>(a, p, gl, lds_stack, tid, deep, cnt);
-    }
-    PT_SEC(cnt, 4);
-    const GOut g = gl.load();
-
-    // ---- 2x2 fine derivatives (js/PathTracingCommon.js:1306-1320): partner lanes ^1 (x) and ^2 (y)
-    const bool xodd = lane & 1, yodd = lane & 2;
-    auto ddx = [&](float v) { float o = xorq(v, 1); return xodd ? v - o : o - v; };
-    auto ddy = [&](float v) { float o = xorq(v, 2); return yodd ? v - o : o - v; };
-    float dNx = fabsf(ddx(g.nrm.x)) + fabsf(ddy(g.nrm.x));
-    float dNy = fabsf(ddx(g.nrm.y)) + fabsf(ddy(g.nrm.y));
-    float dNz = fabsf(ddx(g.nrm.z)) + fabsf(ddy(g.nrm.z));
-    float normalDiff = gsmoothstep(0.2f, 0.6f, dNx) + gsmoothstep(0.2f, 0.6f, dNy) + gsmoothstep(0.2f, 0.6f, dNz);
-    float dObj = fabsf(ddx(g.id)) > 0.0f ? 1.0f : 0.0f;
-    dObj += fabsf(ddy(g.id)) > 0.0f ? 1.0f : 0.0f;
-    float objectDiff = gsmoothstep(0.0f, 0.5f, dObj);
-    f3 dcx = mk(ddx(g.col.x), ddx(g.col.y), ddx(g.col.z));
-    f3 dcy = mk(ddy(g.col.x), ddy(g.col.y), ddy(g.col.z));
-    float dCol = length(dcx) > 0.0f ? 1.0f : 0.0f;
-    dCol += length(dcy) > 0.0f ? 1.0f : 0.0f;
-    float colorDiff = gsmoothstep(0.0f, 0.5f, dCol);
-
-#ifdef PT_SECPROF
-    if (!COUNT && a.wave_log) {   // wave timeline in wall-clock ticks (100 MHz), one slot per workgroup
-        atomicMax(&lds_sec[11], (unsigned long long)cnt.lane_steps);
-        if (tid == 0) {
-            const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
-            unsigned long long* wl = a.wave_log + (size_t)kWaveLogSlots * L;
-            wl[0] = w0_;
-            wl[1] = wall_clock64();
-            wl[2] = lds_sec[10];
-            wl[3] = lds_sec[11];
-            for (int k = 0; k < 8; k++) wl[4 + k] = lds_sec[k];   // section cycle sums (shader clock)
-        }
-    }
-    if (COUNT && active) {   // stack traffic: pops beyond the LDS levels, pushes beyond; node fetches, leaf tests
-        atomicAdd(&a.counters[3], (unsigned long long)cnt.sget_slab);
-        atomicAdd(&a.counters[4], (unsigned long long)cnt.node);
-        atomicAdd(&a.counters[5], (unsigned long long)cnt.leaf);
-        atomicAdd(&a.counters[6], 1ull);
-    }
-#endif
-    if (COUNT && active && !PT_SECPROF_ON) {
-        unsigned long long* C = a.counters;
-        atomicAdd(&C[C_PATHS], 1ull);
-        atomicAdd(&C[C_SEGMENTS], (unsigned long long)cnt.seg);
-        atomicAdd(&C[C_NODE], (unsigned long long)cnt.node);
-        atomicAdd(&C[C_LEAF], (unsigned long long)cnt.leaf);
-        atomicAdd(&C[C_HIT], (unsigned long long)cnt.hit);
-        atomicAdd(&C[C_RGBA8], (unsigned long long)(cnt.tap + 1));
-        atomicAdd(&C[C_OVERFLOW], (unsigned long long)cnt.ovf);
-        atomicAdd(&C[C_HDR], (unsigned long long)cnt.hdr);
-    }
-    if (a.cost && costIdx != ~0u && tid == 0) {   // this wave's duration, averaged with the tile's
-        // history, for the next order (a split tile's four parts share their quadrant's entry)
-        const unsigned long long dur = min(clock64() - t_start, 0xffffffffull);
-        a.cost[costIdx] = (unsigned)((dur + (unsigned long long)a.cost[costIdx]) >> 1);
-    }
-    if (!active || px >= a.width || py >= a.height) return;   // quad helper outside the target, idle lane
-
-    // ---- progressive accumulation (js/PathTracingCommon.js:1326-1357)
-    const long long pi = (long long)py * a.width + px;
-    // history and accumulation stream once per frame: non-temporal loads and stores, so that they
-    // displace fewer BVH records in L2 (helmet -2 %, sky+dragon -1.5 %, bunny -1 %, dragon +-0)
-    float4 prev;
-    prev.x = __builtin_nontemporal_load(&a.prev[pi].x); prev.y = __builtin_nontemporal_load(&a.prev[pi].y);
-    prev.z = __builtin_nontemporal_load(&a.prev[pi].z); prev.w = __builtin_nontemporal_load(&a.prev[pi].w);
-    float cr = r.x, cg = r.y, cb = r.z, ca;
-    if (a.frame == 1.0f) prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    else if (a.moving) {
-        prev.x *= 0.5f; prev.y *= 0.5f; prev.z *= 0.5f;
-        cr *= 0.5f; cg *= 0.5f; cb *= 0.5f;
-        prev.w = 0.0f;
-    }
-    ca = 0.0f;
-    float sharp = g.sharp;
-    if (colorDiff >= 1.0f || normalDiff >= 1.0f || objectDiff >= 1.0f) sharp = 1.01f;
-    if (sharp == 1.01f) ca = 1.01f;
-    if (sharp == -1.0f) ca = -1.0f;
-    if (prev.w == 1.01f) ca = 1.01f;
-    if (prev.w == -1.0f) ca = 0.0f;
-    typedef float nt4 __attribute__((ext_vector_type(4)));
-    const nt4 o = { prev.x + cr, prev.y + cg, prev.z + cb, ca };
-    __builtin_nontemporal_store(o, (nt4*)&a.out[pi]);
-}
-
-#define PT_TRACE_INST(P)                                     \
-    template __global__ void pt_trace<P, false>(TraceArgs); \
-    template __global__ void pt_trace<P, true>(TraceArgs);
-PT_FOR_EACH_PROG(PT_TRACE_INST)
-#undef PT_TRACE_INST
-
-// ------------------------------------------------------------------------------ persistent paths
-// pt_persist<PROG,COUNT>: the same per-pixel program with path regeneration. A wave owns a list
-// of `per_wave` 8x8 wave tiles (the static kernel's lane order) and keeps its 64 lanes busy: when
-// at least `refill` lanes have finished their path, they take the next pixels of the list and
-// start their camera rays, so the wave no longer idles while its longest path runs out its six
-// bounces. A finished path stores its G-buffer (objectNormal/ID/Color, pixelSharpness) and
-// radiance by pixel; wf_finish then does the 2x2 derivatives and the accumulation.
-template <int PROG, bool COUNT>
-__global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_persist(TraceArgs a, WfBufs w, int tiles_x,
-                                                                       unsigned n_wave_tiles, unsigned per_wave,
-                                                                       unsigned refill)
-{
-    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kBlock];   // stack levels + the scratch level, or the trail walk's ring
-    const unsigned tid = threadIdx.x;
-    const unsigned lane = tid & 63u, wave = tid >> 6;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    const unsigned wid = blockIdx.x * (kBlock / 64) + wave;
-    unsigned next = wid * per_wave * 64u;
-    const unsigned end = min(next + per_wave * 64u, n_wave_tiles * 64u);
-    const unsigned deep = blockIdx.x * kBlock + tid;
-    Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
-    unsigned paths = 0;
-    Path p;
-    PState s;
-    GOut g;
-    f3 accum = mk(0, 0, 0);
-    unsigned pix = 0;
-    bool alive = false;
-    for (;;) {
-        const unsigned long long dead = __ballot(!alive);
-        const unsigned ndead = (unsigned)__popcll(dead);
-        if (next < end && (ndead >= refill || ndead == 64u)) {
-            if (!alive) {
-                const unsigned q = next + (unsigned)__popcll(dead & below);
-                if (q < end) {
-                    const unsigned L = q >> 6, l = q & 63u;
-                    const unsigned per_band = (unsigned)tiles_x * 4u;
-                    const unsigned bl = L / per_band, rem = L - bl * per_band;
-                    const unsigned tx = rem >> 2, sub = rem & 3u;
-                    const int band = (int)bl * a.num_parts + a.part;
-                    const int lx = (int)((l & 1u) | ((l >> 1) & 6u)), ly = (int)(((l >> 1) & 1u) | ((l >> 3) & 6u));
-                    const int px = (int)tx * kTile + (int)(sub & 1u) * 8 + lx;
-                    const int py = band * kTile + (int)(sub >> 1) * 8 + ly;
-                    if (px < w.wq && py < w.hq) {
-                        cameraRay(a, px, py, p);
-                        pathBegin(s, g);
-                        accum = mk(0, 0, 0);
-                        pix = (unsigned)py * (unsigned)w.wq + (unsigned)px;
-                        alive = true;
-                        if (COUNT) paths++;
-                    }
-                }
-            }
-            next += ndead;
-        }
-        if (__ballot(alive) == 0ull) {
-            if (next >= end) break;
-            continue;
-        }
-        if (alive && !bounceStep<PROG, COUNT, kBlock>(a, p, s, g, accum, lds_stack, tid, deep, cnt)) {
-            const f3 r = max3s(accum, 0.0f);
-            w.gb0[pix] = make_float4(g.nrm.x, g.nrm.y, g.nrm.z, g.id);
-            w.gb1[pix] = make_float4(g.col.x, g.col.y, g.col.z, g.sharp);
-            w.rad[pix] = make_float4(r.x, r.y, r.z, 0.0f);
-            alive = false;
-        }
-    }
-    if (COUNT) {
-        unsigned long long* C = a.counters;
-        if (paths) atomicAdd(&C[C_PATHS], (unsigned long long)paths);
-        atomicAdd(&C[C_SEGMENTS], (unsigned long long)cnt.seg);
-        atomicAdd(&C[C_NODE], (unsigned long long)cnt.node);
-        atomicAdd(&C[C_LEAF], (unsigned long long)cnt.leaf);
-        atomicAdd(&C[C_HIT], (unsigned long long)cnt.hit);
-        atomicAdd(&C[C_RGBA8], (unsigned long long)(cnt.tap + paths));
-        atomicAdd(&C[C_OVERFLOW], (unsigned long long)cnt.ovf);
-        atomicAdd(&C[C_HDR], (unsigned long long)cnt.hdr);
-    }
-}
-
-#define PT_PERSIST_INST(P)                                                                          \
-    template __global__ void pt_persist<P, false>(TraceArgs, WfBufs, int, unsigned, unsigned, unsigned); \
-    template __global__ void pt_persist<P, true>(TraceArgs, WfBufs, int, unsigned, unsigned, unsigned);
-PT_FOR_EACH_PROG(PT_PERSIST_INST)
-#undef PT_PERSIST_INST
-
 // ------------------------------------------------------------------------------ screenCopy
 __global__ __launch_bounds__(256) void pt_copy(CopyArgs a)
 {
@@ -894,6 +465,63 @@ __global__ __launch_bounds__(256) void pt_pairs_top(const float4* rec, uint32_t 
     for (int q = 0; q < 4; q++) top[4u * idx + q] = ok ? rec[code / 16u + q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
+// Two-level records (PROG_QUAD, bvhWalkQuads in pt_device.h): per inner node n (by inner rank r,
+// 192 B at r * 192) its child-pair line, then each child's own line - the child's child-pair line if
+// it is inner, its leaf triangle line if not. Codes: innerRank * 192 for an inner node, kLeafBit |
+// the offset of the leaf's line in its parent's record for a leaf. A leaf root gets one line of its
+// own after the records (at n_inner * 192).
+PT_D uint32_t quadCode(const float* code, const unsigned char* inner, unsigned c, uint32_t parentOff, unsigned slot)
+{
+    return inner[c] ? (uint32_t)code[c] * 192u : kLeafBit | (parentOff + 64u * slot);
+}
+// node m's child-pair line with two-level codes (m inner; its record at mOff)
+PT_D void quadPairLine(const float4* aabb, long long texels, const float* code, const unsigned char* inner, unsigned m,
+                       uint32_t mOff, float4* o)
+{
+    const float fm = (float)m;
+    const float4 c1 = fetch32(aabb, texels, fm * 2.0f + 1.0f);
+    const float idA = fm + 1.0f, idB = c1.x;
+    const float4 a0 = fetch32(aabb, texels, idA * 2.0f), a1 = fetch32(aabb, texels, idA * 2.0f + 1.0f);
+    const float4 b0 = fetch32(aabb, texels, idB * 2.0f), b1 = fetch32(aabb, texels, idB * 2.0f + 1.0f);
+    o[0] = make_float4(a0.y, a0.z, a0.w, a1.y);
+    o[1] = make_float4(a1.z, a1.w, b0.y, b0.z);
+    o[2] = make_float4(b0.w, b1.y, b1.z, b1.w);
+    o[3] = make_float4(__uint_as_float(quadCode(code, inner, m + 1u, mOff, 1u)),
+                       __uint_as_float(quadCode(code, inner, (unsigned)idB, mOff, 2u)), 0.0f, 0.0f);
+}
+// leaf m's triangle line: v0, e1 = v1 - v0, e2 = v2 - v0, idObject (as the leaf records of pt_pairs_build)
+PT_D void quadLeafLine(const float4* aabb, long long texels, const float4* tri, long long tri_texels, unsigned m, float4* o)
+{
+    const float hdr = fetch32(aabb, texels, (float)m * 2.0f).x;
+    const float id = 8.0f * hdr;
+    const float4 t0 = fetch32(tri, tri_texels, id), t1 = fetch32(tri, tri_texels, id + 1.0f),
+                 t2 = fetch32(tri, tri_texels, id + 2.0f);
+    const f3 v0 = mk(t0.x, t0.y, t0.z), e1 = mk(t0.w, t1.x, t1.y) - v0, e2 = mk(t1.z, t1.w, t2.x) - v0;
+    o[0] = make_float4(v0.x, v0.y, v0.z, e1.x);
+    o[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+    o[2] = make_float4(e2.z, hdr, 0.0f, 0.0f);
+    o[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+__global__ __launch_bounds__(256) void pt_quads_build(const float4* aabb, long long texels, const float4* tri,
+                                                      long long tri_texels, unsigned nrec, const float* code,
+                                                      const unsigned char* inner, float4* out, unsigned n_inner)
+{
+    const unsigned n = blockIdx.x * 256u + threadIdx.x;
+    if (n >= nrec) return;
+    if (!inner[n]) {
+        if (n == 0u) quadLeafLine(aabb, texels, tri, tri_texels, 0u, out + 12ull * n_inner);   // a leaf root
+        return;
+    }
+    const uint32_t off = (uint32_t)code[n] * 192u;
+    float4* o = out + off / 16u;
+    quadPairLine(aabb, texels, code, inner, n, off, o);
+    const unsigned idA = n + 1u, idB = (unsigned)fetch32(aabb, texels, (float)n * 2.0f + 1.0f).x;
+    if (inner[idA]) quadPairLine(aabb, texels, code, inner, idA, (uint32_t)code[idA] * 192u, o + 4);
+    else quadLeafLine(aabb, texels, tri, tri_texels, idA, o + 4);
+    if (inner[idB]) quadPairLine(aabb, texels, code, inner, idB, (uint32_t)code[idB] * 192u, o + 8);
+    else quadLeafLine(aabb, texels, tri, tri_texels, idB, o + 8);
+}
+
 // ------------------------------------------------------------------------------ self-test
 // every binary32 pattern with bits 31..24 == hi: fast device sequence vs the IEEE operation it
 // stands for (NaN == NaN); one atomic per wave with a mismatch
@@ -939,25 +567,33 @@ __global__ void pt_math_probe_kernel(int op, const float* x, const float* y, flo
 } // namespace pt
 
 // ------------------------------------------------------------------------------ launchers
+#define PT_WALK_LAUNCHERS(W)                                                                                     \
+    hipError_t pt_launch_trace_##W(int prog, int count, const pt::TraceArgs* a, dim3 grid, dim3 block, hipStream_t s); \
+    hipError_t pt_launch_persist_##W(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x,   \
+                                     unsigned n_wave_tiles, unsigned per_wave, unsigned refill, dim3 grid, dim3 block, \
+                                     hipStream_t s);
+PT_WALK_LAUNCHERS(ref)
+PT_WALK_LAUNCHERS(pairs)
+PT_WALK_LAUNCHERS(trail)
+PT_WALK_LAUNCHERS(quad)
+#undef PT_WALK_LAUNCHERS
+
 extern "C" {
 
+// the megakernel of a draw: the program variant's walk picks the translation unit that holds it
+// (pt_trace_walk*.hip)
 hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s)
 {
-    dim3 grid(grid_x * pt::kTraceSub, grid_y), block(pt::kTraceBlock);
+    const dim3 grid(grid_x * pt::kTraceSub, grid_y), block(pt::kTraceBlock);
     // texture-free models (the bench's StanfordBunny) take the variant without PBR code
-    prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr, a->bvh_top_base != 0);
-#define PT_CASE(P)                                                                                  \
-    case P:                                                                                          \
-        if (count) hipLaunchKernelGGL((pt::pt_trace<P, true>), grid, block, 0, s, *a);               \
-        else hipLaunchKernelGGL((pt::pt_trace<P, false>), grid, block, 0, s, *a);                    \
-        break;
-    using namespace pt;
-    switch (prog) {
-        PT_FOR_EACH_PROG(PT_CASE)
+    prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_walk);
+    switch (prog / pt::PROG_PAIRS) {
+    case pt::WALK_REF: return pt_launch_trace_ref(prog, count, a, grid, block, s);
+    case pt::WALK_PAIRS: return pt_launch_trace_pairs(prog, count, a, grid, block, s);
+    case pt::WALK_TRAIL: return pt_launch_trace_trail(prog, count, a, grid, block, s);
+    case pt::WALK_QUAD: return pt_launch_trace_quad(prog, count, a, grid, block, s);
     default: return hipErrorInvalidValue;
     }
-#undef PT_CASE
-    return hipGetLastError();
 }
 
 hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,
@@ -971,21 +607,16 @@ hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned
 hipError_t pt_launch_persist(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x,
                              unsigned n_wave_tiles, unsigned per_wave, unsigned refill, hipStream_t s)
 {
-    prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr, a->bvh_top_base != 0);
+    prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_walk);
     const unsigned waves = (n_wave_tiles + per_wave - 1) / per_wave;
-    dim3 grid((waves + 3) / 4), block(pt::kBlock);
-#define PT_CASE(P)                                                                                          \
-    case P:                                                                                                  \
-        if (count) hipLaunchKernelGGL((pt::pt_persist<P, true>), grid, block, 0, s, *a, *w, tiles_x, n_wave_tiles, per_wave, refill); \
-        else hipLaunchKernelGGL((pt::pt_persist<P, false>), grid, block, 0, s, *a, *w, tiles_x, n_wave_tiles, per_wave, refill); \
-        break;
-    using namespace pt;
-    switch (prog) {
-        PT_FOR_EACH_PROG(PT_CASE)
+    const dim3 grid((waves + 3) / 4), block(pt::kBlock);
+    switch (prog / pt::PROG_PAIRS) {
+    case pt::WALK_REF: return pt_launch_persist_ref(prog, count, a, w, tiles_x, n_wave_tiles, per_wave, refill, grid, block, s);
+    case pt::WALK_PAIRS: return pt_launch_persist_pairs(prog, count, a, w, tiles_x, n_wave_tiles, per_wave, refill, grid, block, s);
+    case pt::WALK_TRAIL: return pt_launch_persist_trail(prog, count, a, w, tiles_x, n_wave_tiles, per_wave, refill, grid, block, s);
+    case pt::WALK_QUAD: return pt_launch_persist_quad(prog, count, a, w, tiles_x, n_wave_tiles, per_wave, refill, grid, block, s);
     default: return hipErrorInvalidValue;
     }
-#undef PT_CASE
-    return hipGetLastError();
 }
 
 // the four passes of the child-pair build; `offsets` is filled by the host between pass 2 and 3
@@ -1020,6 +651,15 @@ hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, 
     case 3: hipLaunchKernelGGL(pt::pt_pairs_top, dim3(1), b256, 0, s, rec, root, top); break;
     default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_quads_build(const float4* aabb, long long texels, const float4* tri, long long tri_texels,
+                                 unsigned nrec, const float* code, const unsigned char* inner, float4* out,
+                                 unsigned n_inner, hipStream_t s)
+{
+    hipLaunchKernelGGL(pt::pt_quads_build, dim3((nrec + 255) / 256), dim3(256), 0, s, aabb, texels, tri, tri_texels, nrec,
+                       code, inner, out, n_inner);
     return hipGetLastError();
 }
 

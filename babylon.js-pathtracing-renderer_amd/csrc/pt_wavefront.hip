@@ -239,6 +239,7 @@ __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b
         BvhResult br = { 0.0f, 0.0f, 0.0f, false, 0u, 0u, 0u };
         WfStack st{ (lds_float2*)lds, tid, (glb_float2*)deep, dstride };
         if (kTrail<PROG>) bvhWalkTrail<kRingOf<PROG>>(a, O, D, inv, dbl, rootT, hitT, (lds_float2*)lds, kBlock, tid, br);
+        else if (kQuad<PROG>) bvhWalkQuads(a, O, D, inv, dbl, rootT, hitT, st, br);
         else if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, rootT, hitT, st, br);
         else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, hitT, st, br);
         const unsigned nodes = br.nodes, leaves = br.leaves, ovf = br.ovf;
@@ -417,7 +418,7 @@ extern "C" hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceAr
                                           int tiles_x, int bands, int persist_blocks, hipStream_t s)
 {
     using namespace pt;
-    prog = resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_pairs != nullptr, a->bvh_top_base != 0);
+    prog = resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_walk);
     dim3 tiles(tiles_x, bands), blk(kBlock);
     if (count) hipLaunchKernelGGL((wf_raygen<true>), tiles, blk, 0, s, *a, *w);
     else hipLaunchKernelGGL((wf_raygen<false>), tiles, blk, 0, s, *a, *w);

@@ -169,10 +169,12 @@ int pt_set_backend(pt_ctx* ctx, int backend);
  * ring of the deepest pending entries, re-descending from a jump table of the top levels when the
  * ring runs dry (no stack memory beyond LDS; trees deeper than 32 levels, or whose nodes have more
  * than one parent, keep PT_BVH_PAIRS). A texture whose links are not exact in-range integers keeps
- * PT_BVH_REFERENCE, the walk over the reference's own texel pairs. Same nodes, same order, same
- * results every way (js/GLTFModelPathTracing_FragmentShader.js:211-298).
+ * PT_BVH_REFERENCE, the walk over the reference's own texel pairs. PT_BVH_QUADS walks two-level
+ * records (an inner node's child pair plus each child's own pair or triangle, 192 B): one fetch per
+ * two tree levels, with the short stack. Same nodes, same order, same results every way
+ * (js/GLTFModelPathTracing_FragmentShader.js:211-298).
  * pt_bvh_layout_used reports what the last glTF draw of the context walked (-1: none yet). */
-enum pt_bvh_layout { PT_BVH_REFERENCE = 0, PT_BVH_PAIRS = 1, PT_BVH_TRAIL = 2 };
+enum pt_bvh_layout { PT_BVH_REFERENCE = 0, PT_BVH_PAIRS = 1, PT_BVH_TRAIL = 2, PT_BVH_QUADS = 3 };
 int pt_set_bvh_layout(pt_ctx* ctx, int layout);
 int pt_bvh_layout_used(pt_ctx* ctx);
 /* Enqueue this context's work on a caller-owned HIP stream (e.g. torch.cuda.current_stream(), so

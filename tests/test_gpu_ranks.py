@@ -50,30 +50,32 @@ def test_torch_stream_ranks_bitexact(name, world, size):
             e.resize_canvas(W, Hh)
             e.set_row_partition(world, r)
             e.set_output_partition(True)
-            ranks.append((e, player, acc, canvas))
+            ranks.append((e, player, acc, canvas, cpy))   # the tensors stay alive: libpt holds their pointers
         full_acc = torch.zeros((pad * 16, W, 4), dtype=torch.float32, device="cuda")
         full_can = torch.zeros((pad * 16, W, 4), dtype=torch.uint8, device="cuda")
         ref_acc, ref_can, _ = H.oracle_replay(meta, width=W, height=Hh, with_output=True)
         for i, frame in enumerate(meta["frames"]):
             pt_call, cp_call, out_call = frame
-            for e, player, acc, canvas in ranks:        # path tracing + screenCopy of each rank's bands
+            for e, player, acc, canvas, _ in ranks:        # path tracing + screenCopy of each rank's bands
                 player.play_call(pt_call)
                 player.play_call(cp_call)
-            for r, (e, player, acc, canvas) in enumerate(ranks):   # halo rows from the band neighbours
+            for r, (e, player, acc, canvas, _) in enumerate(ranks):   # halo rows from the band neighbours
                 lo, hi = (r - 1) % world, (r + 1) % world
                 _band_copy(acc, ranks[lo][2], world, lo, slice(14, 16))
                 _band_copy(acc, ranks[hi][2], world, hi, slice(0, 2))
-            for e, player, acc, canvas in ranks:        # screenOutput of each rank's bands into its canvas
+            for e, player, acc, canvas, _ in ranks:        # screenOutput of each rank's bands into its canvas
                 e.canvas_wrap(W, Hh, canvas.data_ptr())
                 player.play_call(out_call)
-            for r, (e, player, acc, canvas) in enumerate(ranks):   # the gather (and the bands' accumulation)
+            for r, (e, player, acc, canvas, _) in enumerate(ranks):   # the gather (and the bands' accumulation)
                 _band_copy(full_can, canvas, world, r)
                 _band_copy(full_acc, acc, world, r)
             torch.cuda.current_stream().synchronize()
             got_acc = full_acc[:Hh].cpu().numpy()
             got_can = full_can[:Hh].cpu().numpy()
             bad = (got_acc.view(np.uint32) != ref_acc[i].view(np.uint32)).any(-1)
-            assert not bad.any(), "frame %d accumulation: %d of %d pixels differ" % (i, bad.sum(), bad.size)
+            assert not bad.any(), "frame %d accumulation: %d of %d pixels differ (rows %s, columns %d..%d)" % (
+                i, bad.sum(), bad.size, sorted(set(np.nonzero(bad)[0].tolist()))[:40], np.nonzero(bad)[1].min(),
+                np.nonzero(bad)[1].max())
             badc = (got_can != ref_can[i]).any(-1)
             assert not badc.any(), "frame %d canvas: %d of %d pixels differ" % (i, badc.sum(), badc.size)
     finally:
