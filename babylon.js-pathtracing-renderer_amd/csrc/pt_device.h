@@ -320,7 +320,13 @@ PT_D void texBilinear(const Tex8& t, float u, float v, float out[4])
     float ax = x - fx, by = y - fy;
     int x0 = wrapTexel(fx, t.w), y0 = wrapTexel(fy, t.h);
     int x1 = x0 + 1 == t.w ? 0 : x0 + 1, y1 = y0 + 1 == t.h ? 0 : y0 + 1;
+#ifdef PT_NT_TEX   // experiment: the maps' taps as non-temporal loads (keep BVH records in L2)
+    const uint32_t* q = (const uint32_t*)t.p;
+    auto ld = [&](int i) { const uint32_t v = __builtin_nontemporal_load(q + i); return make_uchar4(v & 255u, (v >> 8) & 255u, (v >> 16) & 255u, v >> 24); };
+    uchar4 t00 = ld(y0 * t.w + x0), t10 = ld(y0 * t.w + x1), t01 = ld(y1 * t.w + x0), t11 = ld(y1 * t.w + x1);
+#else
     uchar4 t00 = t.p[y0 * t.w + x0], t10 = t.p[y0 * t.w + x1], t01 = t.p[y1 * t.w + x0], t11 = t.p[y1 * t.w + x1];
+#endif
     out[0] = gmix(gmix(unorm8(t00.x), unorm8(t10.x), ax), gmix(unorm8(t01.x), unorm8(t11.x), ax), by);
     out[1] = gmix(gmix(unorm8(t00.y), unorm8(t10.y), ax), gmix(unorm8(t01.y), unorm8(t11.y), ax), by);
     out[2] = gmix(gmix(unorm8(t00.z), unorm8(t10.z), ax), gmix(unorm8(t01.z), unorm8(t11.z), ax), by);
@@ -336,8 +342,16 @@ PT_D float4 texBilinearF(const TexF& t, float u, float v)
     float ax = x - fx, by = y - fy;
     int x0 = wrapTexel(fx, t.w), y0 = wrapTexel(fy, t.h);
     int x1 = x0 + 1 == t.w ? 0 : x0 + 1, y1 = y0 + 1 == t.h ? 0 : y0 + 1;
+#ifdef PT_NT_TEX
+    auto ld = [&](size_t i) { const float* f = (const float*)(t.p + i);
+        return make_float4(__builtin_nontemporal_load(f), __builtin_nontemporal_load(f + 1), __builtin_nontemporal_load(f + 2),
+                           __builtin_nontemporal_load(f + 3)); };
+    const float4 t00 = ld((size_t)y0 * t.w + x0), t10 = ld((size_t)y0 * t.w + x1);
+    const float4 t01 = ld((size_t)y1 * t.w + x0), t11 = ld((size_t)y1 * t.w + x1);
+#else
     const float4 t00 = t.p[(size_t)y0 * t.w + x0], t10 = t.p[(size_t)y0 * t.w + x1];
     const float4 t01 = t.p[(size_t)y1 * t.w + x0], t11 = t.p[(size_t)y1 * t.w + x1];
+#endif
     return make_float4(gmix(gmix(t00.x, t10.x, ax), gmix(t01.x, t11.x, ax), by),
                        gmix(gmix(t00.y, t10.y, ax), gmix(t01.y, t11.y, ax), by),
                        gmix(gmix(t00.z, t10.z, ax), gmix(t01.z, t11.z, ax), by),

@@ -188,32 +188,27 @@ constexpr int kTraceBlock = PT_TRACE_BLOCK;
 constexpr int kTraceSub = 4 / (kTraceBlock / 64);   // workgroups per 16x16 tile
 static_assert(kTraceBlock == 64 || kTraceBlock == 256, "trace workgroups are one wave or one 16x16 tile");
 
-template <int PROG, bool COUNT>
-__global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
+// Which pixel a lane of pt_trace shades: the 8x8 wave tile of this wave inside its 16x16 tile
+// (grid = tiles_x * kTraceSub x bands). Launch slots come in runs of 32 workgroups = 8 tiles x 4
+// quadrants, quadrant-major: the quadrants of one tile are workgroups 8 apart, which the dispatcher
+// deals to the same XCD (one L2), while the runs' tiles still go round-robin over the XCDs (a short
+// last run keeps the map a bijection). The tiles come in longest-first order (the previous frame's
+// costs, pt_order_build) when a.order is set, else row-major.
+// Split tiles: the K = *a.split slowest tiles come first, each as 16 waves of 16 lanes (runs of 128
+// workgroups = 8 tiles x 16 parts, again 8 apart per tile). A wave ends with its slowest lane of each
+// bounce; a 4x4 block waits on fewer of them than an 8x8 one, so the kernel's critical path (the
+// slowest tiles' waves, which start first and end last when a few tiles dominate, as the helmet's do)
+// shortens. Which lane shades which pixel never changes what a pixel computes: same bits.
+// False for the grid's padding. (PT_RECOMPUTE_PLACE builds evaluate it again after the path.)
+struct TracePlace {
+    int px, py, part;
+    unsigned costIdx;
+};
+PT_D bool tracePlace(const TraceArgs& a, int lane, bool first, TracePlace& pl)
 {
-    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];   // stack levels + the scratch level, or the trail walk's ring
-    __shared__ float lds_gout[8 * kTraceBlock];
-    const unsigned tid = threadIdx.x;
-    const int lane = tid & 63;
-    const unsigned long long t_start = clock64();
-#ifdef PT_SECPROF
-    const unsigned long long w0_ = wall_clock64();
-#endif
-    // the 8x8 wave tile of this wave inside its 16x16 tile (grid = tiles_x * kTraceSub x bands)
     int wave, tx, part = -1;
     unsigned bY, costIdx = ~0u;
     if (kTraceSub == 4 && PT_TILE_GROUPS) {
-        // launch slots in runs of 32 workgroups = 8 tiles x 4 quadrants, quadrant-major: the
-        // quadrants of one tile are workgroups 8 apart, which the dispatcher deals to the same XCD
-        // (one L2), while the runs' tiles still go round-robin over the XCDs (a short last run keeps
-        // the map a bijection). The tiles come in longest-first order (the previous frame's costs,
-        // pt_order_build) when a.order is set, else row-major.
-        // Split tiles: the K = *a.split slowest tiles come first, each as 16 waves of 16 lanes
-        // (runs of 128 workgroups = 8 tiles x 16 parts, again 8 apart per tile). A wave ends with
-        // its slowest lane of each bounce; a 4x4 block waits on fewer of them than an 8x8 one, so
-        // the kernel's critical path (the slowest tiles' waves, which start first and end last when
-        // a few tiles dominate, as the helmet's do) shortens. Which lane shades which pixel never
-        // changes what a pixel computes: same bits.
         const unsigned tiles_x = gridDim.x / 4u, ntiles = a.ntiles;
         const unsigned K = (a.order && a.split) ? *a.split : 0u;   // chosen by pt_order_build
         const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
@@ -225,19 +220,19 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
             part = (int)((r >> 3) & 3u);
         } else {
             const unsigned L2 = L - 16u * K;
-            if (L2 >= 4u * (ntiles - K)) return;   // the grid's padding
+            if (L2 >= 4u * (ntiles - K)) return false;
             const unsigned g = L2 >> 5, r = L2 & 31u;
             const unsigned T = min(8u, ntiles - K - g * 8u);
             slot = K + g * 8u + r % T;
             wave = (int)(r / T);
         }
         const unsigned tile = a.order ? a.order[slot] : slot;
-        if (slot < a.prio_tiles) __builtin_amdgcn_s_setprio(3);   // the critical path: issue first
+        if (first && slot < a.prio_tiles) __builtin_amdgcn_s_setprio(3);   // the critical path: issue first
         tx = (int)(tile % tiles_x);
         bY = tile / tiles_x;
         costIdx = tile * 4u + (unsigned)wave;
     } else if (kTraceSub == 1) {
-        wave = (int)(tid >> 6);
+        wave = (int)(threadIdx.x >> 6);
         tx = (int)blockIdx.x;
         bY = blockIdx.y;
     } else {
@@ -249,15 +244,41 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     const int lx = part < 0 ? (lane & 1) | ((lane >> 1) & 6) : (part & 1) * 4 + ((lane & 1) | ((lane >> 1) & 2));
     const int ly = part < 0 ? ((lane >> 1) & 1) | ((lane >> 3) & 6) : (part >> 1) * 4 + (((lane >> 1) & 1) | ((lane >> 2) & 2));
     const int band = (int)bY * a.num_parts + a.part;            // global 16-row band of this block
-    const int px = tx * kTile + (wave & 1) * 8 + lx;
-    const int py = band * kTile + (wave >> 1) * 8 + ly;
+    pl.px = tx * kTile + (wave & 1) * 8 + lx;
+    pl.py = band * kTile + (wave >> 1) * 8 + ly;
+    pl.part = part;
+    pl.costIdx = costIdx;
+    return true;
+}
+// the lane id, computed where it is asked for (not a value the compiler keeps live across the path)
+PT_D int laneAgain()
+{
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
+template <int PROG, bool COUNT>
+__global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
+{
+    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];   // stack levels + the scratch level, or the trail walk's ring
+    __shared__ float lds_gout[8 * kTraceBlock];
+    const unsigned tid = threadIdx.x;
+    const int lane = tid & 63;
+    const unsigned long long t_start = clock64();
+#ifdef PT_SECPROF
+    const unsigned long long w0_ = wall_clock64();
+#endif
+    TracePlace pl;
+    if (!tracePlace(a, lane, true, pl)) return;   // the grid's padding
+    const int px = pl.px, py = pl.py;
     // stack levels >= kStackLds: a global slab [level][lane of the grid] (a private array would be
     // scratch, which the runtime reserves for every resident wave)
     const unsigned deep = (blockIdx.y * gridDim.x + blockIdx.x) * kTraceBlock + tid;
 
     // lanes whose whole 2x2 quad lies beyond the (even-rounded) target do no work; quad helpers
     // that only complete a quad at an odd edge are shaded like GL helper invocations
-    const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1) && (part < 0 || lane < 16);
+    const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1) && (pl.part < 0 || lane < 16);
     Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
 #ifdef PT_SECPROF
     __shared__ unsigned long long lds_sec[16];
@@ -276,10 +297,24 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         r = radiance<PROG, COUNT, kTraceBlock>(a, p, gl, lds_stack, tid, deep, cnt);
     }
     PT_SEC(cnt, 4);
+#ifdef PT_RECOMPUTE_PLACE
+    // experiment: the lane's place again (see tracePlace), so that none of it is kept live across the
+    // path: 56 -> 40 B of scratch per lane on the dragon stand-in, yet 0.6-2.8 % slower (the reload of
+    // the tile order sits on every wave's tail; profiles/r03_ab_place.txt)
+    asm volatile("" ::: "memory");
+    const int lane2 = kTraceBlock == 64 ? laneAgain() : (int)(threadIdx.x & 63u);
+    tracePlace(a, lane2, false, pl);
+    const int px2 = pl.px, py2 = pl.py;
+    const bool active2 = px2 < ((a.width + 1) & ~1) && py2 < ((a.height + 1) & ~1) && (pl.part < 0 || lane2 < 16);
+    const GOut g = (GOutLds<kTraceBlock>{ (lds_float*)lds_gout, kTraceBlock == 64 ? (unsigned)lane2 : threadIdx.x }).load();
+#else
+    const int lane2 = lane, px2 = px, py2 = py;
+    const bool active2 = active;
     const GOut g = gl.load();
+#endif
 
     // ---- 2x2 fine derivatives (js/PathTracingCommon.js:1306-1320): partner lanes ^1 (x) and ^2 (y)
-    const bool xodd = lane & 1, yodd = lane & 2;
+    const bool xodd = lane2 & 1, yodd = lane2 & 2;
     auto ddx = [&](float v) { float o = xorq(v, 1); return xodd ? v - o : o - v; };
     auto ddy = [&](float v) { float o = xorq(v, 2); return yodd ? v - o : o - v; };
     float dNx = fabsf(ddx(g.nrm.x)) + fabsf(ddy(g.nrm.x));
@@ -326,15 +361,15 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         atomicAdd(&C[C_OVERFLOW], (unsigned long long)cnt.ovf);
         atomicAdd(&C[C_HDR], (unsigned long long)cnt.hdr);
     }
-    if (a.cost && costIdx != ~0u && tid == 0) {   // this wave's duration, averaged with the tile's
+    if (a.cost && pl.costIdx != ~0u && lane2 == 0) {   // this wave's duration, averaged with the tile's
         // history, for the next order (a split tile's four parts share their quadrant's entry)
         const unsigned long long dur = min(clock64() - t_start, 0xffffffffull);
-        a.cost[costIdx] = (unsigned)((dur + (unsigned long long)a.cost[costIdx]) >> 1);
+        a.cost[pl.costIdx] = (unsigned)((dur + (unsigned long long)a.cost[pl.costIdx]) >> 1);
     }
-    if (!active || px >= a.width || py >= a.height) return;   // quad helper outside the target, idle lane
+    if (!active2 || px2 >= a.width || py2 >= a.height) return;   // quad helper outside the target, idle lane
 
     // ---- progressive accumulation (js/PathTracingCommon.js:1326-1357)
-    const long long pi = (long long)py * a.width + px;
+    const long long pi = (long long)py2 * a.width + px2;
     // history and accumulation stream once per frame: non-temporal loads and stores, so that they
     // displace fewer BVH records in L2 (helmet -2 %, sky+dragon -1.5 %, bunny -1 %, dragon +-0)
     float4 prev;

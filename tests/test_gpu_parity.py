@@ -291,6 +291,9 @@ def test_stack_overflow_is_defined_and_reported(engine, backend):
         engine.sync()
     engine.sync()   # the error is reported once
     assert _bits_equal(ref_acc[0], player.textures["pathTracingRenderTarget"].read())
+    # the restart trail takes trees of depth <= 28 only (then stackLevels[28] cannot overflow): this
+    # one keeps the child-pair walk with its stack
+    assert engine.bvh_layout_used() == ("pairs" if backend[1] == "trail" else backend[1])
 
 
 @pytest.mark.parametrize("parts", [2, 3, 8])

@@ -13,7 +13,7 @@ for round in $(seq $ROUNDS); do
     [ "$n" = secprof ] && continue
     lib=""; [ "$d" != base ] && lib=$PWD/$d/libpt.so
     for w in $WLS; do
-      PT_LIBPT=$lib timeout -k 10 200 python bench.py --workload $w --steps 100 --warmup 10 --cpu-budget 0 --no-pmc > gpurun_out/ab_tmp.json 2>>$OUT || exit $?
+      PT_LIBPT=$lib timeout -k 10 200 python bench.py --workload $w --steps 100 --warmup 10 --cpu-budget 0 --no-pmc --no-anchors > gpurun_out/ab_tmp.json 2>>$OUT || exit $?
       python3 -c "import json; d=json.loads(open('gpurun_out/ab_tmp.json').read().strip().splitlines()[-1]); print('$n $w r$round', d['value'], d['ms_per_step'], d['kernel_ms']['pathtrace'], d['kernel_ms']['screen_output'], d['kernel_ms']['screen_copy'])" >> $OUT
     done
   done

@@ -12,9 +12,9 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeou
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/pytest_gpu_$TAG.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-for W in dragon sky_dragon helmet bunny; do
+for W in dragon sky_dragon helmet bunny bunny16; do
   timeout -k 10 400 python bench.py --workload $W > gpurun_out/bench_${TAG}_$W.json 2> gpurun_out/bench_${TAG}_$W.err || exit $?
 done
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 --warmup 5 --cpu-budget 0 --no-pmc > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1 || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 --warmup 5 --cpu-budget 0 --no-pmc --no-anchors > "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log" 2>&1 || exit $?
 echo "prof rc=0" >> "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG.log"
