@@ -37,7 +37,10 @@ __host__ __device__ inline uint32_t pairCode(float rankCode, uint32_t leafBase)
 // depth <= 28 (stackLevels[28] then never overflows); a jump table of the inner records at depths
 // 0..kTopLevels, by path, after the leaf records
 constexpr int kTrailMaxDepth = 28;
-constexpr int kTopLevels = 7;
+#ifndef PT_TOP_LEVELS
+#define PT_TOP_LEVELS 7
+#endif
+constexpr int kTopLevels = PT_TOP_LEVELS;
 constexpr unsigned kTopEntries = (2u << kTopLevels) - 1u;   // 255 record copies (64 B), heap order
 
 // the BVH walk of a mesh draw (TraceArgs::bvh_walk; the program variant's thousands digit, pt_device.h)

@@ -721,12 +721,54 @@ struct TrailWalk {
     float triID, triU, triV;
     uint32_t trail, dir;       // per depth d: bit 31 - d
     uint32_t lvl;              // the bit of the depth of the node `code` addresses (root: bit 31)
-    int rtop, rcnt;            // ring: next slot, entries held
-    bool pop, restart, lookup;
+    int rtop, rcnt;            // ring: next slot, entries held (at most R - 1: slot rtop is always free)
+    bool pop, lookup;
 };
 constexpr uint32_t kRootBit = 0x80000000u;
+// push onto the ring without a branch: the store always goes to the free slot rtop, and only a real
+// push advances the ring (a full ring then frees its oldest slot)
+template <int R>
+PT_D void ringPush(lds_float2* ring, unsigned stride, unsigned slot, TrailWalk& w, bool push, float t, float code)
+{
+    const vf2 v = { t, code };
+    ring[(unsigned)w.rtop * stride + slot] = v;
+    w.rtop = push ? (w.rtop == R - 1 ? 0 : w.rtop + 1) : w.rtop;
+    w.rcnt = push ? min(w.rcnt + 1, R - 1) : w.rcnt;
+}
+// The restart (the ring ran dry at a pop of the level w.lvl): from the jump table's copy of the
+// deepest ancestor it holds, down the dir bits to the popped level's parent, pushing the pending
+// siblings met on the way back onto the ring; returns the popped level's far child as a ring entry
+// would hold it (its box distance, its code).
+template <int R>
+PT_D float2 trailRestart(const TraceArgs& a, const PairBufs& b, f3 O, f3 inv, bool fast, lds_float2* ring,
+                         unsigned stride, unsigned slot, TrailWalk& w, BvhResult& r)
+{
+    const int p = min(30 - __builtin_ctz(w.lvl), kTopLevels);   // the popped depth - 1, capped
+    uint32_t code = a.bvh_top_base + ((1u << p) - 1u + (w.dir >> (31 - p))) * 64u;
+    uint32_t l = kRootBit >> p;
+    for (;;) {
+#ifdef PT_SECPROF
+        r.restarts++;   // experiment builds: the restart descents' record loads
+#endif
+        const float4 r0 = ldRec4(b.rec, code), r1 = ldRec4(b.rec, code + 16u), r2 = ldRec4(b.rec, code + 32u);
+        const float2 r3 = ldRec2(b.rec, code + 48u);
+        float tA, tB;
+        if (fast) {
+            tA = boxFast(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
+            tB = boxFast(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+        } else {
+            tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
+            tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+        }
+        l >>= 1;
+        const bool takeB = (w.dir & l) != 0u;
+        if (l == w.lvl) return make_float2(takeB ? tB : tA, takeB ? r3.y : r3.x);   // the far child popped
+        ringPush<R>(ring, stride, slot, w, !(w.trail & l), takeB ? tA : tB, takeB ? r3.x : r3.y);   // a pending sibling
+        code = __float_as_uint(takeB ? r3.y : r3.x);
+    }
+}
 // one step; false once the walk is over. A step pops (culled: the step ends there) and/or loads one
-// record: an inner node's two children, a leaf's triangle, or a restart descent's next level.
+// record: an inner node's two children or a leaf's triangle.
 template <int R>
 PT_D bool trailWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv, bool dbl, bool fast,
                         lds_float2* ring, unsigned stride, unsigned slot, TrailWalk& w, BvhResult& r)
@@ -737,28 +779,23 @@ PT_D bool trailWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 in
         w.lvl = w.trail & (0u - w.trail);
         w.dir ^= w.lvl;                                // its far child
         w.rtop = (w.rtop == 0 ? R : w.rtop) - 1;       // (moving an empty ring's top is harmless)
-        const vf2 e = ring[(unsigned)w.rtop * stride + slot];
+        vf2 e = ring[(unsigned)w.rtop * stride + slot];
         if (w.rcnt == 0) {
-            // restart: the jump table's copy of the deepest ancestor it holds, then down the dir bits
-            const int p = min(30 - __builtin_ctz(w.lvl), kTopLevels);   // the popped depth - 1, capped
-            w.code = a.bvh_top_base + ((1u << p) - 1u + (w.dir >> (31 - p))) * 64u;
-            w.lvl = kRootBit >> p;
-            w.restart = true;
-#ifdef PT_SECPROF
-            r.restarts++;
-#endif
-        } else {
+            const float2 f = trailRestart<R>(a, b, O, inv, fast, ring, stride, slot, w, r);
+            e.x = f.x; e.y = f.y;
+        } else
             w.rcnt--;
-            if (e.x >= w.hitT) return true;            // culled pop
-            w.code = __float_as_uint(e.y);
-            r.nodes++;
-        }
+        if (e.x >= w.hitT) return true;                // culled pop
+        w.code = __float_as_uint(e.y);
+        r.nodes++;
         w.pop = false;
     }
+    w.pop = true;
     const uint32_t off = w.code & ~kLeafBit;
     const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
     const float2 r3 = ldRec2(b.rec, off + 48u);
-    if (!(w.code & kLeafBit)) {   // an inner record (restart descents visit inner records only)
+    if (!(w.code & kLeafBit)) {
+        r.nodes += 2;
         float tA, tB;
         if (fast) {
             tA = boxFast(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
@@ -767,42 +804,20 @@ PT_D bool trailWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 in
             tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
             tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
         }
+        // the reference's step: the near child next if it is hit, else the far one; the far one
+        // pending when both are hit
+        const bool sw = tB < tA;   // the reference's swap: B is the near child
+        const float tF = sw ? tA : tB;
+        const bool hitN = (sw ? tB : tA) < w.hitT, hitF = tF < w.hitT;
+        const bool both = hitN && hitF;
         const uint32_t bk = w.lvl >> 1;
-        bool push;
-        float pt, pc, next;
-        if (w.restart) {   // a restart descent: the child the dir bit names
-            const bool takeB = (w.dir & bk) != 0u;
-            const bool target = (w.trail & (0u - w.trail)) == bk;   // the popped level: its far child
-            const float t = (target == takeB) ? tB : tA;            // else the pending sibling's box
-            next = takeB ? r3.y : r3.x;
-            pt = t; pc = takeB ? r3.x : r3.y;
-            push = !target && !(w.trail & bk);
-            if (target) {
-                w.restart = false;
-                if (!(t < w.hitT)) { w.lvl = bk; w.pop = true; return true; }   // culled pop
-                r.nodes++;
-            }
-        } else {   // the reference's step
-            r.nodes += 2;
-            const bool sw = tB < tA;   // the reference's swap: B is the near child
-            const float tF = sw ? tA : tB;
-            const bool hitN = (sw ? tB : tA) < w.hitT, hitF = tF < w.hitT;
-            if (!hitN && !hitF) { w.pop = true; return true; }
-            push = hitN && hitF;
-            pt = tF; pc = sw ? r3.x : r3.y;
-            if (!push) w.trail |= bk;
-            const bool takeB = hitN ? sw : !sw;
-            w.dir = takeB ? (w.dir | bk) : (w.dir & ~bk);
-            next = takeB ? r3.y : r3.x;
-        }
-        if (push) {
-            const vf2 v = { pt, pc };
-            ring[(unsigned)w.rtop * stride + slot] = v;
-            w.rtop = w.rtop == R - 1 ? 0 : w.rtop + 1;
-            w.rcnt = min(w.rcnt + 1, R);
-        }
-        w.code = __float_as_uint(next);
-        w.lvl = bk;
+        ringPush<R>(ring, stride, slot, w, both, tF, sw ? r3.x : r3.y);
+        const bool takeB = hitN ? sw : !sw;
+        w.trail |= both ? 0u : bk;
+        w.dir = takeB ? (w.dir | bk) : (w.dir & ~bk);
+        w.code = __float_as_uint(takeB ? r3.y : r3.x);
+        w.lvl = (hitN || hitF) ? bk : w.lvl;
+        w.pop = !(hitN || hitF);
         return true;
     }
     r.leaves++;
@@ -810,7 +825,6 @@ PT_D bool trailWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 in
     const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
     if (d < w.hitT) { w.hitT = d; w.triID = 8.0f * r2.y; w.triU = tu; w.triV = tv; w.lookup = true; }
     asm volatile("" ::"v"(r3.x));   // keeps the codes' load with the other three (as pairWalkStep)
-    w.pop = true;
     return true;
 }
 // ring: R float2 slots per lane at ring[k * stride + slot]
@@ -823,7 +837,6 @@ PT_D void bvhWalkTrail(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     w.triID = 0.0f; w.triU = 0.0f; w.triV = 0.0f;
     w.trail = 0u; w.dir = 0u; w.lvl = kRootBit; w.rtop = 0; w.rcnt = 0;
     w.pop = !(curT < hitT);
-    w.restart = false;
     w.lookup = false;
     const bool fast = pairWalkFast(O, inv);
     const PairBufs b = pairBufs(a);

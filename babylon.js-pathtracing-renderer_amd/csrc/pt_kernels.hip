@@ -450,19 +450,19 @@ __global__ __launch_bounds__(256) void pt_pairs_depth(unsigned nrec, const unsig
 
 __global__ __launch_bounds__(256) void pt_pairs_top(const float4* rec, uint32_t root, float4* top)
 {
-    const unsigned idx = threadIdx.x;
-    if (idx >= kTopEntries) return;
-    const int p = 31 - __builtin_clz(idx + 1u);
-    const unsigned prefix = idx + 1u - (1u << p);
-    uint32_t code = root;
-    bool ok = true;
-    for (int j = 0; j < p && ok; j++) {
-        if (code & kLeafBit) { ok = false; break; }
-        const float4 c = rec[code / 16u + 3u];
-        code = __float_as_uint(((prefix >> (p - 1 - j)) & 1u) ? c.y : c.x);
+    for (unsigned idx = threadIdx.x; idx < kTopEntries; idx += blockDim.x) {
+        const int p = 31 - __builtin_clz(idx + 1u);
+        const unsigned prefix = idx + 1u - (1u << p);
+        uint32_t code = root;
+        bool ok = true;
+        for (int j = 0; j < p && ok; j++) {
+            if (code & kLeafBit) { ok = false; break; }
+            const float4 c = rec[code / 16u + 3u];
+            code = __float_as_uint(((prefix >> (p - 1 - j)) & 1u) ? c.y : c.x);
+        }
+        if (code & kLeafBit) ok = false;
+        for (int q = 0; q < 4; q++) top[4u * idx + q] = ok ? rec[code / 16u + q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    if (code & kLeafBit) ok = false;
-    for (int q = 0; q < 4; q++) top[4u * idx + q] = ok ? rec[code / 16u + q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
 // Two-level records (PROG_QUAD, bvhWalkQuads in pt_device.h): per inner node n (by inner rank r,
