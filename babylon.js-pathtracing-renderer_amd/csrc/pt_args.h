@@ -38,10 +38,10 @@ __host__ __device__ inline uint32_t pairCode(float rankCode, uint32_t leafBase)
 // 0..kTopLevels, by path, after the leaf records
 constexpr int kTrailMaxDepth = 28;
 #ifndef PT_TOP_LEVELS
-#define PT_TOP_LEVELS 7
+#define PT_TOP_LEVELS 11
 #endif
 constexpr int kTopLevels = PT_TOP_LEVELS;
-constexpr unsigned kTopEntries = (2u << kTopLevels) - 1u;   // 255 record copies (64 B), heap order
+constexpr unsigned kTopEntries = (2u << kTopLevels) - 1u;   // 4095 record copies (64 B, 256 KB), heap order
 
 // the BVH walk of a mesh draw (TraceArgs::bvh_walk; the program variant's thousands digit, pt_device.h)
 enum { WALK_REF = 0, WALK_PAIRS = 1, WALK_TRAIL = 2, WALK_QUAD = 3 };

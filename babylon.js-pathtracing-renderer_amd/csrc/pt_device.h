@@ -698,28 +698,28 @@ PT_D void bvhWalkQuads(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
 // The child-pair records walked without a stack in memory (PT_BVH_TRAIL; north_star's "stackless
 // BVH traversal"): the ordered near-first walk of js/GLTFModelPathTracing_FragmentShader.js:211-298
 // keeps, per depth d of the current path (bit 31 - d of a register; the root's bit 31 has none),
-//   trail  0: both children were hit and the near one is being walked - the far one is pending
-//             (the reference's stack entry); 1: the level's last child is being walked (the far one
-//             after its pop, or the only one hit);
+//   pend   1: both children were hit and the near one is being walked - the far one is pending (the
+//             reference stack's entry); the restart trail's 0 bits (Laine 2010), kept inverted so that
+//             a pop is two operations: the deepest pending level is pend's lowest set bit;
 //   dir    which child the path took: 1 = B (the right link), 0 = A (the left child n + 1).
-// A pop is arithmetic on the trail: the deepest pending level at or above the current depth
-// becomes its far child, everything below it is cleared ((trail & -L) + L; a carry into the root's
-// bit ends the walk). The pending levels' (tNear, code) entries - the reference stack's contents -
-// are kept in a per-lane ring of R LDS slots that drops its oldest (shallowest) entry when full; when
-// a pop finds the ring empty the walk restarts: it jumps to the deepest level of a jump table of the
-// top kTopLevels levels' inner records (copies, indexed by the path's dir bits, so the jump is no
-// load of its own) and descends along the dir bits to the pending level's parent, testing on the way
-// the pending siblings' boxes to refill the ring. The boxes are the same floats tested by the same
-// function, so a re-tested entry carries the bits it was pushed with, and the walk visits the
-// reference walk's nodes in its order: same hit, same counters (restart descents are no node fetches
-// of the reference's). The host gives it trees of depth <= 28, whose nodes have one parent each
-// (pt_pairs_depth): there at most 27 far children are ever pending, so the reference's stack
-// (stackLevels[28]) never overflows and no push is dropped; other trees keep the stack walk.
+// A pop clears the deepest pending level's bit and flips its dir bit: its far child is next. The
+// pending levels' (tNear, code) entries - the reference stack's contents - are kept in a per-lane ring
+// of R LDS slots (R - 1 of them live, the free one takes every step's push store without a branch)
+// that drops its oldest (shallowest) entry when full; when a pop finds the ring empty the walk
+// restarts (trailRestart): it jumps to a copy of the deepest ancestor held in the jump table of the
+// top kTopLevels levels' inner records (indexed by the path's dir bits, so the jump is no load of its
+// own) and descends along the dir bits to the pending level's parent, testing on the way the pending
+// siblings' boxes to refill the ring. The boxes are the same floats tested by the same function, so a
+// re-tested entry carries the bits it was pushed with, and the walk visits the reference walk's nodes
+// in its order: same hit, same counters (restart descents are no node fetches of the reference's).
+// The host gives it trees of depth <= 28, whose nodes have one parent each (pt_pairs_depth): there
+// at most 27 far children are ever pending, so the reference's stack (stackLevels[28]) never
+// overflows and no push is dropped; other trees keep the stack walk.
 struct TrailWalk {
     uint32_t code;             // record to load next
     float hitT;
     float triID, triU, triV;
-    uint32_t trail, dir;       // per depth d: bit 31 - d
+    uint32_t pend, dir;        // per depth d: bit 31 - d
     uint32_t lvl;              // the bit of the depth of the node `code` addresses (root: bit 31)
     int rtop, rcnt;            // ring: next slot, entries held (at most R - 1: slot rtop is always free)
     bool pop, lookup;
@@ -763,7 +763,7 @@ PT_D float2 trailRestart(const TraceArgs& a, const PairBufs& b, f3 O, f3 inv, bo
         l >>= 1;
         const bool takeB = (w.dir & l) != 0u;
         if (l == w.lvl) return make_float2(takeB ? tB : tA, takeB ? r3.y : r3.x);   // the far child popped
-        ringPush<R>(ring, stride, slot, w, !(w.trail & l), takeB ? tA : tB, takeB ? r3.x : r3.y);   // a pending sibling
+        ringPush<R>(ring, stride, slot, w, (w.pend & l) != 0u, takeB ? tA : tB, takeB ? r3.x : r3.y);   // a pending sibling
         code = __float_as_uint(takeB ? r3.y : r3.x);
     }
 }
@@ -774,9 +774,9 @@ PT_D bool trailWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 in
                         lds_float2* ring, unsigned stride, unsigned slot, TrailWalk& w, BvhResult& r)
 {
     if (w.pop) {
-        w.trail = (w.trail & (0u - w.lvl)) + w.lvl;    // the deepest pending level at or above this one
-        if (w.trail & kRootBit) return false;          // none: the walk is over
-        w.lvl = w.trail & (0u - w.trail);
+        if (w.pend == 0u) return false;                // no level pending: the walk is over
+        w.lvl = w.pend & (0u - w.pend);                // the deepest pending level
+        w.pend ^= w.lvl;
         w.dir ^= w.lvl;                                // its far child
         w.rtop = (w.rtop == 0 ? R : w.rtop) - 1;       // (moving an empty ring's top is harmless)
         vf2 e = ring[(unsigned)w.rtop * stride + slot];
@@ -813,7 +813,7 @@ PT_D bool trailWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 in
         const uint32_t bk = w.lvl >> 1;
         ringPush<R>(ring, stride, slot, w, both, tF, sw ? r3.x : r3.y);
         const bool takeB = hitN ? sw : !sw;
-        w.trail |= both ? 0u : bk;
+        w.pend |= both ? bk : 0u;
         w.dir = takeB ? (w.dir | bk) : (w.dir & ~bk);
         w.code = __float_as_uint(takeB ? r3.y : r3.x);
         w.lvl = (hitN || hitF) ? bk : w.lvl;
@@ -835,7 +835,7 @@ PT_D void bvhWalkTrail(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     TrailWalk w;
     w.code = a.bvh_root_code; w.hitT = hitT;
     w.triID = 0.0f; w.triU = 0.0f; w.triV = 0.0f;
-    w.trail = 0u; w.dir = 0u; w.lvl = kRootBit; w.rtop = 0; w.rcnt = 0;
+    w.pend = 0u; w.dir = 0u; w.lvl = kRootBit; w.rtop = 0; w.rcnt = 0;
     w.pop = !(curT < hitT);
     w.lookup = false;
     const bool fast = pairWalkFast(O, inv);
