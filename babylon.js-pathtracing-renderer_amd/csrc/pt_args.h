@@ -10,7 +10,14 @@ namespace pt {
 
 constexpr int kBlock = 256;          // 4 waves; a block shades a 16x16 pixel tile
 constexpr int kTile = 16;            // tile edge == row-band height used for sharding
-constexpr int kWaveLogSlots = 12;    // experiment builds: u64 per workgroup in TraceArgs::wave_log
+constexpr int kWaveLogSlots = 12;
+// split tiles (pt_trace, longest-first): each 8x8 quadrant of a split 16x16 tile is shaded by this
+// many waves, of 64 / kSplitParts lanes each (4: 4x4-pixel waves of 16 lanes; 16: one 2x2 quad each)
+#ifndef PT_SPLIT_PARTS
+#define PT_SPLIT_PARTS 4
+#endif
+constexpr unsigned kSplitParts = PT_SPLIT_PARTS;
+static_assert(kSplitParts == 4 || kSplitParts == 16, "split quadrants into 4x4 or 2x2 blocks");    // experiment builds: u64 per workgroup in TraceArgs::wave_log
 constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing_FragmentShader.js:95
 #ifndef PT_STACK_LDS
 #define PT_STACK_LDS 7

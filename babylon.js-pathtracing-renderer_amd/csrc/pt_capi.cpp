@@ -642,7 +642,7 @@ int render_trace(DevFx* fx, DevTex* target)
     {   // experiment builds: the wave timeline of the last megakernel draw (pt_debug_wave_log)
         static size_t cap = 0;
         const size_t tx = (size_t)((target->w + pt::kTile - 1) / pt::kTile);   // + split tiles' padding rows
-        const size_t need = (tx * bands_owned(c, target->h) * 4 + 12 * (size_t)c->split_tiles + 4 * tx) * pt::kWaveLogSlots;
+        const size_t need = (tx * bands_owned(c, target->h) * 4 + (4 * pt::kSplitParts - 4) * (size_t)c->split_tiles + 4 * tx) * pt::kWaveLogSlots;
         if (cap < need) { if (g_wave_log) hipFree(g_wave_log); hipMalloc(&g_wave_log, need * 8); cap = need; }
         hipMemsetAsync(g_wave_log, 0, need * 8, c->stream);   // padding workgroups leave zero rows
         g_wave_log_n = need / pt::kWaveLogSlots;
@@ -676,7 +676,8 @@ int render_trace(DevFx* fx, DevTex* target)
                           c->lpt_key_prog == fx->prog && c->lpt_key_part == c->part && c->lpt_key_parts == c->num_parts;
     const unsigned split = (c->backend == PT_BACKEND_MEGAKERNEL && c->lpt && !c->counting && lpt_same)
                                ? (unsigned)std::min<size_t>(c->split_tiles, n_tiles) & ~7u : 0u;   // the cap
-    const int gy_grid = gy + (int)((12u * split + 4u * gx - 1) / (4u * gx));
+    const unsigned extra = 4u * pt::kSplitParts - 4u;   // more workgroups per split tile
+    const int gy_grid = gy + (int)((extra * split + 4u * gx - 1) / (4u * gx));
     if (c->backend == PT_BACKEND_MEGAKERNEL && mesh) {
         const size_t lanes = (size_t)gx * gy_grid * pt::kBlock;
         if (lanes * (pt::kStackLevels - pt::kStackLdsMin) > 0xffffffffull)   // 32-bit slab index

@@ -213,13 +213,14 @@ PT_D bool tracePlace(const TraceArgs& a, int lane, bool first, TracePlace& pl)
         const unsigned K = (a.order && a.split) ? *a.split : 0u;   // chosen by pt_order_build
         const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
         unsigned slot;
-        if (L < 16u * K) {
-            const unsigned g = L >> 7, r = L & 127u;
+        constexpr unsigned kPer = 4u * kSplitParts;   // workgroups per split tile
+        if (L < kPer * K) {
+            const unsigned g = L / (8u * kPer), r = L % (8u * kPer);
             slot = g * 8u + (r & 7u);
-            wave = (int)(r >> 5);
-            part = (int)((r >> 3) & 3u);
+            wave = (int)((r >> 3) / kSplitParts);
+            part = (int)((r >> 3) % kSplitParts);
         } else {
-            const unsigned L2 = L - 16u * K;
+            const unsigned L2 = L - kPer * K;
             if (L2 >= 4u * (ntiles - K)) return false;
             const unsigned g = L2 >> 5, r = L2 & 31u;
             const unsigned T = min(8u, ntiles - K - g * 8u);
@@ -240,9 +241,14 @@ PT_D bool tracePlace(const TraceArgs& a, int lane, bool first, TracePlace& pl)
         tx = (int)(blockIdx.x >> 2);
         bY = blockIdx.y;
     }
-    // lane bits (x0, y0, x1, x2, y1, y2) of an 8x8 block, or (x0, y0, x1, y1) of a split tile's 4x4
-    const int lx = part < 0 ? (lane & 1) | ((lane >> 1) & 6) : (part & 1) * 4 + ((lane & 1) | ((lane >> 1) & 2));
-    const int ly = part < 0 ? ((lane >> 1) & 1) | ((lane >> 3) & 6) : (part >> 1) * 4 + (((lane >> 1) & 1) | ((lane >> 2) & 2));
+    // lane bits (x0, y0, x1, x2, y1, y2) of an 8x8 block, (x0, y0, x1, y1) of a split tile's 4x4, or
+    // (x0, y0) of its 2x2 quads
+    int lx, ly;
+    if (part < 0) { lx = (lane & 1) | ((lane >> 1) & 6); ly = ((lane >> 1) & 1) | ((lane >> 3) & 6); }
+    else if (kSplitParts == 4) {
+        lx = (part & 1) * 4 + ((lane & 1) | ((lane >> 1) & 2));
+        ly = (part >> 1) * 4 + (((lane >> 1) & 1) | ((lane >> 2) & 2));
+    } else { lx = (part & 3) * 2 + (lane & 1); ly = (part >> 2) * 2 + ((lane >> 1) & 1); }
     const int band = (int)bY * a.num_parts + a.part;            // global 16-row band of this block
     pl.px = tx * kTile + (wave & 1) * 8 + lx;
     pl.py = band * kTile + (wave >> 1) * 8 + ly;
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
 
     // lanes whose whole 2x2 quad lies beyond the (even-rounded) target do no work; quad helpers
     // that only complete a quad at an odd edge are shaded like GL helper invocations
-    const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1) && (pl.part < 0 || lane < 16);
+    const bool active = px < ((a.width + 1) & ~1) && py < ((a.height + 1) & ~1) && (pl.part < 0 || lane < (int)(64u / kSplitParts));
     Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
 #ifdef PT_SECPROF
     __shared__ unsigned long long lds_sec[16];
@@ -305,7 +311,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     const int lane2 = kTraceBlock == 64 ? laneAgain() : (int)(threadIdx.x & 63u);
     tracePlace(a, lane2, false, pl);
     const int px2 = pl.px, py2 = pl.py;
-    const bool active2 = px2 < ((a.width + 1) & ~1) && py2 < ((a.height + 1) & ~1) && (pl.part < 0 || lane2 < 16);
+    const bool active2 = px2 < ((a.width + 1) & ~1) && py2 < ((a.height + 1) & ~1) && (pl.part < 0 || lane2 < (int)(64u / kSplitParts));
     const GOut g = (GOutLds<kTraceBlock>{ (lds_float*)lds_gout, kTraceBlock == 64 ? (unsigned)lane2 : threadIdx.x }).load();
 #else
     const int lane2 = lane, px2 = px, py2 = py;
