@@ -507,20 +507,11 @@ PT_D bool pairWalkFast(f3 O, f3 inv)
 {
     return finite3(O) && finite3(inv) && inv.x != 0.0f && inv.y != 0.0f && inv.z != 0.0f;
 }
-// one step; false once the stack has run empty (the walk is over)
+// the record part of a step: w.code's record, its children tested (push / next) or its triangle
 template <class Stk>
-PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv, bool dbl, bool fast, Stk& st,
-                       PairWalk& w, BvhResult& r)
+PT_D void pairWalkRecord(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv, bool dbl, bool fast, Stk& st,
+                         PairWalk& w, BvhResult& r)
 {
-    if (w.pop) {
-        w.sp--;
-        if (w.sp < 0) return false;
-        const float2 e = stackPop(st, w.sp, make_float2(kINF, 0.0f));
-        if (e.x >= w.hitT) return true;
-        w.code = __float_as_uint(e.y);
-        r.nodes++;
-    }
-    w.pop = true;
     // one set of loads for either kind of record (both live in one array): a wave whose lanes sit
     // at inner and at leaf nodes issues 4 vector-memory instructions, not 4 + 3 (the address and
     // data units cost ~17 cycles per wave-instruction however few lanes are active).
@@ -560,7 +551,7 @@ PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv
         if (hitN && hitF) { stackPush(a, st, w.sp, make_float2(tF, cF), r.ovf); w.sp++; }
         w.code = __float_as_uint(hitN ? cN : hitF ? cF : __uint_as_float(w.code));
         w.pop = !(hitN || hitF);
-        return true;
+        return;
     }
     r.leaves++;
     float tu, tv;
@@ -569,6 +560,22 @@ PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv
     // a use on this side too keeps the codes' load with the other three: sunk into the inner-node
     // branch, it was issued only after a mixed wave's leaf tests (-3 % kernel time)
     asm volatile("" ::"v"(r3.x));
+}
+// one step; false once the stack has run empty (the walk is over)
+template <class Stk>
+PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv, bool dbl, bool fast, Stk& st,
+                       PairWalk& w, BvhResult& r)
+{
+    if (w.pop) {
+        w.sp--;
+        if (w.sp < 0) return false;
+        const float2 e = stackPop(st, w.sp, make_float2(kINF, 0.0f));
+        if (e.x >= w.hitT) return true;
+        w.code = __float_as_uint(e.y);
+        r.nodes++;
+    }
+    w.pop = true;
+    pairWalkRecord(a, b, O, D, inv, dbl, fast, st, w, r);
     return true;
 }
 template <class Stk>
@@ -579,7 +586,67 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     pairWalkBegin(w, a.bvh_root_code, curT, hitT);
     const bool fast = pairWalkFast(O, inv);
     const PairBufs b = pairBufs(a);
+#ifndef PT_STEP_LOOP
+    // One loop exit (the empty stack), and the walk's flags as integers in VGPRs: a bool lives in an
+    // SGPR lane mask that every divergent merge rebuilds (s_andn2 / s_and / s_or per flag per merge;
+    // 73 -> 45 scalar instructions in the loop, dragon stand-in -1.3 %). A pop is a
+    // predicated LDS read; a culled pop skips the rest of its step. PT_STEP_LOOP builds the round-2
+    // loop over pairWalkStep for A/B.
 #ifdef PT_SECPROF
+    r.steps = 0;
+#endif
+    {
+        uint32_t code = w.code;
+        float hT = w.hitT;
+        int sp = 0;
+        int pop = w.pop ? 1 : 0;
+        float tID = -1.0f, tU = 0.0f, tV = 0.0f;
+        for (;;) {
+            asm volatile("" : "+v"(pop));
+            const int sp2 = sp - pop;
+            if (sp2 < 0) break;
+#ifdef PT_SECPROF
+            r.steps++;
+#endif
+            sp = sp2;
+            const float2 e = stackPop(st, pop ? sp2 : 0, make_float2(kINF, 0.0f));
+            const bool live = !pop || e.x < hT;
+            if (pop && live) r.nodes++;
+            code = pop ? __float_as_uint(e.y) : code;
+            pop = 1;
+            if (!live) continue;
+            const uint32_t off = code & ~kLeafBit;
+            const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
+            const float2 r3 = ldRec2(b.rec, off + 48u);
+            if (!(code & kLeafBit)) {
+                r.nodes += 2;
+                float tA, tB;
+                if (fast) {
+                    tA = boxFast(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
+                    tB = boxFast(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+                } else {
+                    tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
+                    tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
+                }
+                const bool sw = tB < tA;
+                const float tN = sw ? tB : tA, tF = sw ? tA : tB;
+                const float cN = sw ? r3.y : r3.x, cF = sw ? r3.x : r3.y;
+                const bool hitN = tN < hT, hitF = tF < hT;
+                if (hitN && hitF) { stackPush(a, st, sp, make_float2(tF, cF), r.ovf); sp++; }
+                code = __float_as_uint(hitN ? cN : hitF ? cF : __uint_as_float(code));
+                pop = (hitN || hitF) ? 0 : 1;
+            } else {
+                r.leaves++;
+                float tu, tv;
+                const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
+                if (d < hT) { hT = d; tID = 8.0f * r2.y; tU = tu; tV = tv; }
+                asm volatile("" ::"v"(r3.x));
+            }
+        }
+        w.hitT = hT;
+        if (tID >= 0.0f) { w.lookup = true; w.triID = tID; w.triU = tU; w.triV = tV; }
+    }
+#elif defined(PT_SECPROF)
     r.steps = 0;
     while (pairWalkStep(a, b, O, D, inv, dbl, fast, st, w, r)) r.steps++;
 #else
