@@ -304,7 +304,8 @@ __global__ __launch_bounds__(256) void pt_output(OutputArgs a, int tiles_x, int 
 //   pass 2  per 1024-node block counts; the host scans them
 //   pass 3  dense ranks -> rank codes: inner rank, or -1 - leaf rank
 //   pass 4  inner records (64 B): A.min.xyz A.max.x | A.max.yz B.min.xy | B.min.z B.max.xyz |
-//           codeA codeB (pairCode: record byte offsets, float bits); leaf records (48 B): v0, e1 = v1 - v0, e2 = v2 - v0, idObject
+//           codeA codeB (pairLineWrite; pairCode: record byte offsets, float bits); leaf records (48 B):
+//           v0, e1 = v1 - v0, e2 = v2 - v0, idObject
 constexpr int kPairsBlock = 1024;   // nodes per scan block (256 threads x 4)
 
 __global__ __launch_bounds__(256) void pt_pairs_kinds(const float4* aabb, long long texels, unsigned nrec,
@@ -394,9 +395,7 @@ __global__ __launch_bounds__(256) void pt_pairs_build(const float4* aabb, long l
         const float4 a0 = fetch32(aabb, texels, idA * 2.0f), a1 = fetch32(aabb, texels, idA * 2.0f + 1.0f);
         const float4 b0 = fetch32(aabb, texels, idB * 2.0f), b1 = fetch32(aabb, texels, idB * 2.0f + 1.0f);
         float4* o = inner_rec + 4ull * (unsigned)code[n];
-        o[0] = make_float4(a0.y, a0.z, a0.w, a1.y);
-        o[1] = make_float4(a1.z, a1.w, b0.y, b0.z);
-        o[2] = make_float4(b0.w, b1.y, b1.z, b1.w);
+        pairLineWrite(o, a0, a1, b0, b1);
         o[3] = make_float4(__uint_as_float(pairCode(code[n + 1u], leaf_base)),
                            __uint_as_float(pairCode(code[(unsigned)idB], leaf_base)), 0.0f, 0.0f);
     } else if (leafref[n]) {
@@ -483,9 +482,7 @@ PT_D void quadPairLine(const float4* aabb, long long texels, const float* code, 
     const float idA = fm + 1.0f, idB = c1.x;
     const float4 a0 = fetch32(aabb, texels, idA * 2.0f), a1 = fetch32(aabb, texels, idA * 2.0f + 1.0f);
     const float4 b0 = fetch32(aabb, texels, idB * 2.0f), b1 = fetch32(aabb, texels, idB * 2.0f + 1.0f);
-    o[0] = make_float4(a0.y, a0.z, a0.w, a1.y);
-    o[1] = make_float4(a1.z, a1.w, b0.y, b0.z);
-    o[2] = make_float4(b0.w, b1.y, b1.z, b1.w);
+    pairLineWrite(o, a0, a1, b0, b1);
     o[3] = make_float4(__uint_as_float(quadCode(code, inner, m + 1u, mOff, 1u)),
                        __uint_as_float(quadCode(code, inner, (unsigned)idB, mOff, 2u)), 0.0f, 0.0f);
 }
