@@ -665,6 +665,9 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     pairWalkBegin(w, a.bvh_root_code, curT, hitT);
     const bool fast = pairWalkFast(O, inv);
     const PairBufs b = pairBufs(a);
+#ifndef PT_CODES
+#define PT_CODES 0
+#endif
 #ifndef PT_STEP_LOOP
     // One loop exit (the empty stack), and the walk's flags as integers in VGPRs: a bool lives in an
     // SGPR lane mask that every divergent merge rebuilds (s_andn2 / s_and / s_or per flag per merge;
@@ -696,15 +699,26 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
             if (!live) continue;
             const uint32_t off = code & ~kLeafBit;
             const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
+#if PT_CODES == 0
             const float2 r3 = ldRec2(b.rec, off + 48u);
+#elif PT_CODES == 1   // experiment: the codes' load by the lanes at inner nodes only
+            float2 r3 = make_float2(0.0f, 0.0f);
+            uint32_t c2 = code;
+            asm volatile("" : "+v"(c2));   // an opaque copy: this branch is not merged with the inner/leaf one below,
+            if (!(c2 & kLeafBit)) r3 = ldRec2(b.rec, off + 48u);   // so the load is not sunk past the leaf tests
+#endif
             if (!(code & kLeafBit)) {
                 r.nodes += 2;
                 float tA, tB;
                 pairBoxes(r0, r1, r2, O, inv, fast, tA, tB);
                 const bool sw = tB < tA;
                 const float tN = sw ? tB : tA, tF = sw ? tA : tB;
-                const float cN = sw ? r3.y : r3.x, cF = sw ? r3.x : r3.y;
                 const bool hitN = tN < hT, hitF = tF < hT;
+#if PT_CODES == 2   // experiment: the codes' load by the lanes that take a child only, after the box tests
+                float2 r3 = make_float2(0.0f, 0.0f);
+                if (hitN || hitF) r3 = ldRec2(b.rec, off + 48u);
+#endif
+                const float cN = sw ? r3.y : r3.x, cF = sw ? r3.x : r3.y;
                 if (hitN && hitF) { stackPush(a, st, sp, make_float2(tF, cF), r.ovf); sp++; }
                 code = __float_as_uint(hitN ? cN : hitF ? cF : __uint_as_float(code));
                 pop = (hitN || hitF) ? 0 : 1;
@@ -713,7 +727,9 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
                 float tu, tv;
                 const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
                 if (d < hT) { hT = d; tID = 8.0f * r2.y; tU = tu; tV = tv; }
+#if PT_CODES == 0
                 asm volatile("" ::"v"(r3.x));
+#endif
             }
         }
         w.hitT = hT;
