@@ -387,7 +387,7 @@ def multipart_child(args, world, W, Hh):
            "--devices", ",".join(str(d) for d in range(world)), "--size", "%dx%d" % (W, Hh), "--workload", args.workload,
            "--steps", str(steps), "--warmup", str(min(args.warmup, 10)), "--cpu-budget", "0", "--no-pmc"]
     try:
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150)
         if r.returncode != 0:
             return {"error": "exit %d: %s" % (r.returncode, r.stderr[-300:])}
         d = json.loads(r.stdout.strip().splitlines()[-1])
