@@ -50,6 +50,21 @@ constexpr int kTrailMaxDepth = 28;
 constexpr int kTopLevels = PT_TOP_LEVELS;
 constexpr unsigned kTopEntries = (2u << kTopLevels) - 1u;   // 4095 record copies (64 B, 256 KB), heap order
 
+// Implicit top levels of the child-pair walk (experiment, PT_HEAP_LEVELS = H > 0): a copy of each
+// node at depth < H in heap order (slot 0 the root, the children of slot s at 2s + 1 and 2s + 2),
+// 64 B per slot after the jump table - an inner node's record (its children's boxes, their codes), or
+// a leaf's record with a NaN in its last float (boxes are NaN-free: the marker tells the kinds
+// apart). A step at a slot above the bottom level (depth H - 1) loads 48 B: its children's codes are
+// implicit; the bottom level's children continue in the record array by the codes in its slot.
+// Codes of slots: kHeapBit | slot (record offsets stay below 2^30).
+#ifndef PT_HEAP_LEVELS
+#define PT_HEAP_LEVELS 0
+#endif
+constexpr int kHeapLevels = PT_HEAP_LEVELS;
+constexpr uint32_t kHeapBit = 0x40000000u;
+constexpr unsigned kHeapSlots = kHeapLevels > 0 ? (1u << kHeapLevels) - 1u : 0u;
+constexpr unsigned kHeapBottom = kHeapLevels > 0 ? (1u << (kHeapLevels - 1)) - 1u : 0u;   // first slot of depth H - 1
+
 // the BVH walk of a mesh draw (TraceArgs::bvh_walk; the program variant's thousands digit, pt_device.h)
 enum { WALK_REF = 0, WALK_PAIRS = 1, WALK_TRAIL = 2, WALK_QUAD = 3 };
 
@@ -142,6 +157,7 @@ struct TraceArgs {
                                // every segment reads SGPRs instead of waiting on a load
     uint32_t bvh_pairs_bytes;  // size of the record array (its buffer descriptor)
     uint32_t bvh_top_base;     // PROG_TRAIL: byte offset of the restart jump table (inner-record copies) in it
+    uint32_t bvh_heap_base;    // PT_HEAP_LEVELS builds: byte offset of the implicit top levels in it (0: none)
     int bvh_walk;              // WALK_REF / _PAIRS / _TRAIL / _QUAD (pt_device.h): the variant the draw takes
     const float4* bvh_quads;   // PROG_QUAD: the two-level records (192 B per inner node)
     uint32_t bvh_quads_bytes;

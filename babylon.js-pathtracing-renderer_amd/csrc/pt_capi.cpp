@@ -86,6 +86,7 @@ struct DevTex {
     float pairs_root_box[6] = {};
     uint32_t pairs_bytes = 0;   // inner records, then leaf records from pairs_leaf on, then the jump table
     uint32_t pairs_top = 0;     // byte offset of the restart-trail jump table; 0: the tree is not walkable by the trail
+    uint32_t pairs_heap = 0;    // PT_HEAP_LEVELS builds: byte offset of the implicit top levels (0: none)
     void* quads_mem = nullptr;  // the two-level records (PT_BVH_QUADS; built with the pairs when that walk is asked for)
     uint32_t quads_bytes = 0, quads_root = 0;
     const DevTex* pairs_tri = nullptr;
@@ -470,6 +471,7 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
     t->quads_bytes = 0;
     t->pairs_ok = false;
     t->pairs_top = 0;
+    t->pairs_heap = 0;
     t->pairs_gen = t->gen; t->pairs_tri = tri; t->pairs_tri_gen = tri->gen;
     const unsigned nrec = (unsigned)((texels + 1) / 2);
     const unsigned nblk = (nrec + 1023) / 1024;
@@ -514,7 +516,8 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
         }
         leaf_base = (unsigned)al(n_inner * 64);
         const size_t top_base = leaf_base + al(n_leaf * 48);
-        e = hipMalloc(&t->pairs_mem, top_base + pt::kTopEntries * 64 + 256);
+        const size_t heap_base = top_base + al(pt::kTopEntries * 64);
+        e = hipMalloc(&t->pairs_mem, heap_base + (size_t)pt::kHeapSlots * 64 + 256);
         if (e == hipSuccess) {
             t->pairs_inner = (const float4*)t->pairs_mem;
             t->pairs_leaf = (const float4*)((char*)t->pairs_mem + leaf_base);
@@ -536,11 +539,17 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
         t->pairs_root = pt::pairCode(root, leaf_base);
         const float box6[6] = { node0[1], node0[2], node0[3], node0[5], node0[6], node0[7] };
         std::memcpy(t->pairs_root_box, box6, sizeof(box6));
-        t->pairs_bytes = (uint32_t)(top_base + pt::kTopEntries * 64);
+        t->pairs_bytes = (uint32_t)(heap_base + (size_t)pt::kHeapSlots * 64);
         // the restart trail's jump table, for trees it can walk (one parent per node, depth <= 28)
         if (e == hipSuccess && !notrail) {
             e = tpass(3, t->pairs_root);
             if (e == hipSuccess) t->pairs_top = (uint32_t)top_base;
+        }
+        // the implicit top levels (PT_HEAP_LEVELS builds)
+        if (e == hipSuccess && pt::kHeapSlots > 0) {
+            e = pt_launch_trail_pass(4, aabb, texels, nrec, inner, parent, refs, c->d_err + 2, t->pairs_inner, t->pairs_root,
+                                     (float4*)((char*)t->pairs_mem + heap_base), c->stream);
+            if (e == hipSuccess) t->pairs_heap = (uint32_t)heap_base;
         }
         // the two-level records, when that walk is asked for (192 B per inner node + a leaf root's line)
         const size_t qbytes = n_inner * 192 + 64;
@@ -622,6 +631,7 @@ int render_trace(DevFx* fx, DevTex* target)
             std::memcpy(a.bvh_root_box, bvh->pairs_root_box, sizeof(a.bvh_root_box));
             a.bvh_pairs_bytes = bvh->pairs_bytes;
             a.bvh_top_base = c->bvh_layout == PT_BVH_TRAIL ? bvh->pairs_top : 0u;
+            a.bvh_heap_base = c->bvh_layout == PT_BVH_PAIRS ? bvh->pairs_heap : 0u;
             if (c->bvh_layout == PT_BVH_QUADS && bvh->quads_mem) {
                 a.bvh_quads = (const float4*)bvh->quads_mem;
                 a.bvh_quads_bytes = bvh->quads_bytes;

@@ -662,11 +662,18 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
                        BvhResult& r)
 {
     PairWalk w;
+#if PT_HEAP_LEVELS > 0
+    pairWalkBegin(w, a.bvh_heap_base ? kHeapBit : a.bvh_root_code, curT, hitT);   // slot 0: the root
+#else
     pairWalkBegin(w, a.bvh_root_code, curT, hitT);
+#endif
     const bool fast = pairWalkFast(O, inv);
     const PairBufs b = pairBufs(a);
 #ifndef PT_CODES
 #define PT_CODES 0
+#endif
+#if defined(PT_STEP_LOOP) && PT_HEAP_LEVELS > 0
+#error "PT_HEAP_LEVELS needs the one-exit step loop"
 #endif
 #ifndef PT_STEP_LOOP
     // One loop exit (the empty stack), and the walk's flags as integers in VGPRs: a bool lives in an
@@ -683,10 +690,16 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
         int sp = 0;
         int pop = w.pop ? 1 : 0;
         float tID = -1.0f, tU = 0.0f, tV = 0.0f;
+#if PT_HEAP_LEVELS > 0
+        unsigned guard = 0;   // experiment builds: a bound no walk reaches, so that a layout bug cannot hang the GPU
+#endif
         for (;;) {
             asm volatile("" : "+v"(pop));
             const int sp2 = sp - pop;
             if (sp2 < 0) break;
+#if PT_HEAP_LEVELS > 0
+            if (++guard > (1u << 20)) { atomicOr(a.err, (unsigned)E_STACK); break; }
+#endif
 #ifdef PT_SECPROF
             r.steps++;
 #endif
@@ -697,9 +710,22 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
             code = pop ? __float_as_uint(e.y) : code;
             pop = 1;
             if (!live) continue;
+#if PT_HEAP_LEVELS > 0
+            const bool heap = (code & kHeapBit) != 0;
+            const uint32_t slot = code & (kHeapBit - 1u);
+            const uint32_t off = heap ? a.bvh_heap_base + slot * 64u : code & ~kLeafBit;
+#else
             const uint32_t off = code & ~kLeafBit;
+#endif
             const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
-#if PT_CODES == 0
+#if PT_HEAP_LEVELS > 0
+            // the children's codes: in the record array's records and the heap's bottom slots; implicit above
+            float2 r3 = make_float2(0.0f, 0.0f);
+            uint32_t c2 = code;
+            asm volatile("" : "+v"(c2));   // (an opaque copy: the load is not sunk past the leaf tests)
+            if (!(c2 & kHeapBit) || (c2 & (kHeapBit - 1u)) >= kHeapBottom) r3 = ldRec2(b.rec, off + 48u);
+            const bool leaf = heap ? !(r2.w == r2.w) : (code & kLeafBit) != 0;   // a leaf slot's NaN marker
+#elif PT_CODES == 0
             const float2 r3 = ldRec2(b.rec, off + 48u);
 #elif PT_CODES == 1   // experiment: the codes' load by the lanes at inner nodes only
             float2 r3 = make_float2(0.0f, 0.0f);
@@ -707,7 +733,10 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
             asm volatile("" : "+v"(c2));   // an opaque copy: this branch is not merged with the inner/leaf one below,
             if (!(c2 & kLeafBit)) r3 = ldRec2(b.rec, off + 48u);   // so the load is not sunk past the leaf tests
 #endif
-            if (!(code & kLeafBit)) {
+#if PT_HEAP_LEVELS == 0
+            const bool leaf = (code & kLeafBit) != 0;
+#endif
+            if (!leaf) {
                 r.nodes += 2;
                 float tA, tB;
                 pairBoxes(r0, r1, r2, O, inv, fast, tA, tB);
@@ -718,7 +747,14 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
                 float2 r3 = make_float2(0.0f, 0.0f);
                 if (hitN || hitF) r3 = ldRec2(b.rec, off + 48u);
 #endif
-                const float cN = sw ? r3.y : r3.x, cF = sw ? r3.x : r3.y;
+#if PT_HEAP_LEVELS > 0
+                const bool implicit = heap && slot < kHeapBottom;
+                const float cA = implicit ? __uint_as_float(kHeapBit | (2u * slot + 1u)) : r3.x;
+                const float cB = implicit ? __uint_as_float(kHeapBit | (2u * slot + 2u)) : r3.y;
+#else
+                const float cA = r3.x, cB = r3.y;
+#endif
+                const float cN = sw ? cB : cA, cF = sw ? cA : cB;
                 if (hitN && hitF) { stackPush(a, st, sp, make_float2(tF, cF), r.ovf); sp++; }
                 code = __float_as_uint(hitN ? cN : hitF ? cF : __uint_as_float(code));
                 pop = (hitN || hitF) ? 0 : 1;

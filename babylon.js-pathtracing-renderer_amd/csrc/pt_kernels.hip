@@ -464,6 +464,34 @@ __global__ __launch_bounds__(256) void pt_pairs_top(const float4* rec, uint32_t 
     }
 }
 
+// The implicit top levels (PT_HEAP_LEVELS, pt_args.h): slot idx at depth p = floor(log2(idx + 1)) is
+// the node the path of bits (idx + 1 - 2^p) reaches from the root (MSB first, 1 = the right child),
+// copied from the record array: an inner record whole, a leaf record with a NaN marker in its
+// twelfth float; zero where the path met a leaf earlier (never visited)
+__global__ __launch_bounds__(256) void pt_pairs_heap(const float4* rec, uint32_t root, float4* heap, unsigned slots)
+{
+    const unsigned idx = blockIdx.x * 256u + threadIdx.x;
+    if (idx >= slots) return;
+    const int p = 31 - __builtin_clz(idx + 1u);
+    const unsigned path = idx + 1u - (1u << p);
+    uint32_t code = root;
+    bool ok = true;
+    for (int j = 0; j < p; j++) {
+        if (code & kLeafBit) { ok = false; break; }
+        const float4 c = rec[code / 16u + 3u];
+        code = __float_as_uint(((path >> (p - 1 - j)) & 1u) ? c.y : c.x);
+    }
+    float4* o = heap + 4ull * idx;
+    const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (!ok) { o[0] = z; o[1] = z; o[2] = z; o[3] = z; return; }
+    const unsigned at = (code & ~kLeafBit) / 16u;
+    o[0] = rec[at]; o[1] = rec[at + 1u];
+    float4 r2 = rec[at + 2u];
+    if (code & kLeafBit) { r2.w = __uint_as_float(0x7fc00000u); o[3] = z; }
+    else o[3] = rec[at + 3u];
+    o[2] = r2;
+}
+
 // Two-level records (PROG_QUAD, bvhWalkQuads in pt_device.h): per inner node n (by inner rank r,
 // 192 B at r * 192) its child-pair line, then each child's own line - the child's child-pair line if
 // it is inner, its leaf triangle line if not. Codes: innerRank * 192 for an inner node, kLeafBit |
@@ -636,7 +664,8 @@ hipError_t pt_launch_pairs_pass(int pass, const float4* aabb, long long texels, 
     return hipGetLastError();
 }
 
-// the restart-trail passes: 1 links, 2 depth, 3 top (rec = the record array, top its jump table)
+// the restart-trail passes: 1 links, 2 depth, 3 top (rec = the record array, top its jump table);
+// 4 the implicit top levels of PT_HEAP_LEVELS builds
 hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, unsigned nrec, const unsigned char* inner,
                                 unsigned* parent, unsigned* refs, unsigned* flag, const float4* rec, uint32_t root,
                                 float4* top, hipStream_t s)
@@ -646,6 +675,10 @@ hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, 
     case 1: hipLaunchKernelGGL(pt::pt_pairs_links, nodes, b256, 0, s, aabb, texels, nrec, inner, parent, refs, flag); break;
     case 2: hipLaunchKernelGGL(pt::pt_pairs_depth, nodes, b256, 0, s, nrec, parent, refs, flag); break;
     case 3: hipLaunchKernelGGL(pt::pt_pairs_top, dim3(1), b256, 0, s, rec, root, top); break;
+    case 4:   // the implicit top levels (PT_HEAP_LEVELS builds; top = their first slot)
+        if (pt::kHeapSlots == 0) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(pt::pt_pairs_heap, dim3((pt::kHeapSlots + 255) / 256), b256, 0, s, rec, root, top, pt::kHeapSlots);
+        break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
