@@ -1309,10 +1309,10 @@ static void fetch_acc(const float* acc, int W, int H, int px, int py, int dx, in
     o[0] = p[0]; o[1] = p[1]; o[2] = p[2]; o[3] = p[3];
 }
 
-int pto_screen_output(int W, int H, const float* acc, float oneOverN, float exposure, uint8_t* out, int nthreads)
+/* out (RGBA8 canvas) or out_f (RGBA32F render target: the tone-mapped floats before unorm8) */
+static int screen_output(int W, int H, const float* acc, float oneOverN, float exposure, uint8_t* out, float* out_f)
 {
-    if (!acc || !out || W <= 0 || H <= 0) return -1;
-    (void)nthreads;
+    if (!acc || (!out && !out_f) || W <= 0 || H <= 0) return -1;
     /* m25 index k -> offset (dx, dy): rows dy = +2 .. -2, columns dx = -2 .. +2 */
     static const int taps5[8][3] = {
         /* first-ring tap, then its two outer taps (js/PathTracingCommon.js:82-209) */
@@ -1354,15 +1354,25 @@ int pto_screen_output(int W, int H, const float* acc, float oneOverN, float expo
             if ((cp[3] == 1.01f && oneOverN < 0.005f) || oneOverN < 0.0002f) { fr = cp[0]; fg = cp[1]; fb = cp[2]; }
             fr *= oneOverN; fg *= oneOverN; fb *= oneOverN;
             float c3[3] = { fr * exposure, fg * exposure, fb * exposure };
-            uint8_t* o = out + 4 * ((size_t)y * W + x);
             for (int k = 0; k < 3; k++) {
                 float v = g_clamp(c3[k] / (1.0f + c3[k]), 0.0f, 1.0f);
                 v = g_clamp(g_pow(v, 0.4545f), 0.0f, 1.0f);
-                o[k] = (uint8_t)floorf(v * 255.0f + 0.5f);
+                if (out) out[4 * ((size_t)y * W + x) + k] = (uint8_t)floorf(v * 255.0f + 0.5f);
+                else out_f[4 * ((size_t)y * W + x) + k] = v;
             }
-            o[3] = 255;
+            if (out) out[4 * ((size_t)y * W + x) + 3] = 255;
+            else out_f[4 * ((size_t)y * W + x) + 3] = 1.0f;
         }
     return 0;
+}
+int pto_screen_output(int W, int H, const float* acc, float oneOverN, float exposure, uint8_t* out, int nthreads)
+{
+    (void)nthreads;
+    return out ? screen_output(W, H, acc, oneOverN, exposure, out, NULL) : -1;
+}
+int pto_screen_output_f32(int W, int H, const float* acc, float oneOverN, float exposure, float* out)
+{
+    return out ? screen_output(W, H, acc, oneOverN, exposure, NULL, out) : -1;
 }
 
 /* ---------------------------------------------------------------- quadric probe */

@@ -89,6 +89,9 @@ int pto_quadric_probe(int shape, float k, const float* ro, const float* rd, floa
 /* screenOutput pass (js/PathTracingCommon.js:19-309): RGBA32F accumulation -> RGBA8 canvas. */
 int pto_screen_output(int width, int height, const float* acc, float uOneOverSampleCounter,
                       float uToneMappingExposure, uint8_t* out, int nthreads);
+/* The same pass into an RGBA32F target: the tone-mapped floats before the canvas's unorm8. */
+int pto_screen_output_f32(int width, int height, const float* acc, float uOneOverSampleCounter,
+                          float uToneMappingExposure, float* out);
 
 /* Pinned-math probes (KATs shared with the HIP self-test): op 0 exp2, 1 log2, 2 sin, 3 cos,
  * 4 atan, 5 atan2(x, y2), 6 acos, 7 pow(x, y2), 8 exp, 9 log, 10 sqrt, 11 rng stream. */

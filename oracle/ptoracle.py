@@ -73,6 +73,7 @@ def lib():
         L.pto_path_trace.argtypes = [P(Frame), ctypes.c_void_p, ctypes.c_void_p, c_i, c_i, c_i, P(Counters)]
         L.pto_gbuffer.argtypes = [P(Frame), ctypes.c_void_p, c_i, c_i, c_i]
         L.pto_screen_output.argtypes = [c_i, c_i, ctypes.c_void_p, c_f, c_f, ctypes.c_void_p, c_i]
+        L.pto_screen_output_f32.argtypes = [c_i, c_i, ctypes.c_void_p, c_f, c_f, ctypes.c_void_p]
         L.pto_math_probe.argtypes = [c_i, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
         L.pto_sky_color.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
         L.pto_quadric_probe.argtypes = [c_i, c_f, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
@@ -154,6 +155,17 @@ def screen_output(acc, one_over_n, exposure=1.0):
     rc = lib().pto_screen_output(w, h, acc.ctypes.data, one_over_n, exposure, out.ctypes.data, 0)
     if rc != 0:
         raise RuntimeError("pto_screen_output failed")
+    return out
+
+
+def screen_output_f32(acc, one_over_n, exposure=1.0):
+    """screenOutput into an RGBA32F target: the tone-mapped floats before the canvas's unorm8."""
+    acc = np.ascontiguousarray(acc, dtype=np.float32)
+    h, w = acc.shape[:2]
+    out = np.zeros((h, w, 4), dtype=np.float32)
+    rc = lib().pto_screen_output_f32(w, h, acc.ctypes.data, one_over_n, exposure, out.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("pto_screen_output_f32 failed")
     return out
 
 

@@ -96,6 +96,54 @@ def test_fast_sqrt_is_ieee_on_every_input(engine):
     assert engine.math_exhaustive(1) == 0
 
 
+@pytest.mark.parametrize("seed", [0, 1])
+def test_screen_output_adversarial_accumulation(engine, seed):
+    """screenOutput of an accumulation buffer with values across the binary32 range (denormals,
+    +-0, huge, inf, NaN, negative) and every edge flag value in alpha, drawn through the effect
+    API as the render loop does: bit-exact with the oracle's RGBA8 canvas (and the fused copy)."""
+    import babylon_pt as bp
+    rng = np.random.default_rng(seed)
+    h, w = 67, 93
+    mag = rng.choice(np.array([0.0, 1e-40, 1e-38, 3e-37, 1e-20, 1e-3, 0.5, 1.0, 3.0, 1e3, 1e30, 3e38], np.float32), size=(h, w, 3))
+    acc = (mag * rng.uniform(0.5, 2.0, size=(h, w, 3))).astype(np.float32)
+    acc *= np.where(rng.random((h, w, 3)) < 0.1, -1.0, 1.0).astype(np.float32)
+    special = rng.random((h, w, 3))
+    acc[special < 0.02] = np.inf
+    acc[(special >= 0.02) & (special < 0.03)] = np.nan
+    acc[(special >= 0.03) & (special < 0.05)] = -0.0
+    alpha = rng.choice(np.array([0.0, -1.0, 1.01, 0.5, 1.0, 2.0, np.nan], np.float32), size=(h, w))
+    frame = np.concatenate([acc, alpha[..., None]], axis=-1).astype(np.float32)
+    src = bp.RenderTargetTexture("acc", (w, h), engine)
+    dst = bp.RenderTargetTexture("copy", (w, h), engine)
+    tgt = bp.RenderTargetTexture("out", (w, h), engine)
+    src.write(frame)
+    copy = bp.EffectWrapper(engine, "screenCopy", [], ["pathTracedImageBuffer"], name="copy")
+    out = bp.EffectWrapper(engine, "screenOutput", ["uOneOverSampleCounter", "uToneMappingExposure"],
+                           ["accumulationBuffer"], name="out")
+    ren = bp.EffectRenderer(engine)
+    engine.resize_canvas(w, h)
+    for inv, exp in [(1.0, 1.0), (float(np.float32(1.0 / 7.0)), 1.7), (0.003, 1.0), (0.0001, 0.25)]:
+        copy.effect.setTexture("pathTracedImageBuffer", src)
+        out.effect.setFloat("uOneOverSampleCounter", inv)
+        out.effect.setFloat("uToneMappingExposure", exp)
+        out.effect.setTexture("accumulationBuffer", src)
+        ren.render(copy, dst)
+        ren.render(out)
+        engine.sync()
+        got = engine.read_canvas(w, h)
+        want = H.po_screen_output(frame, inv, exp)
+        assert _bits_equal(want, got), "1/N %r exposure %r: %s" % (inv, exp, _diff_report(want, got))
+        assert _bits_equal(frame, dst.read())
+        # into an RGBA32F target: the tone-mapped floats themselves
+        out.effect.setTexture("accumulationBuffer", src)
+        ren.render(out, tgt)
+        engine.sync()
+        import ptoracle as po
+        want_f = po.screen_output_f32(frame, inv, exp)
+        got_f = tgt.read()
+        assert _bits_equal(want_f, got_f), "float target, 1/N %r exposure %r: %s" % (inv, exp, _diff_report(want_f, got_f))
+
+
 def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1, split_output=False, mesh=None):
     import babylon_pt as bp
     m = None
