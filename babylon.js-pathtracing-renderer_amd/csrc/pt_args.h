@@ -23,9 +23,14 @@ constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing
 #define PT_STACK_LDS 7
 #endif
 // the child-pair walk of the texture-free mesh programs runs at 8 waves/SIMD (pt_device.h
-// kMinWaves), where 5 LDS levels (+ the scratch level) and the G-buffer fill the 160 KB of a CU
+// kMinWaves), where 6 LDS levels and the G-buffer fill the 160 KB of a CU (5 + the scratch level
+// with PT_PUSH_SCRATCH, pt_trace.h MegaStack::push)
 #ifndef PT_STACK_LDS_PAIRS
+#ifdef PT_PUSH_SCRATCH
 #define PT_STACK_LDS_PAIRS 5
+#else
+#define PT_STACK_LDS_PAIRS 6
+#endif
 #endif
 constexpr int kStackLds = PT_STACK_LDS;        // levels kept in LDS per lane; deeper levels go to a global slab
 constexpr int kStackLdsMin = PT_STACK_LDS_PAIRS < PT_STACK_LDS ? PT_STACK_LDS_PAIRS : PT_STACK_LDS;   // sizes the slab

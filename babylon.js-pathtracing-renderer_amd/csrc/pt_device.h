@@ -84,18 +84,26 @@ template <int P> constexpr int kMinWaves = kQuad<P> ? (kHasTex<P> ? PT_MINWAVES_
                                          : kHasTex<P> ? PT_MINWAVES_TEX : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
 // BVH stack levels in LDS per lane (the rest in the global slab): fewer for the 8-wave variants
 template <int P> constexpr int kStackLdsOf = (kPairs<P> && !kHasTex<P> && !kQuad<P>) ? PT_STACK_LDS_PAIRS : kStackLds;
-// the restart-trail walk's LDS ring (entries per lane): the LDS of the stack walk's levels and its
-// scratch level at 8 waves/SIMD (6 x 8 B + the 32-B G-buffer = 80 B per lane = 160 KB per CU); at 4
-// waves/SIMD the textured variants have room for 14
+// the restart-trail walk's LDS ring (entries per lane): the LDS of the stack walk's levels at 8
+// waves/SIMD (6 x 8 B + the 32-B G-buffer = 80 B per lane = 160 KB per CU); at 4 waves/SIMD the
+// textured variants have room for 14
 #ifndef PT_RING_PAIRS
-#define PT_RING_PAIRS (PT_STACK_LDS_PAIRS + 1)
+#define PT_RING_PAIRS 6
 #endif
 #ifndef PT_RING_TEX
 #define PT_RING_TEX 14
 #endif
 template <int P> constexpr int kRingOf = kHasTex<P> ? PT_RING_TEX : PT_RING_PAIRS;
-// LDS float2 slots per lane a walk of program P needs: stack levels + the scratch level, or the ring
-template <int P> constexpr int kWalkSlotsOf = kTrail<P> ? kRingOf<P> : kStackLdsOf<P> + 1;
+// the stack walk's push form (pt_trace.h MegaStack::push): a scratch level and unmasked stores for
+// the textured 4-wave variants, masked stores into one more real level where LDS caps residency
+// (the 8-wave variants); PT_PUSH_SCRATCH: the scratch form everywhere (the round-2 build)
+#ifdef PT_PUSH_SCRATCH
+template <int P> constexpr bool kScratchOf = true;
+#else
+template <int P> constexpr bool kScratchOf = !(kPairs<P> && !kHasTex<P> && !kQuad<P>);
+#endif
+// LDS float2 slots per lane a walk of program P needs: stack levels (+ the scratch level), or the ring
+template <int P> constexpr int kWalkSlotsOf = kTrail<P> ? kRingOf<P> : kStackLdsOf<P> + (kScratchOf<P> ? 1 : 0);
 
 typedef float vf2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) vf2 lds_float2;

@@ -21,7 +21,7 @@ using namespace ptg;
 namespace pt {
 
 // LS = lanes of the block = the stride of one stack level in LDS; NL = stack levels in LDS
-template <int LS, int NL>
+template <int LS, int NL, bool SCRATCH>
 struct MegaStack {
     lds_float2* lds;
     unsigned slot;
@@ -46,13 +46,19 @@ struct MegaStack {
         }
         return make_float2(e.x, e.y);
     }
-    // every lane writes LDS level min(si, NL): level NL is a scratch level that takes
-    // the deeper lanes' store, which then also goes to the slab (false beyond stackLevels[27])
+    // SCRATCH (kScratchOf): every lane writes LDS level min(si, NL), level NL being a scratch
+    // level that takes the deeper lanes' store, which then also goes to the slab - no exec-mask
+    // change. Otherwise lanes within the LDS levels store there (a masked ds_write): where LDS
+    // bounds the residency (the 8-wave variants) the scratch level's 512 B per wave is a stack
+    // level more (6 instead of 5 + scratch: dragon stand-in +1.5 %, sky + dragon +2.2 %; the
+    // textured 4-wave variants keep the scratch form, 1 % faster there).
+    // False beyond stackLevels[27].
     PT_D bool push(int si, float2 e)
     {
         const vf2 v = { e.x, e.y };
         PT_SLABCOUNT(n_put++; if (si >= NL) n_put_slab++;)
-        lds[(unsigned)min(si, NL) * LS + slot] = v;
+        if (SCRATCH) lds[(unsigned)min(si, NL) * LS + slot] = v;
+        else if (si < NL) lds[(unsigned)si * LS + slot] = v;
         if (si >= NL) {
             if (si >= kStackLevels) return false;
             slab[(unsigned)(si - NL) * stride + deep] = v;
@@ -113,7 +119,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     f3 inv = mk(grcp(D.x), grcp(D.y), grcp(D.z));
     const bool dbl = (!a.uses_albedo && a.model_mat == TRANSPARENT);
     BvhResult br = { 0.0f, 0.0f, 0.0f, false, 1u, 0u, 0u };
-    MegaStack<LS, kStackLdsOf<PROG>> st{ (lds_float2*)lds, lane_slot, (glb_float2*)a.spill, deep, a.spill_stride };
+    MegaStack<LS, kStackLdsOf<PROG>, kScratchOf<PROG>> st{ (lds_float2*)lds, lane_slot, (glb_float2*)a.spill, deep, a.spill_stride };
     if (kPairs<PROG>) {   // the root's box from the kernel arguments (the same floats as texels 0-1)
         const float* rb = a.bvh_root_box;
         const float rootT = box(mk(rb[0], rb[1], rb[2]), mk(rb[3], rb[4], rb[5]), O, inv);
@@ -267,7 +273,7 @@ PT_D int laneAgain()
 template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
 {
-    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];   // stack levels + the scratch level, or the trail walk's ring
+    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];   // stack levels (+ the scratch level, kScratchOf), or the trail walk's ring
     __shared__ float lds_gout[8 * kTraceBlock];
     const unsigned tid = threadIdx.x;
     const int lane = tid & 63;
@@ -412,7 +418,7 @@ __global__ __launch_bounds__(kBlock, kMinWaves<PROG>) void pt_persist(TraceArgs 
                                                                        unsigned n_wave_tiles, unsigned per_wave,
                                                                        unsigned refill)
 {
-    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kBlock];   // stack levels + the scratch level, or the trail walk's ring
+    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kBlock];   // stack levels (+ the scratch level, kScratchOf), or the trail walk's ring
     const unsigned tid = threadIdx.x;
     const unsigned lane = tid & 63u, wave = tid >> 6;
     const unsigned long long below = (1ull << lane) - 1ull;
