@@ -82,8 +82,18 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, int walk)
 #endif
 template <int P> constexpr int kMinWaves = kQuad<P> ? (kHasTex<P> ? PT_MINWAVES_QUAD_TEX : PT_MINWAVES_QUAD)
                                          : kHasTex<P> ? PT_MINWAVES_TEX : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
-// BVH stack levels in LDS per lane (the rest in the global slab): fewer for the 8-wave variants
-template <int P> constexpr int kStackLdsOf = (kPairs<P> && !kHasTex<P> && !kQuad<P>) ? PT_STACK_LDS_PAIRS : kStackLds;
+// G-buffer fields in LDS (pt_program.h GOutLds): the glTF / HDRI scenes' 8-wave child-pair stack
+// walk keeps 6 of the 8 (id and sharp go to the stack slab's last row) and has a seventh LDS stack
+// level in their place (dragon stand-in +1.7 %, bunny x16 +1.7 %; the sky + mesh scene, which
+// writes them more often, lost 2.8 % and keeps all 8; PT_GOUT_LDS_GLTF=8 builds the round-3 form)
+#ifndef PT_GOUT_LDS_GLTF
+#define PT_GOUT_LDS_GLTF 6
+#endif
+template <int P> constexpr bool kPairs8 = kPairs<P> && !kHasTex<P> && !kQuad<P>;
+template <int P> constexpr int kGoutLdsOf = (kPairs8<P> && !kTrail<P> && kIsGltf<P>) ? PT_GOUT_LDS_GLTF : 8;
+// BVH stack levels in LDS per lane (the rest in the global slab): fewer for the 8-wave variants,
+// one more where two G-buffer fields left LDS
+template <int P> constexpr int kStackLdsOf = kPairs8<P> ? PT_STACK_LDS_PAIRS + (8 - kGoutLdsOf<P>) / 2 : kStackLds;
 // the restart-trail walk's LDS ring (entries per lane): the LDS of the stack walk's levels at 8
 // waves/SIMD (6 x 8 B + the 32-B G-buffer = 80 B per lane = 160 KB per CU); at 4 waves/SIMD the
 // textured variants have room for 14
@@ -100,7 +110,7 @@ template <int P> constexpr int kRingOf = kHasTex<P> ? PT_RING_TEX : PT_RING_PAIR
 #ifdef PT_PUSH_SCRATCH
 template <int P> constexpr bool kScratchOf = true;
 #else
-template <int P> constexpr bool kScratchOf = !(kPairs<P> && !kHasTex<P> && !kQuad<P>);
+template <int P> constexpr bool kScratchOf = !kPairs8<P>;
 #endif
 // LDS float2 slots per lane a walk of program P needs: stack levels (+ the scratch level), or the ring
 template <int P> constexpr int kWalkSlotsOf = kTrail<P> ? kRingOf<P> : kStackLdsOf<P> + (kScratchOf<P> ? 1 : 0);

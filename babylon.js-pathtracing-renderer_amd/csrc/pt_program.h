@@ -59,12 +59,21 @@ struct GOut {
     PT_D void setSharp(float v) { sharp = v; }
 };
 typedef __attribute__((address_space(3))) float lds_float;
-template <int LS>   // lanes of the workgroup = the stride of one field
+typedef __attribute__((address_space(1))) float glb_float;
+// LS = lanes of the workgroup = the stride of one field; NF = fields kept in LDS, the rest (id,
+// sharp) in the lane's two floats at `gx` (a row of the stack slab): where LDS caps residency that
+// leaves room for one more stack level (kGoutLdsOf, pt_device.h)
+template <int LS, int NF = 8>
 struct GOutLds {
     lds_float* p;
     unsigned slot;
-    PT_D void put(int f, float v) { p[f * LS + slot] = v; }
-    PT_D float get(int f) const { return p[f * LS + slot]; }
+    glb_float* gx = nullptr;
+    PT_D void put(int f, float v)
+    {
+        if (f < NF) p[f * LS + slot] = v;
+        else gx[f - NF] = v;
+    }
+    PT_D float get(int f) const { return f < NF ? p[f * LS + slot] : gx[f - NF]; }
     PT_D void clear() { for (int f = 0; f < 8; f++) put(f, 0.0f); }
     PT_D void setNrm(f3 v) { put(0, v.x); put(1, v.y); put(2, v.z); }
     PT_D void setCol(f3 v) { put(3, v.x); put(4, v.y); put(5, v.z); }

@@ -274,7 +274,7 @@ template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
 {
     __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];   // stack levels (+ the scratch level, kScratchOf), or the trail walk's ring
-    __shared__ float lds_gout[8 * kTraceBlock];
+    __shared__ float lds_gout[kGoutLdsOf<PROG> * kTraceBlock];
     const unsigned tid = threadIdx.x;
     const int lane = tid & 63;
     const unsigned long long t_start = clock64();
@@ -299,7 +299,9 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     cnt.lane_steps = 0;
     cnt.sget = cnt.sget_slab = cnt.sput = cnt.sput_slab = 0;
 #endif
-    GOutLds<kTraceBlock> gl{ (lds_float*)lds_gout, tid };
+    // G-buffer fields beyond the LDS ones: the slab's row kStackLevels - kStackLdsMin (pt_capi.cpp spill_reserve)
+    glb_float* const gx = kGoutLdsOf<PROG> < 8 ? (glb_float*)(a.spill + (size_t)(kStackLevels - kStackLdsMin) * a.spill_stride + deep) : nullptr;
+    GOutLds<kTraceBlock, kGoutLdsOf<PROG>> gl{ (lds_float*)lds_gout, tid, gx };
     gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
     f3 r = mk(0, 0, 0);
     if (active) {
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     tracePlace(a, lane2, false, pl);
     const int px2 = pl.px, py2 = pl.py;
     const bool active2 = px2 < ((a.width + 1) & ~1) && py2 < ((a.height + 1) & ~1) && (pl.part < 0 || lane2 < (int)(64u / kSplitParts));
-    const GOut g = (GOutLds<kTraceBlock>{ (lds_float*)lds_gout, kTraceBlock == 64 ? (unsigned)lane2 : threadIdx.x }).load();
+    const GOut g = (GOutLds<kTraceBlock, kGoutLdsOf<PROG>>{ (lds_float*)lds_gout, kTraceBlock == 64 ? (unsigned)lane2 : threadIdx.x, gx }).load();
 #else
     const int lane2 = lane, px2 = px, py2 = py;
     const bool active2 = active;
