@@ -421,8 +421,9 @@ int spill_reserve(Dev* c, size_t lanes)
     if (lanes <= c->mk_spill_lanes) return PT_OK;
     if (c->mk_spill) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->mk_spill)); c->mk_spill = nullptr; }
     c->mk_spill_lanes = 0;
-    // stack levels kStackLdsMin..27, then one row for the G-buffer fields kept out of LDS (pt_trace.h)
-    HIPCHK(c, hipMalloc(&c->mk_spill, lanes * (pt::kStackLevels - pt::kStackLdsMin + 1) * sizeof(float2)));
+    // stack levels kStackLdsMin..27, then up to 8 floats per lane for the G-buffer fields kept out
+    // of LDS (pt_trace.h)
+    HIPCHK(c, hipMalloc(&c->mk_spill, lanes * (pt::kStackLevels - pt::kStackLdsMin + 4) * sizeof(float2)));
     c->mk_spill_lanes = lanes;
     return PT_OK;
 }
@@ -674,7 +675,7 @@ int render_trace(DevFx* fx, DevTex* target)
         if (rc) return rc;
         const unsigned waves = (n_wave_tiles + c->persist_tiles - 1) / c->persist_tiles;
         const size_t lanes = (size_t)((waves + 3) / 4) * pt::kBlock;
-        if (lanes * (pt::kStackLevels - pt::kStackLdsMin + 1) > 0xffffffffull)   // 32-bit slab index
+        if (lanes * (pt::kStackLevels - pt::kStackLdsMin + 4) > 0xffffffffull)   // 32-bit slab index
             return fail(c, PT_ERR_ARG, "render target too large for the BVH stack slab");
         if (mesh && (rc = spill_reserve(c, lanes))) return rc;
         a.spill = c->mk_spill;
@@ -691,7 +692,7 @@ int render_trace(DevFx* fx, DevTex* target)
     const int gy_grid = gy + (int)((extra * split + 4u * gx - 1) / (4u * gx));
     if (c->backend == PT_BACKEND_MEGAKERNEL && mesh) {
         const size_t lanes = (size_t)gx * gy_grid * pt::kBlock;
-        if (lanes * (pt::kStackLevels - pt::kStackLdsMin + 1) > 0xffffffffull)   // 32-bit slab index
+        if (lanes * (pt::kStackLevels - pt::kStackLdsMin + 4) > 0xffffffffull)   // 32-bit slab index
             return fail(c, PT_ERR_ARG, "render target too large for the BVH stack slab");
         int rc = spill_reserve(c, lanes);
         if (rc) return rc;

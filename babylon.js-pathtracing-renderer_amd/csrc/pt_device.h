@@ -83,11 +83,12 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, int walk)
 template <int P> constexpr int kMinWaves = kQuad<P> ? (kHasTex<P> ? PT_MINWAVES_QUAD_TEX : PT_MINWAVES_QUAD)
                                          : kHasTex<P> ? PT_MINWAVES_TEX : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
 // G-buffer fields in LDS (pt_program.h GOutLds): the glTF / HDRI scenes' 8-wave child-pair stack
-// walk keeps 6 of the 8 (id and sharp go to the stack slab's last row) and has a seventh LDS stack
-// level in their place (dragon stand-in +1.7 %, bunny x16 +1.7 %; the sky + mesh scene, which
-// writes them more often, lost 2.8 % and keeps all 8; PT_GOUT_LDS_GLTF=8 builds the round-3 form)
+// walk keeps 4 of the 8 (colour.yz, id and sharp go after the stack slab's levels) and has two
+// more LDS stack levels in their place (6 -> 7: dragon stand-in +1.8 %, bunny x16 +1.8 %; 7 -> 8:
+// +0.9 %, +1.0 %; 9 levels with 2 fields: no better; the sky + mesh scene lost 2.8 % with the
+// first split and keeps all 8; PT_GOUT_LDS_GLTF=8 builds the earlier form)
 #ifndef PT_GOUT_LDS_GLTF
-#define PT_GOUT_LDS_GLTF 6
+#define PT_GOUT_LDS_GLTF 4
 #endif
 template <int P> constexpr bool kPairs8 = kPairs<P> && !kHasTex<P> && !kQuad<P>;
 template <int P> constexpr int kGoutLdsOf = (kPairs8<P> && !kTrail<P> && kIsGltf<P>) ? PT_GOUT_LDS_GLTF : 8;

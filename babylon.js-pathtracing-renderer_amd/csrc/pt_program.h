@@ -60,9 +60,9 @@ struct GOut {
 };
 typedef __attribute__((address_space(3))) float lds_float;
 typedef __attribute__((address_space(1))) float glb_float;
-// LS = lanes of the workgroup = the stride of one field; NF = fields kept in LDS, the rest (id,
-// sharp) in the lane's two floats at `gx` (a row of the stack slab): where LDS caps residency that
-// leaves room for one more stack level (kGoutLdsOf, pt_device.h)
+// LS = lanes of the workgroup = the stride of one field; NF = fields kept in LDS, the rest (from
+// the last: sharp, id, colour, normal) in the lane's 8 - NF floats at `gx` (after the stack slab's
+// levels): where LDS caps residency that leaves room for more stack levels (kGoutLdsOf, pt_device.h)
 template <int LS, int NF = 8>
 struct GOutLds {
     lds_float* p;

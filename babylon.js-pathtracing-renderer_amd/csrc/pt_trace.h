@@ -299,8 +299,11 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     cnt.lane_steps = 0;
     cnt.sget = cnt.sget_slab = cnt.sput = cnt.sput_slab = 0;
 #endif
-    // G-buffer fields beyond the LDS ones: the slab's row kStackLevels - kStackLdsMin (pt_capi.cpp spill_reserve)
-    glb_float* const gx = kGoutLdsOf<PROG> < 8 ? (glb_float*)(a.spill + (size_t)(kStackLevels - kStackLdsMin) * a.spill_stride + deep) : nullptr;
+    // G-buffer fields beyond the LDS ones: 8 - kGoutLdsOf floats per lane after the slab's stack
+    // levels, [lane][field] (pt_capi.cpp spill_reserve)
+    glb_float* const gx = kGoutLdsOf<PROG> < 8
+        ? (glb_float*)(a.spill + (size_t)(kStackLevels - kStackLdsMin) * a.spill_stride) + (size_t)deep * (8 - kGoutLdsOf<PROG>)
+        : nullptr;
     GOutLds<kTraceBlock, kGoutLdsOf<PROG>> gl{ (lds_float*)lds_gout, tid, gx };
     gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
     f3 r = mk(0, 0, 0);
