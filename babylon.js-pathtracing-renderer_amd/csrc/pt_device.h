@@ -90,8 +90,14 @@ template <int P> constexpr int kMinWaves = kQuad<P> ? (kHasTex<P> ? PT_MINWAVES_
 #ifndef PT_GOUT_LDS_GLTF
 #define PT_GOUT_LDS_GLTF 4
 #endif
+#ifndef PT_GOUT_LDS_SKY
+#define PT_GOUT_LDS_SKY 8
+#endif
 template <int P> constexpr bool kPairs8 = kPairs<P> && !kHasTex<P> && !kQuad<P>;
-template <int P> constexpr int kGoutLdsOf = (kPairs8<P> && !kTrail<P> && kIsGltf<P>) ? PT_GOUT_LDS_GLTF : 8;
+template <int P> constexpr int kGoutLdsOf = !(kPairs8<P> && !kTrail<P>) ? 8 : kIsGltf<P> ? PT_GOUT_LDS_GLTF
+                                          : kScene<P> == PROG_SKYMESH ? PT_GOUT_LDS_SKY : 8;
+// the G-buffer's field order (GOutLds ORDER): the sky + mesh scene keeps sharp and id in LDS first
+template <int P> constexpr int kGoutOrderOf = kScene<P> == PROG_SKYMESH ? 1 : 0;
 // BVH stack levels in LDS per lane (the rest in the global slab): fewer for the 8-wave variants,
 // one more where two G-buffer fields left LDS
 template <int P> constexpr int kStackLdsOf = kPairs8<P> ? PT_STACK_LDS_PAIRS + (8 - kGoutLdsOf<P>) / 2 : kStackLds;

@@ -63,17 +63,21 @@ typedef __attribute__((address_space(1))) float glb_float;
 // LS = lanes of the workgroup = the stride of one field; NF = fields kept in LDS, the rest (from
 // the last: sharp, id, colour, normal) in the lane's 8 - NF floats at `gx` (after the stack slab's
 // levels): where LDS caps residency that leaves room for more stack levels (kGoutLdsOf, pt_device.h)
-template <int LS, int NF = 8>
+template <int LS, int NF = 8, int ORDER = 0>
 struct GOutLds {
     lds_float* p;
     unsigned slot;
     glb_float* gx = nullptr;
+    // ORDER 0: normal, colour, id, sharp; ORDER 1 (the sky + mesh scene, whose shading sets the
+    // sharpness often): sharp, id, normal, colour - the last 8 - NF of the order leave LDS
+    static constexpr int phys(int f) { return ORDER == 0 ? f : f == 7 ? 0 : f == 6 ? 1 : f + 2; }
     PT_D void put(int f, float v)
     {
-        if (f < NF) p[f * LS + slot] = v;
-        else gx[f - NF] = v;
+        const int q = phys(f);
+        if (q < NF) p[q * LS + slot] = v;
+        else gx[q - NF] = v;
     }
-    PT_D float get(int f) const { return f < NF ? p[f * LS + slot] : gx[f - NF]; }
+    PT_D float get(int f) const { const int q = phys(f); return q < NF ? p[q * LS + slot] : gx[q - NF]; }
     PT_D void clear() { for (int f = 0; f < 8; f++) put(f, 0.0f); }
     PT_D void setNrm(f3 v) { put(0, v.x); put(1, v.y); put(2, v.z); }
     PT_D void setCol(f3 v) { put(3, v.x); put(4, v.y); put(5, v.z); }
@@ -86,7 +90,6 @@ struct GOutLds {
         return g;
     }
 };
-
 
 // CalculateRadiance: js/GLTFModelPathTracing_FragmentShader.js:351-609 and
 // js/BabylonPathTracing_FragmentShader.js:117-344 (METAL is a mirror there), as one step per

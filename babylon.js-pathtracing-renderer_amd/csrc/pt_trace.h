@@ -304,7 +304,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     glb_float* const gx = kGoutLdsOf<PROG> < 8
         ? (glb_float*)(a.spill + (size_t)(kStackLevels - kStackLdsMin) * a.spill_stride) + (size_t)deep * (8 - kGoutLdsOf<PROG>)
         : nullptr;
-    GOutLds<kTraceBlock, kGoutLdsOf<PROG>> gl{ (lds_float*)lds_gout, tid, gx };
+    GOutLds<kTraceBlock, kGoutLdsOf<PROG>, kGoutOrderOf<PROG>> gl{ (lds_float*)lds_gout, tid, gx };
     gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
     f3 r = mk(0, 0, 0);
     if (active) {
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     tracePlace(a, lane2, false, pl);
     const int px2 = pl.px, py2 = pl.py;
     const bool active2 = px2 < ((a.width + 1) & ~1) && py2 < ((a.height + 1) & ~1) && (pl.part < 0 || lane2 < (int)(64u / kSplitParts));
-    const GOut g = (GOutLds<kTraceBlock, kGoutLdsOf<PROG>>{ (lds_float*)lds_gout, kTraceBlock == 64 ? (unsigned)lane2 : threadIdx.x, gx }).load();
+    const GOut g = (GOutLds<kTraceBlock, kGoutLdsOf<PROG>, kGoutOrderOf<PROG>>{ (lds_float*)lds_gout, kTraceBlock == 64 ? (unsigned)lane2 : threadIdx.x, gx }).load();
 #else
     const int lane2 = lane, px2 = px, py2 = py;
     const bool active2 = active;
