@@ -1,6 +1,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-PT_LIBPT=$GRAFT_REPO_ROOT/build_variants/sky4/libpt.so timeout -k 10 400 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -k "sky" > gpurun_out/pytest_sky4.log 2>&1
-rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_sky4.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > gpurun_out/pytest_final.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_final.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-bash tools/gpu_ab.sh sky "sky_dragon" 3 || exit $?
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke_final.log 2>&1 || exit $?
+timeout -k 10 400 python bench.py > gpurun_out/bench_final.json 2> gpurun_out/bench_final.err || exit $?
