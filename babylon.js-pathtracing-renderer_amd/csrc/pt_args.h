@@ -10,30 +10,18 @@ namespace pt {
 
 constexpr int kBlock = 256;          // 4 waves; a block shades a 16x16 pixel tile
 constexpr int kTile = 16;            // tile edge == row-band height used for sharding
-constexpr int kWaveLogSlots = 12;
+constexpr int kWaveLogSlots = 12;   // experiment builds (PT_SECPROF): u64 per workgroup in TraceArgs::wave_log
 // split tiles (pt_trace, longest-first): each 8x8 quadrant of a split 16x16 tile is shaded by this
-// many waves, of 64 / kSplitParts lanes each (4: 4x4-pixel waves of 16 lanes; 16: one 2x2 quad each)
-#ifndef PT_SPLIT_PARTS
-#define PT_SPLIT_PARTS 4
-#endif
-constexpr unsigned kSplitParts = PT_SPLIT_PARTS;
-static_assert(kSplitParts == 4 || kSplitParts == 16, "split quadrants into 4x4 or 2x2 blocks");    // experiment builds: u64 per workgroup in TraceArgs::wave_log
+// many waves of 64 / kSplitParts lanes (4x4-pixel waves of 16 lanes; one 2x2 quad per wave measured
+// slower)
+constexpr unsigned kSplitParts = 4;
 constexpr int kStackLevels = 28;     // stackLevels[28], js/GLTFModelPathTracing_FragmentShader.js:95
-#ifndef PT_STACK_LDS
-#define PT_STACK_LDS 7
-#endif
-// the child-pair walk of the texture-free mesh programs runs at 8 waves/SIMD (pt_device.h
-// kMinWaves), where 6 LDS levels and the G-buffer fill the 160 KB of a CU (5 + the scratch level
-// with PT_PUSH_SCRATCH, pt_trace.h MegaStack::push)
-#ifndef PT_STACK_LDS_PAIRS
-#ifdef PT_PUSH_SCRATCH
-#define PT_STACK_LDS_PAIRS 5
-#else
-#define PT_STACK_LDS_PAIRS 6
-#endif
-#endif
-constexpr int kStackLds = PT_STACK_LDS;        // levels kept in LDS per lane; deeper levels go to a global slab
-constexpr int kStackLdsMin = PT_STACK_LDS_PAIRS < PT_STACK_LDS ? PT_STACK_LDS_PAIRS : PT_STACK_LDS;   // sizes the slab
+// BVH stack levels kept in LDS per lane (deeper levels go to a global slab): 7 for the 4-wave variants;
+// the child-pair walk of the texture-free mesh programs runs at 8 waves/SIMD (pt_device.h kMinWaves),
+// where 6 LDS levels and the G-buffer fill the 160 KB of a CU (pt_trace.h MegaStack::push)
+constexpr int kStackLds = 7;
+constexpr int kStackLdsPairs = 6;
+constexpr int kStackLdsMin = kStackLdsPairs < kStackLds ? kStackLdsPairs : kStackLds;   // sizes the slab
 
 // child-pair record codes: a node's rank code from the build's rank pass (rank >= 0 of an inner
 // node, -1 - rank of a leaf) -> the 32-bit code the walk carries: the record's byte offset in the
@@ -49,29 +37,11 @@ __host__ __device__ inline uint32_t pairCode(float rankCode, uint32_t leafBase)
 // depth <= 28 (stackLevels[28] then never overflows); a jump table of the inner records at depths
 // 0..kTopLevels, by path, after the leaf records
 constexpr int kTrailMaxDepth = 28;
-#ifndef PT_TOP_LEVELS
-#define PT_TOP_LEVELS 11
-#endif
-constexpr int kTopLevels = PT_TOP_LEVELS;
+constexpr int kTopLevels = 11;
 constexpr unsigned kTopEntries = (2u << kTopLevels) - 1u;   // 4095 record copies (64 B, 256 KB), heap order
 
-// Implicit top levels of the child-pair walk (experiment, PT_HEAP_LEVELS = H > 0): a copy of each
-// node at depth < H in heap order (slot 0 the root, the children of slot s at 2s + 1 and 2s + 2),
-// 64 B per slot after the jump table - an inner node's record (its children's boxes, their codes), or
-// a leaf's record with a NaN in its last float (boxes are NaN-free: the marker tells the kinds
-// apart). A step at a slot above the bottom level (depth H - 1) loads 48 B: its children's codes are
-// implicit; the bottom level's children continue in the record array by the codes in its slot.
-// Codes of slots: kHeapBit | slot (record offsets stay below 2^30).
-#ifndef PT_HEAP_LEVELS
-#define PT_HEAP_LEVELS 0
-#endif
-constexpr int kHeapLevels = PT_HEAP_LEVELS;
-constexpr uint32_t kHeapBit = 0x40000000u;
-constexpr unsigned kHeapSlots = kHeapLevels > 0 ? (1u << kHeapLevels) - 1u : 0u;
-constexpr unsigned kHeapBottom = kHeapLevels > 0 ? (1u << (kHeapLevels - 1)) - 1u : 0u;   // first slot of depth H - 1
-
 // the BVH walk of a mesh draw (TraceArgs::bvh_walk; the program variant's thousands digit, pt_device.h)
-enum { WALK_REF = 0, WALK_PAIRS = 1, WALK_TRAIL = 2, WALK_QUAD = 3 };
+enum { WALK_REF = 0, WALK_PAIRS = 1, WALK_TRAIL = 2 };
 
 enum Counter { C_PATHS, C_SEGMENTS, C_NODE, C_LEAF, C_HIT, C_RGBA8, C_OVERFLOW, C_HDR, C_NUM };
 enum ErrBits { E_STACK = 1u };
@@ -162,11 +132,7 @@ struct TraceArgs {
                                // every segment reads SGPRs instead of waiting on a load
     uint32_t bvh_pairs_bytes;  // size of the record array (its buffer descriptor)
     uint32_t bvh_top_base;     // PROG_TRAIL: byte offset of the restart jump table (inner-record copies) in it
-    uint32_t bvh_heap_base;    // PT_HEAP_LEVELS builds: byte offset of the implicit top levels in it (0: none)
-    int bvh_walk;              // WALK_REF / _PAIRS / _TRAIL / _QUAD (pt_device.h): the variant the draw takes
-    const float4* bvh_quads;   // PROG_QUAD: the two-level records (192 B per inner node)
-    uint32_t bvh_quads_bytes;
-    uint32_t bvh_quad_root;    // the root's two-level record (byte offset)
+    int bvh_walk;              // WALK_REF / _PAIRS / _TRAIL (pt_device.h): the variant the draw takes
     float2* spill;             // megakernel BVH stack levels >= kStackLds: [level][grid lane]
     unsigned spill_stride;
     // longest-first dispatch (megakernel): order[slot] = the 16x16 tile dealt to tile slot `slot`
@@ -185,6 +151,7 @@ struct TraceArgs {
     unsigned* err;                  // ErrBits
 #ifdef PT_SECPROF
     unsigned long long* wave_log;   // experiment builds: per workgroup (start, end) wall clock, walk iterations, longest lane's steps, 8 section cycle sums
+    unsigned long long* walk_stat;  // experiment builds: per bounce 0..7, the child-pair walk's load coherence (WalkStat, pt_device.h)
 #endif
 };
 

@@ -44,9 +44,6 @@ hipError_t pt_launch_pairs_pass(int pass, const float4* aabb, long long texels, 
                                 hipStream_t s);
 hipError_t pt_launch_wavefront(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x, int bands,
                                int persist_blocks, hipStream_t s);
-hipError_t pt_launch_quads_build(const float4* aabb, long long texels, const float4* tri, long long tri_texels,
-                                 unsigned nrec, const float* code, const unsigned char* inner, float4* out,
-                                 unsigned n_inner, hipStream_t s);
 hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, unsigned nrec, const unsigned char* inner,
                                 unsigned* parent, unsigned* refs, unsigned* flag, const float4* rec, uint32_t root,
                                 float4* top, hipStream_t s);
@@ -86,9 +83,6 @@ struct DevTex {
     float pairs_root_box[6] = {};
     uint32_t pairs_bytes = 0;   // inner records, then leaf records from pairs_leaf on, then the jump table
     uint32_t pairs_top = 0;     // byte offset of the restart-trail jump table; 0: the tree is not walkable by the trail
-    uint32_t pairs_heap = 0;    // PT_HEAP_LEVELS builds: byte offset of the implicit top levels (0: none)
-    void* quads_mem = nullptr;  // the two-level records (PT_BVH_QUADS; built with the pairs when that walk is asked for)
-    uint32_t quads_bytes = 0, quads_root = 0;
     const DevTex* pairs_tri = nullptr;
     unsigned long long pairs_gen = ~0ull, pairs_tri_gen = ~0ull;
     bool pairs_ok = false;
@@ -459,21 +453,27 @@ extern "C" __attribute__((visibility("default"))) size_t pt_debug_wave_log(unsig
     if (g_wave_log && n) hipMemcpy(out, g_wave_log, n * 8 * pt::kWaveLogSlots, hipMemcpyDeviceToHost);
     return n;
 }
+// the child-pair walk's load coherence since the last call (WalkStat, pt_device.h): 8 bounces x 5
+// counters (wave iterations, record loads, uniform loads, loading lanes, lanes at the first lane's record)
+static unsigned long long* g_walk_stat = nullptr;
+extern "C" __attribute__((visibility("default"))) int pt_debug_walk_stats(unsigned long long out[40])
+{
+    hipDeviceSynchronize();
+    if (!g_walk_stat) return -1;
+    hipMemcpy(out, g_walk_stat, 40 * 8, hipMemcpyDeviceToHost);
+    hipMemset(g_walk_stat, 0, 40 * 8);
+    return 0;
+}
 #endif
 bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
 {
     *rc = PT_OK;
     const long long texels = (long long)t->w * t->h;
     if (c->bvh_layout == PT_BVH_REFERENCE || t->kind != TEX_F32 || tri->kind != TEX_F32 || texels > (1ll << 24)) return false;
-    const bool want_quads = c->bvh_layout == PT_BVH_QUADS;
-    if (t->pairs_gen == t->gen && t->pairs_tri == tri && t->pairs_tri_gen == tri->gen && (!want_quads || t->quads_mem || !t->pairs_ok))
-        return t->pairs_ok;
+    if (t->pairs_gen == t->gen && t->pairs_tri == tri && t->pairs_tri_gen == tri->gen) return t->pairs_ok;
     if (t->pairs_mem) { hipStreamSynchronize(c->stream); hipFree(t->pairs_mem); t->pairs_mem = nullptr; }
-    if (t->quads_mem) { hipStreamSynchronize(c->stream); hipFree(t->quads_mem); t->quads_mem = nullptr; }
-    t->quads_bytes = 0;
     t->pairs_ok = false;
     t->pairs_top = 0;
-    t->pairs_heap = 0;
     t->pairs_gen = t->gen; t->pairs_tri = tri; t->pairs_tri_gen = tri->gen;
     const unsigned nrec = (unsigned)((texels + 1) / 2);
     const unsigned nblk = (nrec + 1023) / 1024;
@@ -518,8 +518,8 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
         }
         leaf_base = (unsigned)al(n_inner * 64);
         const size_t top_base = leaf_base + al(n_leaf * 48);
-        const size_t heap_base = top_base + al(pt::kTopEntries * 64);
-        e = hipMalloc(&t->pairs_mem, heap_base + (size_t)pt::kHeapSlots * 64 + 256);
+        const size_t rec_bytes = top_base + (size_t)pt::kTopEntries * 64;
+        e = hipMalloc(&t->pairs_mem, rec_bytes + 256);
         if (e == hipSuccess) {
             t->pairs_inner = (const float4*)t->pairs_mem;
             t->pairs_leaf = (const float4*)((char*)t->pairs_mem + leaf_base);
@@ -541,28 +541,11 @@ bool ensure_pairs(Dev* c, DevTex* t, const DevTex* tri, int* rc)
         t->pairs_root = pt::pairCode(root, leaf_base);
         const float box6[6] = { node0[1], node0[2], node0[3], node0[5], node0[6], node0[7] };
         std::memcpy(t->pairs_root_box, box6, sizeof(box6));
-        t->pairs_bytes = (uint32_t)(heap_base + (size_t)pt::kHeapSlots * 64);
+        t->pairs_bytes = (uint32_t)rec_bytes;
         // the restart trail's jump table, for trees it can walk (one parent per node, depth <= 28)
         if (e == hipSuccess && !notrail) {
             e = tpass(3, t->pairs_root);
             if (e == hipSuccess) t->pairs_top = (uint32_t)top_base;
-        }
-        // the implicit top levels (PT_HEAP_LEVELS builds)
-        if (e == hipSuccess && pt::kHeapSlots > 0) {
-            e = pt_launch_trail_pass(4, aabb, texels, nrec, inner, parent, refs, c->d_err + 2, t->pairs_inner, t->pairs_root,
-                                     (float4*)((char*)t->pairs_mem + heap_base), c->stream);
-            if (e == hipSuccess) t->pairs_heap = (uint32_t)heap_base;
-        }
-        // the two-level records, when that walk is asked for (192 B per inner node + a leaf root's line)
-        const size_t qbytes = n_inner * 192 + 64;
-        if (e == hipSuccess && want_quads && qbytes < (1ull << 31)) {
-            e = hipMalloc(&t->quads_mem, qbytes + 256);
-            if (e == hipSuccess)
-                e = pt_launch_quads_build(aabb, texels, trid, ttex, nrec, code, inner, (float4*)t->quads_mem,
-                                          (unsigned)n_inner, c->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-            t->quads_bytes = (uint32_t)qbytes;
-            t->quads_root = root >= 0.0f ? (uint32_t)root * 192u : pt::kLeafBit | (uint32_t)(n_inner * 192);
         }
     }
     if (scratch) { hipStreamSynchronize(c->stream); hipFree(scratch); }
@@ -633,16 +616,10 @@ int render_trace(DevFx* fx, DevTex* target)
             std::memcpy(a.bvh_root_box, bvh->pairs_root_box, sizeof(a.bvh_root_box));
             a.bvh_pairs_bytes = bvh->pairs_bytes;
             a.bvh_top_base = c->bvh_layout == PT_BVH_TRAIL ? bvh->pairs_top : 0u;
-            a.bvh_heap_base = c->bvh_layout == PT_BVH_PAIRS ? bvh->pairs_heap : 0u;
-            if (c->bvh_layout == PT_BVH_QUADS && bvh->quads_mem) {
-                a.bvh_quads = (const float4*)bvh->quads_mem;
-                a.bvh_quads_bytes = bvh->quads_bytes;
-                a.bvh_quad_root = bvh->quads_root;
-            }
         }
         if (prc) return prc;
-        a.bvh_walk = a.bvh_quads ? pt::WALK_QUAD : a.bvh_top_base ? pt::WALK_TRAIL : a.bvh_pairs ? pt::WALK_PAIRS : pt::WALK_REF;
-        c->bvh_used = a.bvh_quads ? PT_BVH_QUADS : a.bvh_top_base ? PT_BVH_TRAIL : a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
+        a.bvh_walk = a.bvh_top_base ? pt::WALK_TRAIL : a.bvh_pairs ? pt::WALK_PAIRS : pt::WALK_REF;
+        c->bvh_used = a.bvh_top_base ? PT_BVH_TRAIL : a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
         a.albedo = tex8(sampler(fx, "tAlbedoTexture"));
         a.bump = tex8(sampler(fx, "tBumpTexture"));
         a.metal = tex8(sampler(fx, "tMetallicTexture"));
@@ -659,6 +636,8 @@ int render_trace(DevFx* fx, DevTex* target)
         hipMemsetAsync(g_wave_log, 0, need * 8, c->stream);   // padding workgroups leave zero rows
         g_wave_log_n = need / pt::kWaveLogSlots;
         a.wave_log = g_wave_log;
+        if (!g_walk_stat && hipMalloc(&g_walk_stat, 40 * 8) == hipSuccess) hipMemset(g_walk_stat, 0, 40 * 8);
+        a.walk_stat = g_walk_stat;
     }
 #endif
     int gx = (target->w + pt::kTile - 1) / pt::kTile;
@@ -907,8 +886,8 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_SPLIT_NEAR")) c->split_near = std::max(1, std::min(128, std::atoi(v)));
     if (const char* v = std::getenv("PT_SPLIT_ALWAYS")) c->split_dominance = std::atoi(v) ? 0u : 8u;
     if (const char* v = std::getenv("PT_BVH_LAYOUT"))   // reference | pairs | trail: the context's initial walk
-        c->bvh_layout = !std::strcmp(v, "trail") ? PT_BVH_TRAIL : !std::strcmp(v, "quads") ? PT_BVH_QUADS
-                      : !std::strcmp(v, "reference") ? PT_BVH_REFERENCE : PT_BVH_PAIRS;
+        c->bvh_layout = !std::strcmp(v, "trail") ? PT_BVH_TRAIL : !std::strcmp(v, "reference") ? PT_BVH_REFERENCE
+                                                                                  : PT_BVH_PAIRS;
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
@@ -1139,7 +1118,6 @@ void dev_texture_destroy(DevTex* t)
             if (kv.second == t) kv.second = nullptr;
     if (t->d && !t->external) { hipStreamSynchronize(c->stream); hipFree(t->d); }
     if (t->pairs_mem) { hipStreamSynchronize(c->stream); hipFree(t->pairs_mem); }
-    if (t->quads_mem) { hipStreamSynchronize(c->stream); hipFree(t->quads_mem); }
     for (auto* o : c->textures)   // records built against this triangle texture are stale
         if (o->pairs_tri == t) { o->pairs_tri = nullptr; o->pairs_gen = ~0ull; }
     c->textures.erase(t);
@@ -1214,7 +1192,7 @@ int dev_set_backend(Dev* c, int backend)
 
 int dev_set_bvh_layout(Dev* c, int layout)
 {
-    if (!c || layout < PT_BVH_REFERENCE || layout > PT_BVH_QUADS) return PT_ERR_ARG;
+    if (!c || layout < PT_BVH_REFERENCE || layout > PT_BVH_TRAIL) return PT_ERR_ARG;
     c->bvh_layout = layout;
     return PT_OK;
 }

@@ -21,9 +21,8 @@ enum { PROG_TEX = 100, PROG_GLTF_TEX = 104, PROG_HDRI_TEX = 105, PROG_SKYMESH_TE
 // BVH walks (the program variant's thousands digit, chosen per draw by the host, pt_capi.cpp):
 // +PROG_PAIRS the child-pair records (bvhWalkPairs) with the reference's short stack instead of the
 // reference's texel pairs (bvhWalkRef); +PROG_TRAIL the same records without a stack beyond an LDS ring
-// (bvhWalkTrail: the restart trail, PT_BVH_TRAIL); +PROG_QUAD two-level records, one fetch per two
-// tree levels (bvhWalkQuads, PT_BVH_QUADS)
-enum { PROG_PAIRS = 1000, PROG_TRAIL = 2000, PROG_QUAD = 3000 };   // = WALK_* (pt_args.h) x 1000
+// (bvhWalkTrail: the restart trail, PT_BVH_TRAIL)
+enum { PROG_PAIRS = 1000, PROG_TRAIL = 2000 };   // = WALK_* (pt_args.h) x 1000
 template <int P> constexpr int kBase = P % PROG_PAIRS;
 template <int P> constexpr int kScene = kBase<P> % PROG_TEX;
 // the programs whose SceneIntersect walks the glTF model's BVH: glTF, HDRI and the physical-sky
@@ -42,7 +41,6 @@ template <int P> constexpr int kQuadId0 = kIsQuadric<P> ? 12 : 2;
 template <int P> constexpr int kWalk = P / PROG_PAIRS;
 template <int P> constexpr bool kPairs = P >= PROG_PAIRS;   // child-pair records (any walk but the reference's)
 template <int P> constexpr bool kTrail = kWalk<P> == WALK_TRAIL;
-template <int P> constexpr bool kQuad = kWalk<P> == WALK_QUAD;
 // every instantiated program variant, by BVH walk (one translation unit each: pt_trace_walk*.hip)
 #define PT_FOR_EACH_PROG_REF(X)                                                                                           \
     X(PROG_CORNELL) X(PROG_SKY) X(PROG_QUADRIC) X(PROG_GLTF) X(PROG_GLTF_TEX) X(PROG_HDRI) X(PROG_HDRI_TEX)           \
@@ -51,8 +49,7 @@ template <int P> constexpr bool kQuad = kWalk<P> == WALK_QUAD;
     X(W + PROG_GLTF) X(W + PROG_GLTF_TEX) X(W + PROG_HDRI) X(W + PROG_HDRI_TEX) X(W + PROG_SKYMESH) X(W + PROG_SKYMESH_TEX)
 #define PT_FOR_EACH_PROG_PAIRS(X) PT_FOR_EACH_MESH_PROG(X, PROG_PAIRS)
 #define PT_FOR_EACH_PROG_TRAIL(X) PT_FOR_EACH_MESH_PROG(X, PROG_TRAIL)
-#define PT_FOR_EACH_PROG_QUAD(X) PT_FOR_EACH_MESH_PROG(X, PROG_QUAD)
-#define PT_FOR_EACH_PROG(X) PT_FOR_EACH_PROG_REF(X) PT_FOR_EACH_PROG_PAIRS(X) PT_FOR_EACH_PROG_TRAIL(X) PT_FOR_EACH_PROG_QUAD(X)
+#define PT_FOR_EACH_PROG(X) PT_FOR_EACH_PROG_REF(X) PT_FOR_EACH_PROG_PAIRS(X) PT_FOR_EACH_PROG_TRAIL(X)
 
 // the kernel variant of a draw: the scene program, +PROG_TEX when the model carries albedo / bump
 // maps, + the walk's thousands for the mesh programs
@@ -61,64 +58,36 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, int walk)
     if (prog != PROG_GLTF && prog != PROG_HDRI && prog != PROG_SKYMESH) return prog;
     return prog + (textured ? PROG_TEX : 0) + walk * PROG_PAIRS;
 }
-// waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 64 -> 8). Measured
-// with one-wave workgroups after the walk's branch-free stack (round 2): the child-pair walk at 8
-// waves with 5 LDS levels (64 VGPRs, 52 B of spill) 4 % ahead of 6 waves with 7 levels on the
-// dragon stand-in, 1 % on the bunny; 7 waves with 6 levels behind both; the textured variants
-// 1.3 % faster at 4 waves (128 VGPRs, 8 B of spill) than at 3, and slower with 5 LDS levels; the
-// reference walk loses above 4.
-#ifndef PT_MINWAVES_TEX
-#define PT_MINWAVES_TEX 4
-#endif
-#ifndef PT_MINWAVES_PAIRS
-#define PT_MINWAVES_PAIRS 8
-#endif
-// the two-level walk holds three record lines (48 floats) live: fewer waves
-#ifndef PT_MINWAVES_QUAD
-#define PT_MINWAVES_QUAD 5
-#endif
-#ifndef PT_MINWAVES_QUAD_TEX
-#define PT_MINWAVES_QUAD_TEX 3
-#endif
-template <int P> constexpr int kMinWaves = kQuad<P> ? (kHasTex<P> ? PT_MINWAVES_QUAD_TEX : PT_MINWAVES_QUAD)
-                                         : kHasTex<P> ? PT_MINWAVES_TEX : kPairs<P> ? PT_MINWAVES_PAIRS : 4;
+// Occupancy and LDS per variant (measured; the values are the tuned ones, edit them here
+// for an A/B build):
+// waves per SIMD the register allocator must leave room for (128 VGPRs -> 4, 64 -> 8): the
+// texture-free child-pair walk at 8 (64 VGPRs, a small spill outside the walk loop; 4 % ahead of 6
+// waves on the dragon stand-in, 7 waves behind both), the textured variants at 4 (1.3 % ahead of 3),
+// the reference walk at 4 (it loses above)
+constexpr int kMinWavesTex = 4, kMinWavesPairs = 8, kMinWavesRef = 4;
+template <int P> constexpr int kMinWaves = kHasTex<P> ? kMinWavesTex : kPairs<P> ? kMinWavesPairs : kMinWavesRef;
 // G-buffer fields in LDS (pt_program.h GOutLds): the glTF / HDRI scenes' 8-wave child-pair stack
 // walk keeps 4 of the 8 (colour.yz, id and sharp go after the stack slab's levels) and has two
 // more LDS stack levels in their place (6 -> 7: dragon stand-in +1.8 %, bunny x16 +1.8 %; 7 -> 8:
-// +0.9 %, +1.0 %; 9 levels with 2 fields: no better; the sky + mesh scene lost 2.8 % with the
-// first split and keeps all 8; PT_GOUT_LDS_GLTF=8 builds the earlier form)
-#ifndef PT_GOUT_LDS_GLTF
-#define PT_GOUT_LDS_GLTF 4
-#endif
-#ifndef PT_GOUT_LDS_SKY
-#define PT_GOUT_LDS_SKY 8
-#endif
-template <int P> constexpr bool kPairs8 = kPairs<P> && !kHasTex<P> && !kQuad<P>;
-template <int P> constexpr int kGoutLdsOf = !(kPairs8<P> && !kTrail<P>) ? 8 : kIsGltf<P> ? PT_GOUT_LDS_GLTF
-                                          : kScene<P> == PROG_SKYMESH ? PT_GOUT_LDS_SKY : 8;
+// +0.9 %, +1.0 %; 9 levels with 2 fields: no better); the sky + mesh scene lost 2.8 % with the
+// first split and keeps all 8
+constexpr int kGoutLdsGltf = 4, kGoutLdsSky = 8;
+template <int P> constexpr bool kPairs8 = kPairs<P> && !kHasTex<P>;
+template <int P> constexpr int kGoutLdsOf = !(kPairs8<P> && !kTrail<P>) ? 8 : kIsGltf<P> ? kGoutLdsGltf
+                                          : kScene<P> == PROG_SKYMESH ? kGoutLdsSky : 8;
 // the G-buffer's field order (GOutLds ORDER): the sky + mesh scene keeps sharp and id in LDS first
 template <int P> constexpr int kGoutOrderOf = kScene<P> == PROG_SKYMESH ? 1 : 0;
 // BVH stack levels in LDS per lane (the rest in the global slab): fewer for the 8-wave variants,
 // one more where two G-buffer fields left LDS
-template <int P> constexpr int kStackLdsOf = kPairs8<P> ? PT_STACK_LDS_PAIRS + (8 - kGoutLdsOf<P>) / 2 : kStackLds;
+template <int P> constexpr int kStackLdsOf = kPairs8<P> ? kStackLdsPairs + (8 - kGoutLdsOf<P>) / 2 : kStackLds;
 // the restart-trail walk's LDS ring (entries per lane): the LDS of the stack walk's levels at 8
 // waves/SIMD (6 x 8 B + the 32-B G-buffer = 80 B per lane = 160 KB per CU); at 4 waves/SIMD the
 // textured variants have room for 14
-#ifndef PT_RING_PAIRS
-#define PT_RING_PAIRS 6
-#endif
-#ifndef PT_RING_TEX
-#define PT_RING_TEX 14
-#endif
-template <int P> constexpr int kRingOf = kHasTex<P> ? PT_RING_TEX : PT_RING_PAIRS;
+template <int P> constexpr int kRingOf = kHasTex<P> ? 14 : 6;
 // the stack walk's push form (pt_trace.h MegaStack::push): a scratch level and unmasked stores for
-// the textured 4-wave variants, masked stores into one more real level where LDS caps residency
-// (the 8-wave variants); PT_PUSH_SCRATCH: the scratch form everywhere (the round-2 build)
-#ifdef PT_PUSH_SCRATCH
-template <int P> constexpr bool kScratchOf = true;
-#else
+// the textured 4-wave variants (1 % faster there), masked stores into one more real level where LDS
+// caps residency (the 8-wave variants: dragon stand-in +1.5 %, sky + dragon +2.2 %)
 template <int P> constexpr bool kScratchOf = !kPairs8<P>;
-#endif
 // LDS float2 slots per lane a walk of program P needs: stack levels (+ the scratch level), or the ring
 template <int P> constexpr int kWalkSlotsOf = kTrail<P> ? kRingOf<P> : kStackLdsOf<P> + (kScratchOf<P> ? 1 : 0);
 
@@ -300,80 +269,19 @@ PT_D float boxFast(f3 mn, f3 mx, f3 ro, f3 inv)
 }
 PT_D bool finite3(f3 v) { return __builtin_isfinite(v.x) && __builtin_isfinite(v.y) && __builtin_isfinite(v.z); }
 
-// ---- child-pair lines: the two child boxes of an inner record (PT_BVH_PAIRS / _TRAIL / _QUADS) in
-// 12 floats, A.min.xyz A.max.xyz B.min.xyz B.max.xyz. PT_PAIR_AXIS=1 builds the experiment of a
-// per-axis layout (each box's (min, max) adjacent: A.min.x A.max.x A.min.y A.max.y | A.min.z A.max.z
-// B.min.x B.max.x | B.min.y B.max.y B.min.z B.max.z), in which one v_pk_add_f32 (min - O, max - O)
-// and one v_pk_mul_f32 (x inv) compute an axis's two slab distances: 6 packed instructions per box
-// instead of 12, bit-exact (IEEE per element), but 2 % slower on the dragon stand-in, the helmet and
-// the sky composite (-0.8 % on the bunny): the packed forms issue no faster here.
-#ifndef PT_PAIR_AXIS
-#define PT_PAIR_AXIS 0
-#endif
-typedef float pf2 __attribute__((ext_vector_type(2)));
+// ---- child-pair lines: the two child boxes of an inner record in 12 floats, A.min.xyz A.max.xyz
+// B.min.xyz B.max.xyz (a per-axis layout for packed v_pk_add/mul slab arithmetic measured 2 % slower,
+// DESIGN.md §6)
 // (a0, a1), (b0, b1): the reference texels of children A and B (.yzw = min, max)
 PT_D void pairLineWrite(float4* o, float4 a0, float4 a1, float4 b0, float4 b1)
 {
-#if PT_PAIR_AXIS
-    o[0] = make_float4(a0.y, a1.y, a0.z, a1.z);
-    o[1] = make_float4(a0.w, a1.w, b0.y, b1.y);
-    o[2] = make_float4(b0.w, b1.w, b0.z, b1.z);
-    o[2] = make_float4(b0.z, b1.z, b0.w, b1.w);
-#else
     o[0] = make_float4(a0.y, a0.z, a0.w, a1.y);
     o[1] = make_float4(a1.z, a1.w, b0.y, b0.z);
     o[2] = make_float4(b0.w, b1.y, b1.z, b1.w);
-#endif
-}
-// the ray's model-space origin and inverse direction as aligned register pairs (O.x, O.y),
-// (inv.x, inv.y), (O.z, inv.z) for the packed slab arithmetic (op_sel picks the element each half uses)
-struct PairRay {
-    pf2 oxy, ixy, zz;
-};
-PT_D PairRay pairRay(f3 O, f3 inv)
-{
-    PairRay p;
-    p.oxy = pf2{ O.x, O.y }; p.ixy = pf2{ inv.x, inv.y }; p.zz = pf2{ O.z, inv.z };
-    return p;
-}
-// boxFast of one child from its per-axis pairs x = (min.x, max.x), y, z
-PT_D float boxFastAxis(pf2 x, pf2 y, pf2 z, const PairRay& p)
-{
-    pf2 tx, ty, tz;
-    asm("v_pk_add_f32 %0, %3, %6 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
-        "v_pk_add_f32 %1, %4, %6 op_sel:[0,1] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[0,1]\n\t"
-        "v_pk_add_f32 %2, %5, %8 op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]\n\t"
-        "v_pk_mul_f32 %0, %0, %7 op_sel_hi:[1,0]\n\t"
-        "v_pk_mul_f32 %1, %1, %7 op_sel:[0,1] op_sel_hi:[1,1]\n\t"
-        "v_pk_mul_f32 %2, %2, %8 op_sel:[0,1] op_sel_hi:[1,1]"
-        : "=&v"(tx), "=&v"(ty), "=&v"(tz)
-        : "v"(x), "v"(y), "v"(z), "v"(p.oxy), "v"(p.ixy), "v"(p.zz));
-    float t0, t1, a, b, c, d;
-    asm("v_min_f32 %0, %6, %7\n\t"
-        "v_max_f32 %1, %6, %7\n\t"
-        "v_min_f32 %2, %8, %9\n\t"
-        "v_max_f32 %3, %8, %9\n\t"
-        "v_min_f32 %4, %10, %11\n\t"
-        "v_max_f32 %5, %10, %11\n\t"
-        "v_max3_f32 %0, %0, %2, %4\n\t"
-        "v_min3_f32 %1, %1, %3, %5"
-        : "=&v"(t0), "=&v"(t1), "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
-        : "v"(tx.x), "v"(tx.y), "v"(ty.x), "v"(ty.y), "v"(tz.x), "v"(tz.y));
-    return vmax0(t0) > t1 ? kINF : t0;
 }
 // the children's box distances of a child-pair line r0..r2 (tA, tB as BoundingBoxIntersect)
 PT_D void pairBoxes(float4 r0, float4 r1, float4 r2, f3 O, f3 inv, bool fast, float& tA, float& tB)
 {
-#if PT_PAIR_AXIS
-    if (fast) {
-        const PairRay p = pairRay(O, inv);
-        tA = boxFastAxis(pf2{ r0.x, r0.y }, pf2{ r0.z, r0.w }, pf2{ r1.x, r1.y }, p);
-        tB = boxFastAxis(pf2{ r1.z, r1.w }, pf2{ r2.x, r2.y }, pf2{ r2.z, r2.w }, p);
-    } else {
-        tA = box(mk(r0.x, r0.z, r1.x), mk(r0.y, r0.w, r1.y), O, inv);
-        tB = box(mk(r1.z, r2.x, r2.z), mk(r1.w, r2.y, r2.w), O, inv);
-    }
-#else
     if (fast) {
         tA = boxFast(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
         tB = boxFast(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
@@ -381,7 +289,6 @@ PT_D void pairBoxes(float4 r0, float4 r1, float4 r2, f3 O, f3 inv, bool fast, fl
         tA = box(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), O, inv);
         tB = box(mk(r1.z, r1.w, r2.x), mk(r2.y, r2.z, r2.w), O, inv);
     }
-#endif
 }
 
 // BVH_TriangleIntersect / BVH_DoubleSidedTriangleIntersect (js/PathTracingCommon.js:1214-1245)
@@ -429,13 +336,7 @@ PT_D void texBilinear(const Tex8& t, float u, float v, float out[4])
     float ax = x - fx, by = y - fy;
     int x0 = wrapTexel(fx, t.w), y0 = wrapTexel(fy, t.h);
     int x1 = x0 + 1 == t.w ? 0 : x0 + 1, y1 = y0 + 1 == t.h ? 0 : y0 + 1;
-#ifdef PT_NT_TEX   // experiment: the maps' taps as non-temporal loads (keep BVH records in L2)
-    const uint32_t* q = (const uint32_t*)t.p;
-    auto ld = [&](int i) { const uint32_t v = __builtin_nontemporal_load(q + i); return make_uchar4(v & 255u, (v >> 8) & 255u, (v >> 16) & 255u, v >> 24); };
-    uchar4 t00 = ld(y0 * t.w + x0), t10 = ld(y0 * t.w + x1), t01 = ld(y1 * t.w + x0), t11 = ld(y1 * t.w + x1);
-#else
     uchar4 t00 = t.p[y0 * t.w + x0], t10 = t.p[y0 * t.w + x1], t01 = t.p[y1 * t.w + x0], t11 = t.p[y1 * t.w + x1];
-#endif
     out[0] = gmix(gmix(unorm8(t00.x), unorm8(t10.x), ax), gmix(unorm8(t01.x), unorm8(t11.x), ax), by);
     out[1] = gmix(gmix(unorm8(t00.y), unorm8(t10.y), ax), gmix(unorm8(t01.y), unorm8(t11.y), ax), by);
     out[2] = gmix(gmix(unorm8(t00.z), unorm8(t10.z), ax), gmix(unorm8(t01.z), unorm8(t11.z), ax), by);
@@ -451,16 +352,8 @@ PT_D float4 texBilinearF(const TexF& t, float u, float v)
     float ax = x - fx, by = y - fy;
     int x0 = wrapTexel(fx, t.w), y0 = wrapTexel(fy, t.h);
     int x1 = x0 + 1 == t.w ? 0 : x0 + 1, y1 = y0 + 1 == t.h ? 0 : y0 + 1;
-#ifdef PT_NT_TEX
-    auto ld = [&](size_t i) { const float* f = (const float*)(t.p + i);
-        return make_float4(__builtin_nontemporal_load(f), __builtin_nontemporal_load(f + 1), __builtin_nontemporal_load(f + 2),
-                           __builtin_nontemporal_load(f + 3)); };
-    const float4 t00 = ld((size_t)y0 * t.w + x0), t10 = ld((size_t)y0 * t.w + x1);
-    const float4 t01 = ld((size_t)y1 * t.w + x0), t11 = ld((size_t)y1 * t.w + x1);
-#else
     const float4 t00 = t.p[(size_t)y0 * t.w + x0], t10 = t.p[(size_t)y0 * t.w + x1];
     const float4 t01 = t.p[(size_t)y1 * t.w + x0], t11 = t.p[(size_t)y1 * t.w + x1];
-#endif
     return make_float4(gmix(gmix(t00.x, t10.x, ax), gmix(t01.x, t11.x, ax), by),
                        gmix(gmix(t00.y, t10.y, ax), gmix(t01.y, t11.y, ax), by),
                        gmix(gmix(t00.z, t10.z, ax), gmix(t01.z, t11.z, ax), by),
@@ -477,14 +370,60 @@ PT_D f3 pow22(f3 c) { return mk(gpow(c.x, 2.2f), gpow(c.y, 2.2f), gpow(c.z, 2.2f
 // The stack policy Stk provides pop(level, sentinel) -> float2 and push(level, float2) -> bool
 // (false: beyond stackLevels[27], dropped) for any level >= 0.
 
+#ifdef PT_SECPROF
+// Experiment builds: the walk loop's load coherence, per wave and bounce (pt_debug_walk_stats): wave
+// iterations, those that load a record, those whose loading lanes all load one record, the loading
+// lanes, the loading lanes that load the first loading lane's record
+struct WalkStat {
+    unsigned iters = 0, loads = 0, uniform = 0, lanes = 0, first = 0;
+    PT_D void step(bool live, uint32_t off)
+    {
+        const unsigned long long ld = __ballot(live);
+        iters++;
+        if (!ld) return;
+        const int fl = __ffsll((long long)ld) - 1;
+        const uint32_t f = __shfl(off, fl, 64);
+        const unsigned long long same = __ballot(live && off == f);
+        loads++;
+        uniform += same == ld ? 1u : 0u;
+        lanes += (unsigned)__popcll(ld);
+        first += (unsigned)__popcll(same);
+    }
+    // by the wave's first active lane, at bounce `bounce` (the same for every lane in a walk: the
+    // megakernel's bounce loop is structured)
+    PT_D void flush(unsigned long long* out, unsigned bounce)
+    {
+        if (!out) return;
+        const int ln = __lane_id();
+        if (ln != (int)__builtin_amdgcn_readfirstlane(ln)) return;
+        unsigned long long* o = out + 5u * min(bounce, 7u);
+        atomicAdd(o, (unsigned long long)iters);
+        atomicAdd(o + 1, (unsigned long long)loads);
+        atomicAdd(o + 2, (unsigned long long)uniform);
+        atomicAdd(o + 3, (unsigned long long)lanes);
+        atomicAdd(o + 4, (unsigned long long)first);
+    }
+};
+#endif
+
 struct BvhResult {
     float triID, triU, triV;
     bool lookup;
     unsigned nodes, leaves, ovf;
 #ifdef PT_SECPROF
-    unsigned steps, restarts;
+    unsigned steps, restarts;   // (value-initialised by the callers' brace initialisers)
+    WalkStat ws;
 #endif
 };
+// instrumentation hooks of the walks (no code outside PT_SECPROF builds): a walk-loop iteration (its
+// lane loads the record at `off` when `live`), a restart descent's record load
+#ifdef PT_SECPROF
+PT_D void secWalkStep(BvhResult& r, bool live, uint32_t off) { r.steps++; r.ws.step(live, off); }
+PT_D void secRestart(BvhResult& r) { r.restarts++; }
+#else
+PT_D void secWalkStep(BvhResult&, bool, uint32_t) {}
+PT_D void secRestart(BvhResult&) {}
+#endif
 
 template <class Stk>
 PT_D void stackPush(const TraceArgs& a, Stk& st, int si, float2 e, unsigned& ovf)
@@ -567,17 +506,9 @@ PT_D void bvhWalkRef(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float4 c0
 // no fetch (the stack entry (tNear, code) already says what the node is), and a leaf's vertices
 // sit in a dense 48-byte record instead of the first third of a 128-byte triangle texel group:
 // both arrays together are about 3.4 MB for StanfordBunny, within one XCD's L2.
-// The walk as a resumable state machine (a step is one pop, culled or not, and/or one record):
-// `pop` = the next step pops the stack (the reference loop's !skip). `fast` = the ray qualifies
-// for boxFast (records are NaN-free, checked at build). A schedule that interleaved walk steps
-// with other lanes' shading on top of it measured slower.
-struct PairWalk {
-    uint32_t code;           // node to process
-    float hitT;              // closest hit so far
-    float triID, triU, triV; // the hit triangle (lookup), its barycentrics
-    int sp;                  // stack pointer
-    bool pop, lookup;
-};
+// The walk: `pop` = the next step pops the stack (the reference loop's !skip). `fast` = the ray
+// qualifies for boxFast (records are NaN-free, checked at build). A schedule that interleaved walk
+// steps with other lanes' shading on top of it measured slower.
 // the record array as a buffer descriptor, built from kernel arguments and made provably
 // wave-uniform (readfirstlane) so that no waterfall loop wraps the loads
 struct PairBufs {
@@ -606,303 +537,68 @@ PT_D float2 ldRec2(__amdgpu_buffer_rsrc_t r, uint32_t off)
     const vu2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, 0);
     return make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
 }
-PT_D void pairWalkBegin(PairWalk& w, uint32_t rootCode, float rootT, float hitT)
-{
-    w.code = rootCode; w.hitT = hitT; w.sp = 0;
-    w.pop = !(rootT < hitT);
-    w.lookup = false;
-    w.triID = 0.0f; w.triU = 0.0f; w.triV = 0.0f;
-}
 PT_D bool pairWalkFast(f3 O, f3 inv)
 {
     return finite3(O) && finite3(inv) && inv.x != 0.0f && inv.y != 0.0f && inv.z != 0.0f;
 }
-// the record part of a step: w.code's record, its children tested (push / next) or its triangle
-template <class Stk>
-PT_D void pairWalkRecord(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv, bool dbl, bool fast, Stk& st,
-                         PairWalk& w, BvhResult& r)
-{
-    // one set of loads for either kind of record (both live in one array): a wave whose lanes sit
-    // at inner and at leaf nodes issues 4 vector-memory instructions, not 4 + 3 (the address and
-    // data units cost ~17 cycles per wave-instruction however few lanes are active).
-    // A leaf record is 48 B; its lane's fourth load reads the next record's first 8 B (or 0 past
-    // the end of the array) and is not used.
-    const uint32_t off = w.code & ~kLeafBit;
-#ifdef PT_SECPROF_LOADS
-    if (a.counters) {   // experiment: wave-level record loads, those with one record for all lanes, lanes served
-        const uint32_t first = __builtin_amdgcn_readfirstlane(off);
-        const unsigned long long act = __ballot(1), same = __ballot(off == first);
-        if (__lane_id() == (int)__builtin_amdgcn_readfirstlane(__lane_id())) {
-            atomicAdd(&a.counters[0], 1ull);
-            if (same == act) atomicAdd(&a.counters[1], 1ull);
-            atomicAdd(&a.counters[2], (unsigned long long)__popcll(act));
-        }
-    }
-#endif
-    const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
-    const float2 r3 = ldRec2(b.rec, off + 48u);
-    if (!(w.code & kLeafBit)) {
-        r.nodes += 2;
-        float tA, tB;
-        pairBoxes(r0, r1, r2, O, inv, fast, tA, tB);
-        float cA = r3.x, cB = r3.y;   // codes as float bits: only moved, never computed on
-        // the reference's swap and two ifs as selects: the near child is next if it is hit, else the
-        // far one; the far one is pushed when both are hit
-        const bool sw = tB < tA;
-        const float tN = sw ? tB : tA, tF = sw ? tA : tB;
-        const float cN = sw ? cB : cA, cF = sw ? cA : cB;
-        const bool hitN = tN < w.hitT, hitF = tF < w.hitT;
-        if (hitN && hitF) { stackPush(a, st, w.sp, make_float2(tF, cF), r.ovf); w.sp++; }
-        w.code = __float_as_uint(hitN ? cN : hitF ? cF : __uint_as_float(w.code));
-        w.pop = !(hitN || hitF);
-        return;
-    }
-    r.leaves++;
-    float tu, tv;
-    const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
-    if (d < w.hitT) { w.hitT = d; w.triID = 8.0f * r2.y; w.triU = tu; w.triV = tv; w.lookup = true; }
-    // a use on this side too keeps the codes' load with the other three: sunk into the inner-node
-    // branch, it was issued only after a mixed wave's leaf tests (-3 % kernel time)
-    asm volatile("" ::"v"(r3.x));
-}
-// one step; false once the stack has run empty (the walk is over)
-template <class Stk>
-PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv, bool dbl, bool fast, Stk& st,
-                       PairWalk& w, BvhResult& r)
-{
-    if (w.pop) {
-        w.sp--;
-        if (w.sp < 0) return false;
-        const float2 e = stackPop(st, w.sp, make_float2(kINF, 0.0f));
-        if (e.x >= w.hitT) return true;
-        w.code = __float_as_uint(e.y);
-        r.nodes++;
-    }
-    w.pop = true;
-    pairWalkRecord(a, b, O, D, inv, dbl, fast, st, w, r);
-    return true;
-}
+// One loop exit (the empty stack), and the walk's flags as integers in VGPRs: a bool lives in an
+// SGPR lane mask that every divergent merge rebuilds (s_andn2 / s_and / s_or per flag per merge;
+// 73 -> 45 scalar instructions in the loop, dragon stand-in -1.3 %). A pop is a
+// predicated LDS read; a culled pop skips the rest of its step. One set of four record loads for
+// either kind of record (both live in one array): a wave whose lanes sit at inner and at leaf nodes
+// issues 4 vector-memory instructions, not 4 + 3. A leaf record is 48 B; its lane's fourth load reads
+// the next record's first 8 B (or 0 past the end of the array) and is not used.
 template <class Stk>
 PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float curT, float& hitT, Stk& st,
                        BvhResult& r)
 {
-    PairWalk w;
-#if PT_HEAP_LEVELS > 0
-    pairWalkBegin(w, a.bvh_heap_base ? kHeapBit : a.bvh_root_code, curT, hitT);   // slot 0: the root
-#else
-    pairWalkBegin(w, a.bvh_root_code, curT, hitT);
-#endif
     const bool fast = pairWalkFast(O, inv);
     const PairBufs b = pairBufs(a);
-#ifndef PT_CODES
-#define PT_CODES 0
-#endif
-#if defined(PT_STEP_LOOP) && PT_HEAP_LEVELS > 0
-#error "PT_HEAP_LEVELS needs the one-exit step loop"
-#endif
-#ifndef PT_STEP_LOOP
-    // One loop exit (the empty stack), and the walk's flags as integers in VGPRs: a bool lives in an
-    // SGPR lane mask that every divergent merge rebuilds (s_andn2 / s_and / s_or per flag per merge;
-    // 73 -> 45 scalar instructions in the loop, dragon stand-in -1.3 %). A pop is a
-    // predicated LDS read; a culled pop skips the rest of its step. PT_STEP_LOOP builds the round-2
-    // loop over pairWalkStep for A/B.
-#ifdef PT_SECPROF
-    r.steps = 0;
-#endif
-    {
-        uint32_t code = w.code;
-        float hT = w.hitT;
-        int sp = 0;
-        int pop = w.pop ? 1 : 0;
-        float tID = -1.0f, tU = 0.0f, tV = 0.0f;
-#if PT_HEAP_LEVELS > 0
-        unsigned guard = 0;   // experiment builds: a bound no walk reaches, so that a layout bug cannot hang the GPU
-#endif
-        for (;;) {
-            asm volatile("" : "+v"(pop));
-            const int sp2 = sp - pop;
-            if (sp2 < 0) break;
-#if PT_HEAP_LEVELS > 0
-            if (++guard > (1u << 20)) { atomicOr(a.err, (unsigned)E_STACK); break; }
-#endif
-#ifdef PT_SECPROF
-            r.steps++;
-#endif
-            sp = sp2;
-            const float2 e = stackPop(st, pop ? sp2 : 0, make_float2(kINF, 0.0f));
-            const bool live = !pop || e.x < hT;
-            if (pop && live) r.nodes++;
-            code = pop ? __float_as_uint(e.y) : code;
-            pop = 1;
-            if (!live) continue;
-#if PT_HEAP_LEVELS > 0
-            const bool heap = (code & kHeapBit) != 0;
-            const uint32_t slot = code & (kHeapBit - 1u);
-            const uint32_t off = heap ? a.bvh_heap_base + slot * 64u : code & ~kLeafBit;
-#else
-            const uint32_t off = code & ~kLeafBit;
-#endif
-            const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
-#if PT_HEAP_LEVELS > 0
-            // the children's codes: in the record array's records and the heap's bottom slots; implicit above
-            float2 r3 = make_float2(0.0f, 0.0f);
-            uint32_t c2 = code;
-            asm volatile("" : "+v"(c2));   // (an opaque copy: the load is not sunk past the leaf tests)
-            if (!(c2 & kHeapBit) || (c2 & (kHeapBit - 1u)) >= kHeapBottom) r3 = ldRec2(b.rec, off + 48u);
-            const bool leaf = heap ? !(r2.w == r2.w) : (code & kLeafBit) != 0;   // a leaf slot's NaN marker
-#elif PT_CODES == 0
-            const float2 r3 = ldRec2(b.rec, off + 48u);
-#elif PT_CODES == 1   // experiment: the codes' load by the lanes at inner nodes only
-            float2 r3 = make_float2(0.0f, 0.0f);
-            uint32_t c2 = code;
-            asm volatile("" : "+v"(c2));   // an opaque copy: this branch is not merged with the inner/leaf one below,
-            if (!(c2 & kLeafBit)) r3 = ldRec2(b.rec, off + 48u);   // so the load is not sunk past the leaf tests
-#endif
-#if PT_HEAP_LEVELS == 0
-            const bool leaf = (code & kLeafBit) != 0;
-#endif
-            if (!leaf) {
-                r.nodes += 2;
-                float tA, tB;
-                pairBoxes(r0, r1, r2, O, inv, fast, tA, tB);
-                const bool sw = tB < tA;
-                const float tN = sw ? tB : tA, tF = sw ? tA : tB;
-                const bool hitN = tN < hT, hitF = tF < hT;
-#if PT_CODES == 2   // experiment: the codes' load by the lanes that take a child only, after the box tests
-                float2 r3 = make_float2(0.0f, 0.0f);
-                if (hitN || hitF) r3 = ldRec2(b.rec, off + 48u);
-#endif
-#if PT_HEAP_LEVELS > 0
-                const bool implicit = heap && slot < kHeapBottom;
-                const float cA = implicit ? __uint_as_float(kHeapBit | (2u * slot + 1u)) : r3.x;
-                const float cB = implicit ? __uint_as_float(kHeapBit | (2u * slot + 2u)) : r3.y;
-#else
-                const float cA = r3.x, cB = r3.y;
-#endif
-                const float cN = sw ? cB : cA, cF = sw ? cA : cB;
-                if (hitN && hitF) { stackPush(a, st, sp, make_float2(tF, cF), r.ovf); sp++; }
-                code = __float_as_uint(hitN ? cN : hitF ? cF : __uint_as_float(code));
-                pop = (hitN || hitF) ? 0 : 1;
-            } else {
-                r.leaves++;
-                float tu, tv;
-                const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
-                if (d < hT) { hT = d; tID = 8.0f * r2.y; tU = tu; tV = tv; }
-#if PT_CODES == 0
-                asm volatile("" ::"v"(r3.x));
-#endif
-            }
+    uint32_t code = a.bvh_root_code;
+    float hT = hitT;
+    int sp = 0;
+    int pop = curT < hitT ? 0 : 1;
+    float tID = -1.0f, tU = 0.0f, tV = 0.0f;
+    for (;;) {
+        asm volatile("" : "+v"(pop));
+        const int sp2 = sp - pop;
+        if (sp2 < 0) break;
+        sp = sp2;
+        const float2 e = stackPop(st, pop ? sp2 : 0, make_float2(kINF, 0.0f));
+        const bool live = !pop || e.x < hT;
+        if (pop && live) r.nodes++;
+        code = pop ? __float_as_uint(e.y) : code;
+        pop = 1;
+        secWalkStep(r, live, code & ~kLeafBit);
+        if (!live) continue;
+        const uint32_t off = code & ~kLeafBit;
+        const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
+        const float2 r3 = ldRec2(b.rec, off + 48u);
+        if (!(code & kLeafBit)) {
+            r.nodes += 2;
+            float tA, tB;
+            pairBoxes(r0, r1, r2, O, inv, fast, tA, tB);
+            // the reference's swap and two ifs as selects: the near child is next if it is hit, else
+            // the far one; the far one is pushed when both are hit
+            const bool sw = tB < tA;
+            const float tN = sw ? tB : tA, tF = sw ? tA : tB;
+            const bool hitN = tN < hT, hitF = tF < hT;
+            const float cN = sw ? r3.y : r3.x, cF = sw ? r3.x : r3.y;   // codes as float bits: only moved
+            if (hitN && hitF) { stackPush(a, st, sp, make_float2(tF, cF), r.ovf); sp++; }
+            code = __float_as_uint(hitN ? cN : hitF ? cF : __uint_as_float(code));
+            pop = (hitN || hitF) ? 0 : 1;
+        } else {
+            r.leaves++;
+            float tu, tv;
+            const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
+            if (d < hT) { hT = d; tID = 8.0f * r2.y; tU = tu; tV = tv; }
+            // a use on this side too keeps the codes' load with the other three: sunk into the inner-node
+            // branch, it was issued only after a mixed wave's leaf tests (-3 % kernel time)
+            asm volatile("" ::"v"(r3.x));
         }
-        w.hitT = hT;
-        if (tID >= 0.0f) { w.lookup = true; w.triID = tID; w.triU = tU; w.triV = tV; }
     }
-#elif defined(PT_SECPROF)
-    r.steps = 0;
-    while (pairWalkStep(a, b, O, D, inv, dbl, fast, st, w, r)) r.steps++;
-#else
-    while (pairWalkStep(a, b, O, D, inv, dbl, fast, st, w, r)) {}
-#endif
-    hitT = w.hitT;
-    if (w.lookup) { r.triID = w.triID; r.triU = w.triU; r.triV = w.triV; r.lookup = true; }
-}
-
-// ------------------------------------------------------------------------------ two-level records
-// PT_BVH_QUADS: one fetch per two tree levels. An inner node n's record (192 B, three 64-B lines) is
-//   line 0  n's child-pair line: A.box, B.box, codeA, codeB (A = n + 1, B = its right link)
-//   line 1  A's own line: A's child-pair line (A inner: A1.box, A2.box, codes) or A's leaf triangle
-//           (v0, e1 = v1 - v0, e2 = v2 - v0, idObject)
-//   line 2  the same for B
-// Codes: an inner node's record offset (innerRank * 192), or kLeafBit | the offset of the leaf's line
-// inside its parent's record. A step loads the three lines together, tests n's children (the
-// reference's step at n), and goes on at once with the child it takes, whose line it already holds
-// (the reference's next step): its children's boxes, or its triangle. The next fetch is that child's
-// near child's record - half the dependent round trips of the child-pair walk, with the same
-// comparisons in the same order, so the same hit and the same reference-priced counts.
-struct QuadWalk {
-    uint32_t code;
-    float hitT;
-    float triID, triU, triV;
-    int sp;
-    bool pop, lookup;
-};
-PT_D void quadLeaf(float4 l0, float4 l1, float4 l2, f3 O, f3 D, bool dbl, QuadWalk& w, BvhResult& r)
-{
-    r.leaves++;
-    float tu, tv;
-    const float d = bvhTriangleE(mk(l0.x, l0.y, l0.z), mk(l0.w, l1.x, l1.y), mk(l1.z, l1.w, l2.x), O, D, tu, tv, dbl);
-    if (d < w.hitT) { w.hitT = d; w.triID = 8.0f * l2.y; w.triU = tu; w.triV = tv; w.lookup = true; }
-}
-// one inner node's children from its line (the reference's inner step): false = neither is hit (pop)
-template <class Stk>
-PT_D bool quadInner(const TraceArgs& a, float4 l0, float4 l1, float4 l2, float2 l3, f3 O, f3 inv, bool fast, Stk& st,
-                    QuadWalk& w, BvhResult& r, uint32_t& next)
-{
-    r.nodes += 2;
-    float tA, tB;
-    pairBoxes(l0, l1, l2, O, inv, fast, tA, tB);
-    const bool sw = tB < tA;
-    const float tN = sw ? tB : tA, tF = sw ? tA : tB;
-    const float cN = sw ? l3.y : l3.x, cF = sw ? l3.x : l3.y;
-    const bool hitN = tN < w.hitT, hitF = tF < w.hitT;
-    if (hitN && hitF) { stackPush(a, st, w.sp, make_float2(tF, cF), r.ovf); w.sp++; }
-    next = __float_as_uint(hitN ? cN : cF);
-    return hitN || hitF;
-}
-template <class Stk>
-PT_D bool quadWalkStep(const TraceArgs& a, __amdgpu_buffer_rsrc_t rec, f3 O, f3 D, f3 inv, bool dbl, bool fast, Stk& st,
-                       QuadWalk& w, BvhResult& r)
-{
-    if (w.pop) {
-        w.sp--;
-        if (w.sp < 0) return false;
-        const float2 e = stackPop(st, w.sp, make_float2(kINF, 0.0f));
-        if (e.x >= w.hitT) return true;
-        w.code = __float_as_uint(e.y);
-        r.nodes++;
-    }
-    w.pop = true;
-    const uint32_t off = w.code & ~kLeafBit;
-    const float4 n0 = ldRec4(rec, off), n1 = ldRec4(rec, off + 16u), n2 = ldRec4(rec, off + 32u);
-    const float2 n3 = ldRec2(rec, off + 48u);
-    if (w.code & kLeafBit) {   // a popped leaf: its line in its parent's record
-        quadLeaf(n0, n1, n2, O, D, dbl, w, r);
-        return true;
-    }
-    const float4 a0 = ldRec4(rec, off + 64u), a1 = ldRec4(rec, off + 80u), a2 = ldRec4(rec, off + 96u);
-    const float2 a3 = ldRec2(rec, off + 112u);
-    const float4 b0 = ldRec4(rec, off + 128u), b1 = ldRec4(rec, off + 144u), b2 = ldRec4(rec, off + 160u);
-    const float2 b3 = ldRec2(rec, off + 176u);
-    uint32_t x;
-    if (!quadInner(a, n0, n1, n2, n3, O, inv, fast, st, w, r, x)) return true;
-    // the child taken: its line is line 1 (A) or line 2 (B)
-    const bool isB = x == __float_as_uint(n3.y);
-    const float4 x0 = isB ? b0 : a0, x1 = isB ? b1 : a1, x2 = isB ? b2 : a2;
-    const float2 x3 = isB ? b3 : a3;
-    if (x & kLeafBit) { quadLeaf(x0, x1, x2, O, D, dbl, w, r); return true; }
-    uint32_t y;
-    if (!quadInner(a, x0, x1, x2, x3, O, inv, fast, st, w, r, y)) return true;
-    w.code = y;
-    w.pop = false;
-    return true;
-}
-template <class Stk>
-PT_D void bvhWalkQuads(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float curT, float& hitT, Stk& st, BvhResult& r)
-{
-    QuadWalk w;
-    w.code = a.bvh_quad_root; w.hitT = hitT; w.sp = 0;
-    w.pop = !(curT < hitT);
-    w.lookup = false;
-    w.triID = 0.0f; w.triU = 0.0f; w.triV = 0.0f;
-    const bool fast = pairWalkFast(O, inv);
-    const __amdgpu_buffer_rsrc_t rec = uniformRsrc(a.bvh_quads, a.bvh_quads_bytes);
-#ifdef PT_SECPROF
-    r.steps = 0;
-    while (quadWalkStep(a, rec, O, D, inv, dbl, fast, st, w, r)) r.steps++;
-#else
-    while (quadWalkStep(a, rec, O, D, inv, dbl, fast, st, w, r)) {}
-#endif
-    hitT = w.hitT;
-    if (w.lookup) { r.triID = w.triID; r.triU = w.triU; r.triV = w.triV; r.lookup = true; }
+    hitT = hT;
+    if (tID >= 0.0f) { r.triID = tID; r.triU = tU; r.triV = tV; r.lookup = true; }
 }
 
 // ------------------------------------------------------------------------------ restart-trail walk
@@ -958,9 +654,7 @@ PT_D float2 trailRestart(const TraceArgs& a, const PairBufs& b, f3 O, f3 inv, bo
     uint32_t code = a.bvh_top_base + ((1u << p) - 1u + (w.dir >> (31 - p))) * 64u;
     uint32_t l = kRootBit >> p;
     for (;;) {
-#ifdef PT_SECPROF
-        r.restarts++;   // experiment builds: the restart descents' record loads
-#endif
+        secRestart(r);
         const float4 r0 = ldRec4(b.rec, code), r1 = ldRec4(b.rec, code + 16u), r2 = ldRec4(b.rec, code + 32u);
         const float2 r3 = ldRec2(b.rec, code + 48u);
         float tA, tB;
@@ -1039,12 +733,7 @@ PT_D void bvhWalkTrail(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     w.lookup = false;
     const bool fast = pairWalkFast(O, inv);
     const PairBufs b = pairBufs(a);
-#ifdef PT_SECPROF
-    r.steps = 0;
-    while (trailWalkStep<R>(a, b, O, D, inv, dbl, fast, ring, stride, slot, w, r)) r.steps++;
-#else
-    while (trailWalkStep<R>(a, b, O, D, inv, dbl, fast, ring, stride, slot, w, r)) {}
-#endif
+    while (trailWalkStep<R>(a, b, O, D, inv, dbl, fast, ring, stride, slot, w, r)) secWalkStep(r, false, 0u);
     hitT = w.hitT;
     if (w.lookup) { r.triID = w.triID; r.triU = w.triU; r.triV = w.triV; r.lookup = true; }
 }

@@ -464,89 +464,6 @@ __global__ __launch_bounds__(256) void pt_pairs_top(const float4* rec, uint32_t 
     }
 }
 
-// The implicit top levels (PT_HEAP_LEVELS, pt_args.h): slot idx at depth p = floor(log2(idx + 1)) is
-// the node the path of bits (idx + 1 - 2^p) reaches from the root (MSB first, 1 = the right child),
-// copied from the record array: an inner record whole, a leaf record with a NaN marker in its
-// twelfth float; zero where the path met a leaf earlier (never visited)
-__global__ __launch_bounds__(256) void pt_pairs_heap(const float4* rec, uint32_t root, float4* heap, unsigned slots)
-{
-    const unsigned idx = blockIdx.x * 256u + threadIdx.x;
-    if (idx >= slots) return;
-    const int p = 31 - __builtin_clz(idx + 1u);
-    const unsigned path = idx + 1u - (1u << p);
-    uint32_t code = root;
-    bool ok = true;
-    for (int j = 0; j < p; j++) {
-        if (code & kLeafBit) { ok = false; break; }
-        const float4 c = rec[code / 16u + 3u];
-        code = __float_as_uint(((path >> (p - 1 - j)) & 1u) ? c.y : c.x);
-    }
-    float4* o = heap + 4ull * idx;
-    const float4 z = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    if (!ok) { o[0] = z; o[1] = z; o[2] = z; o[3] = z; return; }
-    const unsigned at = (code & ~kLeafBit) / 16u;
-    o[0] = rec[at]; o[1] = rec[at + 1u];
-    float4 r2 = rec[at + 2u];
-    if (code & kLeafBit) { r2.w = __uint_as_float(0x7fc00000u); o[3] = z; }
-    else o[3] = rec[at + 3u];
-    o[2] = r2;
-}
-
-// Two-level records (PROG_QUAD, bvhWalkQuads in pt_device.h): per inner node n (by inner rank r,
-// 192 B at r * 192) its child-pair line, then each child's own line - the child's child-pair line if
-// it is inner, its leaf triangle line if not. Codes: innerRank * 192 for an inner node, kLeafBit |
-// the offset of the leaf's line in its parent's record for a leaf. A leaf root gets one line of its
-// own after the records (at n_inner * 192).
-PT_D uint32_t quadCode(const float* code, const unsigned char* inner, unsigned c, uint32_t parentOff, unsigned slot)
-{
-    return inner[c] ? (uint32_t)code[c] * 192u : kLeafBit | (parentOff + 64u * slot);
-}
-// node m's child-pair line with two-level codes (m inner; its record at mOff)
-PT_D void quadPairLine(const float4* aabb, long long texels, const float* code, const unsigned char* inner, unsigned m,
-                       uint32_t mOff, float4* o)
-{
-    const float fm = (float)m;
-    const float4 c1 = fetch32(aabb, texels, fm * 2.0f + 1.0f);
-    const float idA = fm + 1.0f, idB = c1.x;
-    const float4 a0 = fetch32(aabb, texels, idA * 2.0f), a1 = fetch32(aabb, texels, idA * 2.0f + 1.0f);
-    const float4 b0 = fetch32(aabb, texels, idB * 2.0f), b1 = fetch32(aabb, texels, idB * 2.0f + 1.0f);
-    pairLineWrite(o, a0, a1, b0, b1);
-    o[3] = make_float4(__uint_as_float(quadCode(code, inner, m + 1u, mOff, 1u)),
-                       __uint_as_float(quadCode(code, inner, (unsigned)idB, mOff, 2u)), 0.0f, 0.0f);
-}
-// leaf m's triangle line: v0, e1 = v1 - v0, e2 = v2 - v0, idObject (as the leaf records of pt_pairs_build)
-PT_D void quadLeafLine(const float4* aabb, long long texels, const float4* tri, long long tri_texels, unsigned m, float4* o)
-{
-    const float hdr = fetch32(aabb, texels, (float)m * 2.0f).x;
-    const float id = 8.0f * hdr;
-    const float4 t0 = fetch32(tri, tri_texels, id), t1 = fetch32(tri, tri_texels, id + 1.0f),
-                 t2 = fetch32(tri, tri_texels, id + 2.0f);
-    const f3 v0 = mk(t0.x, t0.y, t0.z), e1 = mk(t0.w, t1.x, t1.y) - v0, e2 = mk(t1.z, t1.w, t2.x) - v0;
-    o[0] = make_float4(v0.x, v0.y, v0.z, e1.x);
-    o[1] = make_float4(e1.y, e1.z, e2.x, e2.y);
-    o[2] = make_float4(e2.z, hdr, 0.0f, 0.0f);
-    o[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-}
-__global__ __launch_bounds__(256) void pt_quads_build(const float4* aabb, long long texels, const float4* tri,
-                                                      long long tri_texels, unsigned nrec, const float* code,
-                                                      const unsigned char* inner, float4* out, unsigned n_inner)
-{
-    const unsigned n = blockIdx.x * 256u + threadIdx.x;
-    if (n >= nrec) return;
-    if (!inner[n]) {
-        if (n == 0u) quadLeafLine(aabb, texels, tri, tri_texels, 0u, out + 12ull * n_inner);   // a leaf root
-        return;
-    }
-    const uint32_t off = (uint32_t)code[n] * 192u;
-    float4* o = out + off / 16u;
-    quadPairLine(aabb, texels, code, inner, n, off, o);
-    const unsigned idA = n + 1u, idB = (unsigned)fetch32(aabb, texels, (float)n * 2.0f + 1.0f).x;
-    if (inner[idA]) quadPairLine(aabb, texels, code, inner, idA, (uint32_t)code[idA] * 192u, o + 4);
-    else quadLeafLine(aabb, texels, tri, tri_texels, idA, o + 4);
-    if (inner[idB]) quadPairLine(aabb, texels, code, inner, idB, (uint32_t)code[idB] * 192u, o + 8);
-    else quadLeafLine(aabb, texels, tri, tri_texels, idB, o + 8);
-}
-
 // ------------------------------------------------------------------------------ self-test
 // every binary32 pattern with bits 31..24 == hi: fast device sequence vs the IEEE operation it
 // stands for (NaN == NaN); one atomic per wave with a mismatch
@@ -600,7 +517,6 @@ __global__ void pt_math_probe_kernel(int op, const float* x, const float* y, flo
 PT_WALK_LAUNCHERS(ref)
 PT_WALK_LAUNCHERS(pairs)
 PT_WALK_LAUNCHERS(trail)
-PT_WALK_LAUNCHERS(quad)
 #undef PT_WALK_LAUNCHERS
 
 extern "C" {
@@ -616,7 +532,6 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
     case pt::WALK_REF: return pt_launch_trace_ref(prog, count, a, grid, block, s);
     case pt::WALK_PAIRS: return pt_launch_trace_pairs(prog, count, a, grid, block, s);
     case pt::WALK_TRAIL: return pt_launch_trace_trail(prog, count, a, grid, block, s);
-    case pt::WALK_QUAD: return pt_launch_trace_quad(prog, count, a, grid, block, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -639,7 +554,6 @@ hipError_t pt_launch_persist(int prog, int count, const pt::TraceArgs* a, const 
     case pt::WALK_REF: return pt_launch_persist_ref(prog, count, a, w, tiles_x, n_wave_tiles, per_wave, refill, grid, block, s);
     case pt::WALK_PAIRS: return pt_launch_persist_pairs(prog, count, a, w, tiles_x, n_wave_tiles, per_wave, refill, grid, block, s);
     case pt::WALK_TRAIL: return pt_launch_persist_trail(prog, count, a, w, tiles_x, n_wave_tiles, per_wave, refill, grid, block, s);
-    case pt::WALK_QUAD: return pt_launch_persist_quad(prog, count, a, w, tiles_x, n_wave_tiles, per_wave, refill, grid, block, s);
     default: return hipErrorInvalidValue;
     }
 }
@@ -664,8 +578,7 @@ hipError_t pt_launch_pairs_pass(int pass, const float4* aabb, long long texels, 
     return hipGetLastError();
 }
 
-// the restart-trail passes: 1 links, 2 depth, 3 top (rec = the record array, top its jump table);
-// 4 the implicit top levels of PT_HEAP_LEVELS builds
+// the restart-trail passes: 1 links, 2 depth, 3 top (rec = the record array, top its jump table)
 hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, unsigned nrec, const unsigned char* inner,
                                 unsigned* parent, unsigned* refs, unsigned* flag, const float4* rec, uint32_t root,
                                 float4* top, hipStream_t s)
@@ -675,21 +588,8 @@ hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, 
     case 1: hipLaunchKernelGGL(pt::pt_pairs_links, nodes, b256, 0, s, aabb, texels, nrec, inner, parent, refs, flag); break;
     case 2: hipLaunchKernelGGL(pt::pt_pairs_depth, nodes, b256, 0, s, nrec, parent, refs, flag); break;
     case 3: hipLaunchKernelGGL(pt::pt_pairs_top, dim3(1), b256, 0, s, rec, root, top); break;
-    case 4:   // the implicit top levels (PT_HEAP_LEVELS builds; top = their first slot)
-        if (pt::kHeapSlots == 0) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(pt::pt_pairs_heap, dim3((pt::kHeapSlots + 255) / 256), b256, 0, s, rec, root, top, pt::kHeapSlots);
-        break;
     default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
-}
-
-hipError_t pt_launch_quads_build(const float4* aabb, long long texels, const float4* tri, long long tri_texels,
-                                 unsigned nrec, const float* code, const unsigned char* inner, float4* out,
-                                 unsigned n_inner, hipStream_t s)
-{
-    hipLaunchKernelGGL(pt::pt_quads_build, dim3((nrec + 255) / 256), dim3(256), 0, s, aabb, texels, tri, tri_texels, nrec,
-                       code, inner, out, n_inner);
     return hipGetLastError();
 }
 

@@ -29,6 +29,7 @@ struct Cnt {
                                // [9] walk max scratch, [10] wave walk iterations, [11] longest lane's walk steps)
     unsigned lane_steps;
     unsigned sget, sget_slab, sput, sput_slab;   // stack pops / pushes, and those beyond the LDS levels
+    unsigned bounce;                             // SceneIntersect calls so far (the walk statistics' bounce)
 #endif
 };
 // section profile (experiment builds only, -DPT_SECPROF): the wave's shader clock between marks,

@@ -125,7 +125,6 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
         const float rootT = box(mk(rb[0], rb[1], rb[2]), mk(rb[3], rb[4], rb[5]), O, inv);
         auto walk = [&]() {
             if (kTrail<PROG>) bvhWalkTrail<kRingOf<PROG>>(a, O, D, inv, dbl, rootT, h.t, (lds_float2*)lds, LS, lane_slot, br);
-            else if (kQuad<PROG>) bvhWalkQuads(a, O, D, inv, dbl, rootT, h.t, st, br);
             else bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
         };
 #ifdef PT_SECPROF
@@ -147,6 +146,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     if (COUNT) { cnt.node += br.nodes; cnt.leaf += br.leaves; cnt.ovf += br.ovf; }
 #ifdef PT_SECPROF
     if (COUNT) { cnt.sget += st.n_get; cnt.sget_slab += st.n_get_slab + br.restarts; cnt.sput += st.n_put; cnt.sput_slab += st.n_put_slab; }
+    br.ws.flush(a.walk_stat, cnt.bounce++);
 #endif
     PT_SEC(cnt, 2);
     if (br.lookup) meshHit<PROG, COUNT>(a, br.triID, br.triU, br.triV, h, cnt);
@@ -180,19 +180,11 @@ PT_D float xorq(float v, int m) { return __shfl_xor(v, m, 64); }
 // longest-first dispatch: wave durations (shader clock) in 8 log-scale buckets per octave (pt_order_build)
 constexpr int kCostBuckets = 128;
 
-// Workgroups of kTraceBlock lanes. At one wave per workgroup (64, the default) every 8x8 wave tile
-// is its own workgroup: a wave that finishes frees its LDS (stack + G-buffer, 5.5 KB) at once,
-// instead of holding a 4-wave workgroup's 22.5 KB until the slowest of the four (sky next to
-// mesh) is done - LDS is what caps residency at 7 waves/SIMD.
-#ifndef PT_TRACE_BLOCK
-#define PT_TRACE_BLOCK 64
-#endif
-constexpr int kTraceBlock = PT_TRACE_BLOCK;
-#ifndef PT_TILE_GROUPS
-#define PT_TILE_GROUPS 1
-#endif
-constexpr int kTraceSub = 4 / (kTraceBlock / 64);   // workgroups per 16x16 tile
-static_assert(kTraceBlock == 64 || kTraceBlock == 256, "trace workgroups are one wave or one 16x16 tile");
+// One-wave workgroups: every 8x8 wave tile is its own workgroup, so a wave that finishes frees its
+// LDS (stack + G-buffer, 5 KB) at once, instead of holding a 4-wave workgroup's share until the
+// slowest of the four (sky next to mesh) is done - LDS is what caps residency.
+constexpr int kTraceBlock = 64;
+constexpr int kTraceSub = 4;   // workgroups per 16x16 tile
 
 // Which pixel a lane of pt_trace shades: the 8x8 wave tile of this wave inside its 16x16 tile
 // (grid = tiles_x * kTraceSub x bands). Launch slots come in runs of 32 workgroups = 8 tiles x 4
@@ -205,69 +197,49 @@ static_assert(kTraceBlock == 64 || kTraceBlock == 256, "trace workgroups are one
 // bounce; a 4x4 block waits on fewer of them than an 8x8 one, so the kernel's critical path (the
 // slowest tiles' waves, which start first and end last when a few tiles dominate, as the helmet's do)
 // shortens. Which lane shades which pixel never changes what a pixel computes: same bits.
-// False for the grid's padding. (PT_RECOMPUTE_PLACE builds evaluate it again after the path.)
+// False for the grid's padding.
 struct TracePlace {
     int px, py, part;
     unsigned costIdx;
 };
-PT_D bool tracePlace(const TraceArgs& a, int lane, bool first, TracePlace& pl)
+PT_D bool tracePlace(const TraceArgs& a, int lane, TracePlace& pl)
 {
-    int wave, tx, part = -1;
-    unsigned bY, costIdx = ~0u;
-    if (kTraceSub == 4 && PT_TILE_GROUPS) {
-        const unsigned tiles_x = gridDim.x / 4u, ntiles = a.ntiles;
-        const unsigned K = (a.order && a.split) ? *a.split : 0u;   // chosen by pt_order_build
-        const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
-        unsigned slot;
-        constexpr unsigned kPer = 4u * kSplitParts;   // workgroups per split tile
-        if (L < kPer * K) {
-            const unsigned g = L / (8u * kPer), r = L % (8u * kPer);
-            slot = g * 8u + (r & 7u);
-            wave = (int)((r >> 3) / kSplitParts);
-            part = (int)((r >> 3) % kSplitParts);
-        } else {
-            const unsigned L2 = L - kPer * K;
-            if (L2 >= 4u * (ntiles - K)) return false;
-            const unsigned g = L2 >> 5, r = L2 & 31u;
-            const unsigned T = min(8u, ntiles - K - g * 8u);
-            slot = K + g * 8u + r % T;
-            wave = (int)(r / T);
-        }
-        const unsigned tile = a.order ? a.order[slot] : slot;
-        if (first && slot < a.prio_tiles) __builtin_amdgcn_s_setprio(3);   // the critical path: issue first
-        tx = (int)(tile % tiles_x);
-        bY = tile / tiles_x;
-        costIdx = tile * 4u + (unsigned)wave;
-    } else if (kTraceSub == 1) {
-        wave = (int)(threadIdx.x >> 6);
-        tx = (int)blockIdx.x;
-        bY = blockIdx.y;
+    int wave, part = -1;
+    const unsigned tiles_x = gridDim.x / 4u, ntiles = a.ntiles;
+    const unsigned K = (a.order && a.split) ? *a.split : 0u;   // chosen by pt_order_build
+    const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
+    unsigned slot;
+    constexpr unsigned kPer = 4u * kSplitParts;   // workgroups per split tile
+    if (L < kPer * K) {
+        const unsigned g = L / (8u * kPer), r = L % (8u * kPer);
+        slot = g * 8u + (r & 7u);
+        wave = (int)((r >> 3) / kSplitParts);
+        part = (int)((r >> 3) % kSplitParts);
     } else {
-        wave = (int)(blockIdx.x & 3u);
-        tx = (int)(blockIdx.x >> 2);
-        bY = blockIdx.y;
+        const unsigned L2 = L - kPer * K;
+        if (L2 >= 4u * (ntiles - K)) return false;
+        const unsigned g = L2 >> 5, r = L2 & 31u;
+        const unsigned T = min(8u, ntiles - K - g * 8u);
+        slot = K + g * 8u + r % T;
+        wave = (int)(r / T);
     }
-    // lane bits (x0, y0, x1, x2, y1, y2) of an 8x8 block, (x0, y0, x1, y1) of a split tile's 4x4, or
-    // (x0, y0) of its 2x2 quads
+    const unsigned tile = a.order ? a.order[slot] : slot;
+    if (slot < a.prio_tiles) __builtin_amdgcn_s_setprio(3);   // the critical path: issue first
+    const int tx = (int)(tile % tiles_x);
+    const unsigned bY = tile / tiles_x;
+    // lane bits (x0, y0, x1, x2, y1, y2) of an 8x8 block, or (x0, y0, x1, y1) of a split tile's 4x4
     int lx, ly;
     if (part < 0) { lx = (lane & 1) | ((lane >> 1) & 6); ly = ((lane >> 1) & 1) | ((lane >> 3) & 6); }
-    else if (kSplitParts == 4) {
+    else {
         lx = (part & 1) * 4 + ((lane & 1) | ((lane >> 1) & 2));
         ly = (part >> 1) * 4 + (((lane >> 1) & 1) | ((lane >> 2) & 2));
-    } else { lx = (part & 3) * 2 + (lane & 1); ly = (part >> 2) * 2 + ((lane >> 1) & 1); }
+    }
     const int band = (int)bY * a.num_parts + a.part;            // global 16-row band of this block
     pl.px = tx * kTile + (wave & 1) * 8 + lx;
     pl.py = band * kTile + (wave >> 1) * 8 + ly;
     pl.part = part;
-    pl.costIdx = costIdx;
+    pl.costIdx = tile * 4u + (unsigned)wave;
     return true;
-}
-// the lane id, computed where it is asked for (not a value the compiler keeps live across the path)
-PT_D int laneAgain()
-{
-    int l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
 }
 
 template <int PROG, bool COUNT>
@@ -282,7 +254,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     const unsigned long long w0_ = wall_clock64();
 #endif
     TracePlace pl;
-    if (!tracePlace(a, lane, true, pl)) return;   // the grid's padding
+    if (!tracePlace(a, lane, pl)) return;   // the grid's padding
     const int px = pl.px, py = pl.py;
     // stack levels >= kStackLds: a global slab [level][lane of the grid] (a private array would be
     // scratch, which the runtime reserves for every resident wave)
@@ -298,6 +270,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     cnt.sec = lds_sec;
     cnt.lane_steps = 0;
     cnt.sget = cnt.sget_slab = cnt.sput = cnt.sput_slab = 0;
+    cnt.bounce = 0;
 #endif
     // G-buffer fields beyond the LDS ones: 8 - kGoutLdsOf floats per lane after the slab's stack
     // levels, [lane][field] (pt_capi.cpp spill_reserve)
@@ -314,24 +287,10 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         r = radiance<PROG, COUNT, kTraceBlock>(a, p, gl, lds_stack, tid, deep, cnt);
     }
     PT_SEC(cnt, 4);
-#ifdef PT_RECOMPUTE_PLACE
-    // experiment: the lane's place again (see tracePlace), so that none of it is kept live across the
-    // path: 56 -> 40 B of scratch per lane on the dragon stand-in, yet 0.6-2.8 % slower (the reload of
-    // the tile order sits on every wave's tail; profiles/r03_ab_place.txt)
-    asm volatile("" ::: "memory");
-    const int lane2 = kTraceBlock == 64 ? laneAgain() : (int)(threadIdx.x & 63u);
-    tracePlace(a, lane2, false, pl);
-    const int px2 = pl.px, py2 = pl.py;
-    const bool active2 = px2 < ((a.width + 1) & ~1) && py2 < ((a.height + 1) & ~1) && (pl.part < 0 || lane2 < (int)(64u / kSplitParts));
-    const GOut g = (GOutLds<kTraceBlock, kGoutLdsOf<PROG>, kGoutOrderOf<PROG>>{ (lds_float*)lds_gout, kTraceBlock == 64 ? (unsigned)lane2 : threadIdx.x, gx }).load();
-#else
-    const int lane2 = lane, px2 = px, py2 = py;
-    const bool active2 = active;
     const GOut g = gl.load();
-#endif
 
     // ---- 2x2 fine derivatives (js/PathTracingCommon.js:1306-1320): partner lanes ^1 (x) and ^2 (y)
-    const bool xodd = lane2 & 1, yodd = lane2 & 2;
+    const bool xodd = lane & 1, yodd = lane & 2;
     auto ddx = [&](float v) { float o = xorq(v, 1); return xodd ? v - o : o - v; };
     auto ddy = [&](float v) { float o = xorq(v, 2); return yodd ? v - o : o - v; };
     float dNx = fabsf(ddx(g.nrm.x)) + fabsf(ddy(g.nrm.x));
@@ -378,15 +337,15 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         atomicAdd(&C[C_OVERFLOW], (unsigned long long)cnt.ovf);
         atomicAdd(&C[C_HDR], (unsigned long long)cnt.hdr);
     }
-    if (a.cost && pl.costIdx != ~0u && lane2 == 0) {   // this wave's duration, averaged with the tile's
+    if (a.cost && lane == 0) {   // this wave's duration, averaged with the tile's
         // history, for the next order (a split tile's four parts share their quadrant's entry)
         const unsigned long long dur = min(clock64() - t_start, 0xffffffffull);
         a.cost[pl.costIdx] = (unsigned)((dur + (unsigned long long)a.cost[pl.costIdx]) >> 1);
     }
-    if (!active2 || px2 >= a.width || py2 >= a.height) return;   // quad helper outside the target, idle lane
+    if (!active || px >= a.width || py >= a.height) return;   // quad helper outside the target, idle lane
 
     // ---- progressive accumulation (js/PathTracingCommon.js:1326-1357)
-    const long long pi = (long long)py2 * a.width + px2;
+    const long long pi = (long long)py * a.width + px;
     // history and accumulation stream once per frame: non-temporal loads and stores, so that they
     // displace fewer BVH records in L2 (helmet -2 %, sky+dragon -1.5 %, bunny -1 %, dragon +-0)
     float4 prev;

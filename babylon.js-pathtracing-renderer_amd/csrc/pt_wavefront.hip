@@ -239,7 +239,6 @@ __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b
         BvhResult br = { 0.0f, 0.0f, 0.0f, false, 0u, 0u, 0u };
         WfStack st{ (lds_float2*)lds, tid, (glb_float2*)deep, dstride };
         if (kTrail<PROG>) bvhWalkTrail<kRingOf<PROG>>(a, O, D, inv, dbl, rootT, hitT, (lds_float2*)lds, kBlock, tid, br);
-        else if (kQuad<PROG>) bvhWalkQuads(a, O, D, inv, dbl, rootT, hitT, st, br);
         else if (kPairs<PROG>) bvhWalkPairs(a, O, D, inv, dbl, rootT, hitT, st, br);
         else bvhWalkRef(a, O, D, inv, dbl, c0, c1, rootT, hitT, st, br);
         const unsigned nodes = br.nodes, leaves = br.leaves, ovf = br.ovf;

@@ -168,20 +168,19 @@ class Engine:
         self.check(lib().pt_set_backend(self.ctx, {"megakernel": 0, "wavefront": 1, "persistent": 2}[backend]),
                    "pt_set_backend")
 
-    BVH_LAYOUTS = {"reference": 0, "pairs": 1, "trail": 2, "quads": 3}
+    BVH_LAYOUTS = {"reference": 0, "pairs": 1, "trail": 2}
 
     def set_bvh_layout(self, layout):
         """'pairs' (default: child-pair records with the short stack, falls back to the reference
         walk for malformed trees), 'trail' (the same records walked stacklessly with the restart
-        trail; trees it cannot walk keep 'pairs'), 'quads' (two-level records: one fetch per two
-        levels) or 'reference' (walk the reference texel pairs):
+        trail; trees it cannot walk keep 'pairs') or 'reference' (walk the reference texel pairs):
         same bits, different memory path."""
         self.check(lib().pt_set_bvh_layout(self.ctx, self.BVH_LAYOUTS[layout]), "pt_set_bvh_layout")
 
     def bvh_layout_used(self):
         """Layout walked by the last glTF draw: 'trail', 'pairs', 'reference' or None."""
         v = lib().pt_bvh_layout_used(self.ctx)
-        return {0: "reference", 1: "pairs", 2: "trail", 3: "quads"}.get(v)
+        return {0: "reference", 1: "pairs", 2: "trail"}.get(v)
 
     def last_render_ms(self, program):
         ms = ctypes.c_float(0)

@@ -36,6 +36,7 @@ configs[4]'s 1024-frame converging run timed whole (`converge_1024spp`). Prints 
 """
 import argparse
 import csv
+import datetime
 import glob
 import json
 import math
@@ -57,6 +58,8 @@ PEAK_HBM_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-le
 BYTES = {"node_fetches": 32, "leaf_tests": 48, "hit_lookups": 128, "rgba8_taps": 4, "hdr_taps": 16}
 PIXEL_IO = 32                  # previousBuffer texel read + accumulation texel write (+4 B blue noise = an rgba8 tap)
 CONVERGED_SPP = 1024           # BASELINE configs[4]
+PG_TIMEOUT_S = 240             # N > 1: process-group / store timeout, well inside the driver's per-run budget
+PARITY_FRAMES = 2              # N > 1: recorded frames replayed after the timed region and compared with one GPU
 
 METRICS = {
     "bunny": "Mpaths/s + achieved HBM GB/s, StanfordBunny 1080p 1spp (BASELINE configs[1])",
@@ -234,12 +237,46 @@ def frame_size_for(args, world):
 
 
 def plan(args, world):
-    """What a run measures, from its arguments (CPU-testable): the frame, the scaling mode and the
-    kernel-timing sample rate."""
+    """What a run measures, from its arguments (CPU-testable): the frame, the scaling mode (none at
+    one GPU), the kernel-timing sample rate, and at N > 1 the recorded frames replayed after the timed
+    region through the N-GPU route and compared bit for bit with a one-GPU render (n_gpu_bitexact)."""
     W, Hh = frame_size_for(args, world)
     fixed = world > 1 and (args.scaling == "strong" or args.size is not None or args.workload == "sky_dragon")
-    return {"width": W, "height": Hh, "scaling": "strong" if fixed else "weak",
-            "event_every": args.event_every or max(1, args.steps // 10)}
+    return {"width": W, "height": Hh, "scaling": None if world == 1 else "strong" if fixed else "weak",
+            "event_every": args.event_every or max(1, args.steps // 10),
+            "parity_frames": PARITY_FRAMES if world > 1 and not getattr(args, "no_check", False) else 0}
+
+
+# ------------------------------------------------------------------------------ N-GPU parity check
+def one_gpu_reference(workload, W, Hh, device, frames):
+    """The recorded frames `frames` (indices) of the workload rendered whole on one GPU by a fresh
+    context: (RGBA8 canvas, RGBA32F accumulation) as numpy arrays, rows in GL order."""
+    import babylon_pt as bp
+    engine = bp.Engine(device)
+    try:
+        player, _, _ = make_player(engine, workload, W, Hh)
+        engine.resize_canvas(W, Hh)
+        for i in frames:
+            player.play_frame(i)
+        engine.sync()
+        return engine.read_canvas(W, Hh), player.textures["pathTracingRenderTarget"].read()
+    finally:
+        engine.dispose()
+
+
+def compare_frames(canvas, acc, ref_canvas, ref_acc):
+    """Bitwise comparison of an N-GPU frame (canvas RGBA8, accumulation RGBA32F) with the one-GPU
+    render of the same frames: the line's n_gpu_bitexact and the differing pixel counts."""
+    import numpy as np
+    canvas, ref_canvas = np.asarray(canvas), np.asarray(ref_canvas)
+    acc, ref_acc = np.ascontiguousarray(acc, np.float32), np.ascontiguousarray(ref_acc, np.float32)
+    if canvas.shape != ref_canvas.shape or acc.shape != ref_acc.shape:
+        return {"n_gpu_bitexact": False, "error": "shape %s / %s vs %s / %s" % (canvas.shape, acc.shape,
+                                                                            ref_canvas.shape, ref_acc.shape)}
+    dc = int((canvas != ref_canvas).any(-1).sum())
+    da = int((acc.view(np.uint32) != ref_acc.view(np.uint32)).any(-1).sum())
+    return {"n_gpu_bitexact": dc == 0 and da == 0, "canvas_pixels_differing": dc, "accumulation_pixels_differing": da,
+            "pixels": int(canvas.shape[0] * canvas.shape[1])}
 
 
 def timed_region(engine, step, first, count, event_every, barrier_sync, program):
@@ -357,11 +394,21 @@ def multipart_main(args, event_every):
     if args.dump_canvas:
         import numpy as np
         np.save(args.dump_canvas, engine.read_canvas(W, Hh))
+    check = None
+    if len(devs) > 1 and not args.no_check:
+        # the recorded frames again (the first clears the history) through the parts, against one GPU
+        idx = list(range(PARITY_FRAMES))
+        for i in idx:
+            player.play_frame(i)
+        engine.sync()
+        got = engine.read_canvas(W, Hh), player.textures["pathTracingRenderTarget"].read()
+        check = compare_frames(*got, *one_gpu_reference(args.workload, W, Hh, devs[0], idx))
+        check["frames"] = PARITY_FRAMES
     line = {"metric": baseline_metric() if args.workload == "dragon" else METRICS[args.workload],
             "value": round(W * Hh * args.steps / elapsed / 1e6, 2), "unit": "Mpaths/s",
             "n_gpus": len(set(devs)), "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "strong" if len(devs) > 1 else "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "strong" if len(devs) > 1 else None, "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: " + DATA[args.workload], "engine": "multipart", "parts_seen": engine.parts,
             "devices": devs,
             "config": {"workload": "%s_%s_%dx%d" % (program, args.workload, W, Hh), "width": W, "height": Hh,
@@ -370,6 +417,9 @@ def multipart_main(args, event_every):
                                  "as peer copies inside pt_render (hipMemcpy2DAsync, event-ordered)"},
             "kernel_timing": "HIP events around every %d-th timed frame's draws, slowest part (%d launches)" % (event_every, n),
             "kernel_ms": km}
+    if check is not None:
+        line["n_gpu_bitexact"] = check["n_gpu_bitexact"]
+        line["n_gpu_check"] = check
     print(json.dumps(line), flush=True)
     engine.dispose()
     return 0
@@ -386,14 +436,42 @@ def multipart_child(args, world, W, Hh):
     cmd = [sys.executable, os.path.abspath(__file__), "--engine", "multipart", "--gpus", str(world),
            "--devices", ",".join(str(d) for d in range(world)), "--size", "%dx%d" % (W, Hh), "--workload", args.workload,
            "--steps", str(steps), "--warmup", str(min(args.warmup, 10)), "--cpu-budget", "0", "--no-pmc"]
+    if args.no_check:
+        cmd.append("--no-check")
     try:
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=150)
         if r.returncode != 0:
             return {"error": "exit %d: %s" % (r.returncode, r.stderr[-300:])}
         d = json.loads(r.stdout.strip().splitlines()[-1])
-        return {k: d[k] for k in ("value", "unit", "ms_per_step", "steps", "parts_seen", "devices", "kernel_ms")}
+        return {k: d.get(k) for k in ("value", "unit", "ms_per_step", "steps", "parts_seen", "devices", "kernel_ms",
+                                      "n_gpu_bitexact", "n_gpu_check")}
     except Exception as e:   # noqa: BLE001 - reported in the line
         return {"error": repr(e)[-300:]}
+
+
+def nrank_check(dist, torch, engine, player, route, barrier_sync, gather, acc_t, workload, W, Hh, world, rank, device):
+    """After the timed region: the first PARITY_FRAMES recorded frames (the first clears the history)
+    through the N-rank route - path tracing of each rank's bands, RCCL halos, screenOutput of own
+    bands, the RGBA8 gather - and every rank's RGBA32F bands gathered to rank 0 too; rank 0 renders the
+    same frames whole on its own GPU in a fresh context and compares both bit for bit."""
+    import babylon_pt as bp
+    for i in range(PARITY_FRAMES):
+        route(player.meta["frames"][i])
+    barrier_sync()
+    share = bp.band_view(acc_t, world)[:, rank]
+    send = torch.empty_like(share)
+    glist = [torch.empty_like(share) for _ in range(world)] if rank == 0 else None
+    full = torch.zeros_like(acc_t) if rank == 0 else None
+    bp.gather_bands(dist, acc_t, world, rank, send, glist, full)
+    torch.cuda.synchronize()
+    res = None
+    if rank == 0:
+        canvas = gather.last_frame()[:Hh].cpu().numpy()
+        acc = full[:Hh].cpu().numpy()
+        res = compare_frames(canvas, acc, *one_gpu_reference(workload, W, Hh, device, range(PARITY_FRAMES)))
+        res["frames"] = PARITY_FRAMES
+    dist.barrier()
+    return res
 
 
 def main():
@@ -420,6 +498,8 @@ def main():
     ap.add_argument("--no-anchors", action="store_true",
                     help="N = 1: skip the 4K, scan-like and converged-run fields beside the headline")
     ap.add_argument("--no-multipart", action="store_true", help="N > 1: skip the multipart curve beside the RCCL one")
+    ap.add_argument("--no-check", action="store_true",
+                    help="N > 1: skip the bitwise check of the N-GPU frame against a one-GPU render (n_gpu_bitexact)")
     ap.add_argument("--event-every", type=int, default=None, metavar="K",
                     help="time the kernels with HIP events around every K-th frame of the timed region "
                          "(default: steps // 10, so that about 10 draws are bracketed whatever --steps is)")
@@ -450,7 +530,10 @@ def main():
         import torch
         import torch.distributed as tdist
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # an explicit timeout: a rank that stops answering fails the run (the watchdog aborts the
+        # process) instead of holding the driver's run until its own limit
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local),
+                                 timeout=datetime.timedelta(seconds=PG_TIMEOUT_S))
         dist = tdist
         # one dedicated stream per rank for libpt draws and torch/RCCL work alike (the legacy default
         # stream would not order them: libpt's own stream is non-blocking)
@@ -485,8 +568,8 @@ def main():
         halo = bp.halo_buffers(acc_t, world)
         gather = bp.PipelinedBandGather(dist, world, rank, pad_bands * 16, W, "cuda")
 
-    def step(k):
-        pt_call, cp_call, out_call = player.synth_frame(k)
+    def route(frame):
+        pt_call, cp_call, out_call = frame
         player.play_call(pt_call)
         player.play_call(cp_call)
         if args.no_output:
@@ -500,6 +583,9 @@ def main():
         engine.canvas_wrap(W, Hh, gather.target().data_ptr())
         player.play_call(out_call)
         gather.submit()
+
+    def step(k):
+        route(player.synth_frame(k))
 
     def barrier_sync():
         if dist is not None:
@@ -522,6 +608,11 @@ def main():
             np.save(args.dump_canvas, engine.read_canvas(W, Hh))
         elif rank == 0:
             np.save(args.dump_canvas, gather.last_frame()[:Hh].cpu().numpy())
+
+    check = None
+    if dist is not None and p["parity_frames"]:
+        check = nrank_check(dist, torch, engine, player, route, barrier_sync, gather, acc_t, args.workload, W, Hh,
+                            world, rank, local)
 
     ranks_seen = world
     if dist is not None:
@@ -550,7 +641,8 @@ def main():
             # rank 0's multipart curve runs in a child process on these GPUs meanwhile: wait on the
             # host (the rendezvous store), not in a device-side RCCL barrier that would hold CUs
             dist.barrier()
-            dist.distributed_c10d._get_default_store().wait(["bench_multipart_done"])
+            dist.distributed_c10d._get_default_store().wait(["bench_multipart_done"],
+                                                            datetime.timedelta(seconds=PG_TIMEOUT_S))
         dist.barrier()
         dist.destroy_process_group()
         return 0
@@ -609,6 +701,9 @@ def main():
         "roofline": roofline,
     }
     line.update(anchors)
+    if check is not None:
+        line["n_gpu_bitexact"] = check["n_gpu_bitexact"]
+        line["n_gpu_check"] = check
     if args.workload == "sky_dragon":
         line["converge_%dspp_s" % CONVERGED_SPP] = round(CONVERGED_SPP * elapsed / args.steps, 3)
         line["converge_note"] = ("%d frames timed; seconds for %d progressive frames = %s"
@@ -630,4 +725,12 @@ def main():
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    try:
+        rc = main()
+    except BaseException:   # noqa: BLE001 - any failure of a rank ends it at once, non-zero
+        import traceback
+        traceback.print_exc()
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(1)          # no interpreter teardown (a process group torn down mid-collective can hang)
+    sys.exit(rc)

@@ -167,14 +167,13 @@ int pt_set_backend(pt_ctx* ctx, int backend);
  * those with the reference's short stack (LDS levels, deeper ones in a global slab); PT_BVH_TRAIL
  * walks the same records stacklessly: a restart trail of one bit per tree level plus a per-lane LDS
  * ring of the deepest pending entries, re-descending from a jump table of the top levels when the
- * ring runs dry (no stack memory beyond LDS; trees deeper than 32 levels, or whose nodes have more
- * than one parent, keep PT_BVH_PAIRS). A texture whose links are not exact in-range integers keeps
- * PT_BVH_REFERENCE, the walk over the reference's own texel pairs. PT_BVH_QUADS walks two-level
- * records (an inner node's child pair plus each child's own pair or triangle, 192 B): one fetch per
- * two tree levels, with the short stack. Same nodes, same order, same results every way
- * (js/GLTFModelPathTracing_FragmentShader.js:211-298).
+ * ring runs dry (no stack memory beyond LDS; trees deeper than 28 levels - the reference's
+ * stackLevels[28] - or whose nodes have more than one parent, keep PT_BVH_PAIRS). A texture whose
+ * links are not exact in-range integers keeps PT_BVH_REFERENCE, the walk over the reference's own
+ * texel pairs. Same nodes, same order, same results every way
+ * (js/GLTFModelPathTracing_FragmentShader.js:211-298). Other values: PT_ERR_ARG.
  * pt_bvh_layout_used reports what the last glTF draw of the context walked (-1: none yet). */
-enum pt_bvh_layout { PT_BVH_REFERENCE = 0, PT_BVH_PAIRS = 1, PT_BVH_TRAIL = 2, PT_BVH_QUADS = 3 };
+enum pt_bvh_layout { PT_BVH_REFERENCE = 0, PT_BVH_PAIRS = 1, PT_BVH_TRAIL = 2 };
 int pt_set_bvh_layout(pt_ctx* ctx, int layout);
 int pt_bvh_layout_used(pt_ctx* ctx);
 /* Enqueue this context's work on a caller-owned HIP stream (e.g. torch.cuda.current_stream(), so

@@ -57,7 +57,8 @@ def _plan(argv, world):
     import argparse
     ap = argparse.ArgumentParser()
     for a, kw in (("--size", {}), ("--workload", {"default": "dragon"}), ("--scaling", {"default": "strong"}),
-                  ("--steps", {"type": int, "default": 200}), ("--event-every", {"type": int, "default": None})):
+                  ("--steps", {"type": int, "default": 200}), ("--event-every", {"type": int, "default": None}),
+                  ("--no-check", {"action": "store_true"})):
         ap.add_argument(a, **kw)
     return bench.plan(ap.parse_args(argv), world)
 
@@ -67,14 +68,41 @@ def test_plan_headline_and_scaling_configs():
     configs[3]'s 3840x2160 frame split over the GPUs (strong scaling), the frame the N = 1 line's
     dragon_4k_1gpu field renders on one GPU; --scaling weak keeps N x 2.07 MP; --size and the sky
     workload fix the frame."""
-    assert _plan([], 1) == {"width": 1920, "height": 1080, "scaling": "weak", "event_every": 20}
+    assert _plan([], 1) == {"width": 1920, "height": 1080, "scaling": None, "event_every": 20, "parity_frames": 0}
     for n in (2, 4, 8):
         p = _plan([], n)
         assert (p["width"], p["height"], p["scaling"]) == (3840, 2160, "strong")
+        assert p["parity_frames"] == 2          # the N-GPU frame is checked against one GPU after the timed region
     assert (_plan(["--scaling", "weak"], 8)["width"], _plan(["--scaling", "weak"], 8)["height"]) == (7680, 2160)
     assert _plan(["--scaling", "weak"], 8)["scaling"] == "weak"
     assert (_plan(["--size", "640x480"], 2)["width"], _plan(["--size", "640x480"], 2)["scaling"]) == (640, "strong")
     assert (_plan(["--workload", "sky_dragon"], 1)["width"], _plan(["--workload", "sky_dragon"], 1)["height"]) == (3840, 2160)
+    assert _plan(["--no-check"], 8)["parity_frames"] == 0
+
+
+def test_compare_frames_reports_bitwise_equality():
+    """n_gpu_bitexact: the N-GPU canvas and accumulation against the one-GPU render, bit for bit
+    (a -0.0 / +0.0 or NaN-payload difference counts; a canvas byte counts)."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    rng = np.random.default_rng(1)
+    can = rng.integers(0, 256, (18, 20, 4), dtype=np.uint8)
+    acc = rng.standard_normal((18, 20, 4)).astype(np.float32)
+    r = bench.compare_frames(can, acc, can.copy(), acc.copy())
+    assert r["n_gpu_bitexact"] is True and r["canvas_pixels_differing"] == 0 and r["pixels"] == 360
+    acc2 = acc.copy()
+    acc2[3, 4, 1] = -acc2[3, 4, 1] if acc2[3, 4, 1] == 0 else np.nextafter(acc2[3, 4, 1], np.float32(np.inf))
+    acc2[0, 0, 0] = 0.0
+    acc3 = acc2.copy()
+    acc3[0, 0, 0] = -0.0
+    r = bench.compare_frames(can, acc3, can, acc2)
+    assert r["n_gpu_bitexact"] is False and r["accumulation_pixels_differing"] == 1
+    can2 = can.copy()
+    can2[17, 19, 3] ^= 1
+    r = bench.compare_frames(can2, acc, can, acc)
+    assert r["n_gpu_bitexact"] is False and r["canvas_pixels_differing"] == 1
+    assert bench.compare_frames(can[:4], acc, can, acc)["n_gpu_bitexact"] is False
 
 
 def test_kernel_timing_brackets_about_ten_draws():
@@ -94,12 +122,16 @@ def test_gpus_n_check_launch_reports_the_4k_strong_config():
     assert (d["width"], d["height"], d["scaling"], d["event_every"], d["ranks_seen"]) == (3840, 2160, "strong", 2, 2)
 
 
-def test_multipart_devices_fall_back_to_device_zero():
+def test_multipart_devices_fall_back_to_device_zero(monkeypatch):
     """--engine multipart: one part per visible GPU, or every part on device 0 when fewer are visible
     (the one-GPU rehearsal of the multi-device route); --devices fixes them."""
     sys.path.insert(0, ROOT)
     import bench
     import argparse
+    import torch
     a = argparse.Namespace(devices=None, gpus=3)
-    assert bench.multipart_devices(a) == [0, 0, 0]          # no GPU visible here
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 1)
+    assert bench.multipart_devices(a) == [0, 0, 0]          # fewer GPUs visible than parts
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    assert bench.multipart_devices(a) == [0, 1, 2]
     assert bench.multipart_devices(argparse.Namespace(devices="0,1", gpus=2)) == [0, 1]

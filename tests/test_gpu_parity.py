@@ -182,7 +182,7 @@ def _replay_gpu(engine, meta, frames=None, width=None, height=None, parts=1, spl
 
 
 # (schedule, BVH layout): every combination must give the same bits
-BACKENDS = [(b, l) for b in ("megakernel", "persistent", "wavefront") for l in ("pairs", "trail", "quads", "reference")]
+BACKENDS = [(b, l) for b in ("megakernel", "persistent", "wavefront") for l in ("pairs", "trail", "reference")]
 
 
 @pytest.fixture(params=BACKENDS, ids=["-".join(b) for b in BACKENDS])

@@ -23,55 +23,76 @@ def _band_copy(dst, src, world, rank, rows=slice(0, 16)):
     bp.band_view(dst, world)[:, rank, rows].copy_(bp.band_view(src, world)[:, rank, rows])
 
 
+class _Ranks:
+    """N contexts on device 0 standing for the bench's N ranks on one torch stream (module docstring):
+    frame(calls) runs one frame's three draws through the partitioned route with torch copies in place
+    of the RCCL halo exchange and gather; full_acc / full_can hold the assembled frame."""
+
+    def __init__(self, world, W, Hh, make):
+        import torch
+        import babylon_pt as bp
+        self.world, self.W, self.Hh = world, W, Hh
+        pad = bp.padded_bands(Hh, world)
+        self.stream = torch.cuda.Stream(device=0)
+        torch.cuda.set_stream(self.stream)
+        self.ranks = []
+        for r in range(world):
+            e = bp.Engine(0)
+            e.set_stream(self.stream.cuda_stream)
+            acc = torch.zeros((pad * 16, W, 4), dtype=torch.float32, device="cuda")
+            cpy = torch.zeros((Hh, W, 4), dtype=torch.float32, device="cuda")
+            canvas = torch.zeros((pad * 16, W, 4), dtype=torch.uint8, device="cuda")
+            player = make(e, {"pathTracingRenderTarget": acc.data_ptr(), "screenCopyRenderTarget": cpy.data_ptr()})
+            e.resize_canvas(W, Hh)
+            e.set_row_partition(world, r)
+            e.set_output_partition(True)
+            self.ranks.append((e, player, acc, canvas, cpy))   # the tensors stay alive: libpt holds their pointers
+        self.full_acc = torch.zeros((pad * 16, W, 4), dtype=torch.float32, device="cuda")
+        self.full_can = torch.zeros((pad * 16, W, 4), dtype=torch.uint8, device="cuda")
+
+    def frame(self, calls):
+        import torch
+        world, W, Hh = self.world, self.W, self.Hh
+        pt_call, cp_call, out_call = calls
+        for e, player, acc, canvas, _ in self.ranks:        # path tracing + screenCopy of each rank's bands
+            player.play_call(pt_call)
+            player.play_call(cp_call)
+        for r, (e, player, acc, canvas, _) in enumerate(self.ranks):   # halo rows from the band neighbours
+            lo, hi = (r - 1) % world, (r + 1) % world
+            _band_copy(acc, self.ranks[lo][2], world, lo, slice(14, 16))
+            _band_copy(acc, self.ranks[hi][2], world, hi, slice(0, 2))
+        for e, player, acc, canvas, _ in self.ranks:        # screenOutput of each rank's bands into its canvas
+            e.canvas_wrap(W, Hh, canvas.data_ptr())
+            player.play_call(out_call)
+        for r, (e, player, acc, canvas, _) in enumerate(self.ranks):   # the gather (and the bands' accumulation)
+            _band_copy(self.full_can, canvas, world, r)
+            _band_copy(self.full_acc, acc, world, r)
+        torch.cuda.current_stream().synchronize()
+        return self.full_acc[:Hh].cpu().numpy(), self.full_can[:Hh].cpu().numpy()
+
+    def close(self):
+        import torch
+        for e, *_ in self.ranks:
+            e.set_stream(None)
+            e.dispose()
+        torch.cuda.set_stream(torch.cuda.default_stream(0))
+
+
 @pytest.mark.parametrize("name,world,size", [
     ("gltf_teapot_320x180", 2, None),
     ("gltf_teapot_320x180", 3, (203, 117)),   # a partial last band, halos clipped at the frame's edges
     ("cornell_256", 2, None),
 ])
 def test_torch_stream_ranks_bitexact(name, world, size):
-    import torch
     import babylon_pt as bp
     meta = H.stream(name)
     W, Hh = size or (meta["width"], meta["height"])
-    pad = bp.padded_bands(Hh, world)
-    stream = torch.cuda.Stream(device=0)
-    torch.cuda.set_stream(stream)
     payload = H.texture_payloads(meta, H.mesh(meta)) if meta["scene"] in ("gltf", "hdri") else None
-    ranks = []
+    rk = _Ranks(world, W, Hh, lambda e, rt: bp.StreamPlayer(e, meta, H.bluenoise(), payload, W, Hh, rt))
     try:
-        for r in range(world):
-            e = bp.Engine(0)
-            e.set_stream(stream.cuda_stream)
-            acc = torch.zeros((pad * 16, W, 4), dtype=torch.float32, device="cuda")
-            cpy = torch.zeros((Hh, W, 4), dtype=torch.float32, device="cuda")
-            canvas = torch.zeros((pad * 16, W, 4), dtype=torch.uint8, device="cuda")
-            player = bp.StreamPlayer(e, meta, H.bluenoise(), payload, W, Hh,
-                                     {"pathTracingRenderTarget": acc.data_ptr(), "screenCopyRenderTarget": cpy.data_ptr()})
-            e.resize_canvas(W, Hh)
-            e.set_row_partition(world, r)
-            e.set_output_partition(True)
-            ranks.append((e, player, acc, canvas, cpy))   # the tensors stay alive: libpt holds their pointers
-        full_acc = torch.zeros((pad * 16, W, 4), dtype=torch.float32, device="cuda")
-        full_can = torch.zeros((pad * 16, W, 4), dtype=torch.uint8, device="cuda")
         ref_acc, ref_can, _ = H.oracle_replay(meta, width=W, height=Hh, with_output=True)
         for i, frame in enumerate(meta["frames"]):
-            pt_call, cp_call, out_call = frame
-            for e, player, acc, canvas, _ in ranks:        # path tracing + screenCopy of each rank's bands
-                player.play_call(pt_call)
-                player.play_call(cp_call)
-            for r, (e, player, acc, canvas, _) in enumerate(ranks):   # halo rows from the band neighbours
-                lo, hi = (r - 1) % world, (r + 1) % world
-                _band_copy(acc, ranks[lo][2], world, lo, slice(14, 16))
-                _band_copy(acc, ranks[hi][2], world, hi, slice(0, 2))
-            for e, player, acc, canvas, _ in ranks:        # screenOutput of each rank's bands into its canvas
-                e.canvas_wrap(W, Hh, canvas.data_ptr())
-                player.play_call(out_call)
-            for r, (e, player, acc, canvas, _) in enumerate(ranks):   # the gather (and the bands' accumulation)
-                _band_copy(full_can, canvas, world, r)
-                _band_copy(full_acc, acc, world, r)
-            torch.cuda.current_stream().synchronize()
-            got_acc = full_acc[:Hh].cpu().numpy()
-            got_can = full_can[:Hh].cpu().numpy()
+            got_acc, got_can = rk.frame(frame)
             bad = (got_acc.view(np.uint32) != ref_acc[i].view(np.uint32)).any(-1)
             assert not bad.any(), "frame %d accumulation: %d of %d pixels differ (rows %s, columns %d..%d)" % (
                 i, bad.sum(), bad.size, sorted(set(np.nonzero(bad)[0].tolist()))[:40], np.nonzero(bad)[1].min(),
@@ -79,7 +100,30 @@ def test_torch_stream_ranks_bitexact(name, world, size):
             badc = (got_can != ref_can[i]).any(-1)
             assert not badc.any(), "frame %d canvas: %d of %d pixels differ" % (i, badc.sum(), badc.size)
     finally:
-        for e, *_ in ranks:
-            e.set_stream(None)
-            e.dispose()
-        torch.cuda.set_stream(torch.cuda.default_stream(0))
+        rk.close()
+
+
+@pytest.mark.parametrize("workload,world,size", [("bunny", 3, (203, 117)), ("helmet", 2, (256, 144))])
+def test_bench_n_gpu_check_with_torch_copies(workload, world, size):
+    """bench.py's n_gpu_bitexact check (nrank_check) on the one-GPU lease: the first PARITY_FRAMES
+    recorded frames through the N-rank route (torch copies in place of RCCL), compared by
+    bench.compare_frames with bench.one_gpu_reference's whole-frame render in a fresh context: equal;
+    and one flipped accumulation bit or canvas byte is reported."""
+    import bench
+    W, Hh = size
+    rk = _Ranks(world, W, Hh, lambda e, rt: bench.make_player(e, workload, W, Hh, rt)[0])
+    try:
+        player = rk.ranks[0][1]
+        for i in range(bench.PARITY_FRAMES):
+            acc, can = rk.frame(player.meta["frames"][i])
+    finally:
+        rk.close()
+    ref = bench.one_gpu_reference(workload, W, Hh, 0, range(bench.PARITY_FRAMES))
+    res = bench.compare_frames(can, acc, *ref)
+    assert res["n_gpu_bitexact"] is True, res
+    acc2 = acc.copy()
+    acc2.view(np.uint32)[Hh // 2, W // 3, 0] ^= 1
+    assert bench.compare_frames(can, acc2, *ref)["accumulation_pixels_differing"] == 1
+    can2 = can.copy()
+    can2[Hh - 1, W - 1, 0] ^= 4
+    assert bench.compare_frames(can2, acc, *ref)["n_gpu_bitexact"] is False
