@@ -263,7 +263,7 @@ PT_D bool shadeStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, Hit
     int hitType = h.type;
     s.hitType = hitType;
     if (h.t == kINF) {
-        if (hdri) {   // js/HDRIEnvironmentPathTracing_FragmentShader.js:288-323 (always ends the path)
+        if (hdri) {   // js/HDRIEnvironmentPathTracing_FragmentShader.js:404-438 (always ends the path)
             const f3 env = envColor<COUNT>(a, p.rd, cnt);
             if (bounces == 0) { g.setSharp(1.01f); accum = env; }
             else if (s.diffuseCount == 0 && s.specular) { g.setSharp(1.01f); accum = s.mask * env; }

@@ -34,6 +34,23 @@ static inline float g_smoothstep(float e0, float e1, float x)
     return (t * t) * (3.0f - 2.0f * t);
 }
 
+#ifdef PTO_LIBM
+/* TOLERANCE STUDY ONLY (oracle/Makefile: libptoracle_libm.so, libptoracle_gpu.so; tools/tolerance.py):
+ * another built-in set a GL driver may legally use - the C library's correctly rounded or
+ * near-correctly rounded transcendentals (glibc expf/exp2f/logf/log2f/powf/sinf/cosf/atanf/atan2f/
+ * acosf) instead of the pinned sequences below - to measure how far a render moves when only the
+ * built-ins' rounding changes (the tolerance table). Never used by the parity tests. */
+static inline float g_exp2(float x) { return exp2f(x); }
+static inline float g_log2(float x) { return log2f(x); }
+static inline float g_exp(float x) { return expf(x); }
+static inline float g_log(float x) { return logf(x); }
+static inline float g_pow(float x, float y) { return powf(x, y); }
+static inline float g_sin(float x) { return sinf(x); }
+static inline float g_cos(float x) { return cosf(x); }
+static inline float g_atan(float x) { return atanf(x); }
+static inline float g_atan2(float y, float x) { return atan2f(y, x); }
+static inline float g_acos(float x) { return acosf(x); }
+#else
 /* 2^x: round-to-nearest integer split, degree-7 Taylor of 2^f on |f| <= 0.5, exact ldexp. */
 static inline float g_exp2(float x)
 {
@@ -159,6 +176,8 @@ static inline float g_acos(float x)
     return 2.0f * g_atan(sqrtf((1.0f - x) / (1.0f + x)));
 }
 
+#endif /* PTO_LIBM */
+
 /* ------------------------------------------------------------------ vec3 */
 typedef struct { float x, y, z; } v3;
 static inline v3 V3(float x, float y, float z) { v3 r = { x, y, z }; return r; }
@@ -173,7 +192,21 @@ static inline v3 v_cross(v3 a, v3 b)
     return V3(a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y);
 }
 static inline float v_length(v3 a) { return sqrtf(v_dot(a, a)); }
+#ifdef PTO_APPROX_RSQ
+/* TOLERANCE STUDY ONLY (libptoracle_gpu.so): normalize as a GPU driver compiles it, v * rsq(dot(v, v)),
+ * with the reciprocal square root rounded toward zero (within 1 ulp, as v_rsq_f32; GLSL ES 3.00 allows
+ * 2 ulp for inversesqrt) instead of a correctly rounded 1 / sqrt */
+static inline float g_rsq_approx(float x)
+{
+    const double r = 1.0 / sqrt((double)x);
+    float f = (float)r;
+    if ((double)f > r) f = nextafterf(f, 0.0f);
+    return f;
+}
+static inline v3 v_normalize(v3 a) { return v_muls(a, g_rsq_approx(v_dot(a, a))); }
+#else
 static inline v3 v_normalize(v3 a) { float inv = 1.0f / sqrtf(v_dot(a, a)); return v_muls(a, inv); }
+#endif
 static inline float v_distance(v3 a, v3 b) { return v_length(v_sub(a, b)); }
 static inline v3 v_reflect(v3 I, v3 N) { return v_sub(I, v_muls(N, 2.0f * v_dot(N, I))); }
 static inline v3 v_refract(v3 I, v3 N, float eta)

@@ -60,15 +60,17 @@ class Counters(ctypes.Structure):
         return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
-_lib = None
+_libs = {}
+# the tolerance study's other built-in sets (oracle/Makefile; tools/tolerance.py): "" = the pinned build
+VARIANTS = ("", "fma", "libm", "gpu")
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
+def lib(variant=""):
+    if variant not in _libs:
+        path = LIB_PATH if not variant else os.path.join(HERE, "libptoracle_%s.so" % variant)
+        if not os.path.exists(path):
             subprocess.run(["make", "-s", "-C", HERE], check=True)
-        L = ctypes.CDLL(LIB_PATH)
+        L = ctypes.CDLL(path)
         P = ctypes.POINTER
         L.pto_path_trace.argtypes = [P(Frame), ctypes.c_void_p, ctypes.c_void_p, c_i, c_i, c_i, P(Counters)]
         L.pto_gbuffer.argtypes = [P(Frame), ctypes.c_void_p, c_i, c_i, c_i]
@@ -77,16 +79,18 @@ def lib():
         L.pto_math_probe.argtypes = [c_i, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
         L.pto_sky_color.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
         L.pto_quadric_probe.argtypes = [c_i, c_f, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, c_i]
-        _lib = L
-    return _lib
+        _libs[variant] = L
+    return _libs[variant]
 
 
 class Scene:
     """Keeps the sampler arrays alive and builds Frame structs from recorded uniforms."""
 
-    def __init__(self, scene, width, height, bluenoise, bvh=None, tri=None, hdr=None, maps=None):
+    def __init__(self, scene, width, height, bluenoise, bvh=None, tri=None, hdr=None, maps=None, variant=""):
         """hdr: the tHDRTexture payload as the setup script uploads it (rows top-first, invertY).
-        maps: {"albedo"|"bump"|"metallic"|"emissive": RGBA8 (h, w, 4)} in upload row order."""
+        maps: {"albedo"|"bump"|"metallic"|"emissive": RGBA8 (h, w, 4)} in upload row order.
+        variant: the built-in set (VARIANTS; "" = pinned, the only one the parity tests use)."""
+        self.variant = variant
         self.maps = {k: np.ascontiguousarray(v, dtype=np.uint8) for k, v in (maps or {}).items()}
         self.scene = scene
         self.hdr = None if hdr is None else np.ascontiguousarray(np.asarray(hdr, dtype=np.float32)[::-1])
@@ -133,7 +137,7 @@ class Scene:
         prev = np.ascontiguousarray(prev, dtype=np.float32)
         out = prev.copy()
         cnt = Counters()
-        rc = lib().pto_path_trace(ctypes.byref(f), prev.ctypes.data, out.ctypes.data, row0, row1, nthreads, ctypes.byref(cnt))
+        rc = lib(self.variant).pto_path_trace(ctypes.byref(f), prev.ctypes.data, out.ctypes.data, row0, row1, nthreads, ctypes.byref(cnt))
         if rc != 0:
             raise RuntimeError("pto_path_trace failed: %d" % rc)
         return out, cnt.as_dict()
@@ -142,7 +146,7 @@ class Scene:
         row1 = self.height if row1 is None else row1
         f = self.frame(uniforms)
         g = np.zeros((row1 - row0, self.width, 11), dtype=np.float32)
-        rc = lib().pto_gbuffer(ctypes.byref(f), g.ctypes.data, row0, row1, nthreads)
+        rc = lib(self.variant).pto_gbuffer(ctypes.byref(f), g.ctypes.data, row0, row1, nthreads)
         if rc != 0:
             raise RuntimeError("pto_gbuffer failed: %d" % rc)
         return g
