@@ -145,15 +145,6 @@ struct TraceArgs {
     // the grid carries padding rows for up to split_cap of them
     const unsigned* split;
     unsigned ntiles;       // 16x16 tiles of the draw
-    // late-bounce compaction (pt_trace -> pt_cont): once a wave has at most cont_lanes paths left at a
-    // bounce >= cont_bounce (>= 2: the G-buffer's normal, colour and id are final), those paths leave the
-    // wave as 64-B records (cont_rec) for pt_cont, which runs them packed into full waves; cont_aux[slot]
-    // = the pixel | the 2x2-derivative flag << 31; cont_count[cont_parity] counts this draw's records,
-    // pt_cont clears cont_count[cont_parity ^ 1] for the next draw. NULL cont_rec: no deferral.
-    float4* cont_rec;
-    unsigned* cont_aux;
-    unsigned* cont_count;
-    unsigned cont_parity, cont_bounce, cont_lanes, cont_refill;
     Tex8 albedo, bump, metal, emissive;
     // diagnostics
     unsigned long long* counters;   // C_NUM entries, only with counting builds

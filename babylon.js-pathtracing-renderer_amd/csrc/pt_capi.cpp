@@ -30,7 +30,6 @@
 extern "C" {
 hipError_t pt_launch_exhaustive(int op, unsigned long long* bad, hipStream_t s);
 hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s);
-hipError_t pt_launch_cont(int prog, const pt::TraceArgs* a, int waves, hipStream_t s);
 hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,
                                  unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s);
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
@@ -121,13 +120,6 @@ struct Dev {
     size_t wf_pixels = 0, wf_slots = 0, wf_spill = 0;
     float2* mk_spill = nullptr;   // megakernel BVH stack spill slab
     size_t mk_spill_lanes = 0;
-    // late-bounce compaction of the megakernel's mesh draws (pt_trace -> pt_cont; PT_CONT=0 disables):
-    // path records (64 B), their pixels, the two draw counters; the bounce from which and the lanes at
-    // or below which a wave hands its paths on, the refill batch and pt_cont's one-wave workgroups per CU
-    bool cont = true;
-    void* cont_mem = nullptr;
-    size_t cont_cap = 0;
-    unsigned cont_parity = 0, cont_bounce = 3, cont_lanes = 16, cont_refill = 16, cont_waves_per_cu = 32;
     pt::WfBufs gb = {};           // persistent backend: per-pixel G-buffer + radiance
     void* gb_mem = nullptr;
     size_t gb_pixels = 0;
@@ -430,21 +422,6 @@ int spill_reserve(Dev* c, size_t lanes)
     return PT_OK;
 }
 
-// the late-bounce compaction's buffers for up to `paths` deferred paths: records (64 B), pixels (4 B),
-// then the two draw counters (cleared here once; afterwards pt_cont clears the next draw's)
-int cont_reserve(Dev* c, size_t paths)
-{
-    if (paths <= c->cont_cap) return PT_OK;
-    if (c->cont_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->cont_mem)); c->cont_mem = nullptr; }
-    c->cont_cap = 0;
-    const size_t rec = paths * 64, aux = (paths * 4 + 255) & ~(size_t)255;
-    HIPCHK(c, hipMalloc(&c->cont_mem, rec + aux + 256));
-    HIPCHK(c, hipMemsetAsync((char*)c->cont_mem + rec + aux, 0, 2 * sizeof(unsigned), c->stream));
-    c->cont_cap = paths;
-    c->cont_parity = 0;
-    return PT_OK;
-}
-
 int gb_reserve(Dev* c, int wq, int hq)
 {
     const size_t pixels = (size_t)wq * hq;
@@ -731,26 +708,7 @@ int render_trace(DevFx* fx, DevTex* target)
                 a.split = (a.order && split) ? c->lpt_mem + 5 * c->lpt_cap : nullptr;
             }
             a.ntiles = (unsigned)n;
-            // late-bounce compaction (not in counting draws: their counts are per path either way)
-            const bool cont = c->cont && mesh && !c->counting;
-            if (cont) {
-                if (int rc = cont_reserve(c, (size_t)target->w * target->h)) return rc;
-                const size_t rec = c->cont_cap * 64, aux = (c->cont_cap * 4 + 255) & ~(size_t)255;
-                a.cont_rec = (float4*)c->cont_mem;
-                a.cont_aux = (unsigned*)((char*)c->cont_mem + rec);
-                a.cont_count = (unsigned*)((char*)c->cont_mem + rec + aux);
-                a.cont_parity = c->cont_parity;
-                a.cont_bounce = std::max(2u, c->cont_bounce);   // the G-buffer's normal / colour / id are final from bounce 2
-                a.cont_lanes = c->cont_lanes;
-                a.cont_refill = std::max(1u, std::min(64u, c->cont_refill));
-            }
             HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, c->stream));
-            if (cont) {
-                // pt_cont's waves index the stack slab as pt_trace's first lanes do: no more of them
-                const int waves = (int)std::min<size_t>((size_t)c->cu_count * c->cont_waves_per_cu, (size_t)gx * gy * 4);
-                HIPCHK(c, pt_launch_cont(fx->prog, &a, waves, c->stream));
-                c->cont_parity ^= 1u;
-            }
             if (a.cost) {
                 c->pending_order = { true, (unsigned)n, a.cost, c->lpt_mem + 4 * c->lpt_cap, c->lpt_mem + 5 * c->lpt_cap,
                                      (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance, c->split_near };
@@ -930,11 +888,6 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_BVH_LAYOUT"))   // reference | pairs | trail: the context's initial walk
         c->bvh_layout = !std::strcmp(v, "trail") ? PT_BVH_TRAIL : !std::strcmp(v, "reference") ? PT_BVH_REFERENCE
                                                                                   : PT_BVH_PAIRS;
-    if (const char* v = std::getenv("PT_CONT")) c->cont = std::atoi(v) != 0;
-    if (const char* v = std::getenv("PT_CONT_BOUNCE")) c->cont_bounce = (unsigned)std::max(2, std::min(6, std::atoi(v)));
-    if (const char* v = std::getenv("PT_CONT_LANES")) c->cont_lanes = (unsigned)std::max(0, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("PT_CONT_REFILL")) c->cont_refill = (unsigned)std::max(1, std::min(64, std::atoi(v)));
-    if (const char* v = std::getenv("PT_CONT_WAVES")) c->cont_waves_per_cu = (unsigned)std::max(1, std::min(64, std::atoi(v)));
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
@@ -971,7 +924,6 @@ void dev_ctx_destroy(Dev* c)
     if (c->wf_mem) hipFree(c->wf_mem);
     if (c->lpt_mem) hipFree(c->lpt_mem);
     if (c->mk_spill) hipFree(c->mk_spill);
-    if (c->cont_mem) hipFree(c->cont_mem);
     if (c->gb_mem) hipFree(c->gb_mem);
     if (c->d_err) hipFree(c->d_err);
     if (c->d_counters) hipFree(c->d_counters);

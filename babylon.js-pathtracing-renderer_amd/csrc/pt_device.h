@@ -66,20 +66,20 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, int walk)
 // the reference walk at 4 (it loses above)
 constexpr int kMinWavesTex = 4, kMinWavesPairs = 8, kMinWavesRef = 4;
 template <int P> constexpr int kMinWaves = kHasTex<P> ? kMinWavesTex : kPairs<P> ? kMinWavesPairs : kMinWavesRef;
-// G-buffer fields in LDS (pt_program.h GOutLds): the glTF / HDRI scenes' 8-wave child-pair stack
-// walk keeps 4 of the 8 (colour.yz, id and sharp go after the stack slab's levels) and has two
-// more LDS stack levels in their place (6 -> 7: dragon stand-in +1.8 %, bunny x16 +1.8 %; 7 -> 8:
-// +0.9 %, +1.0 %; 9 levels with 2 fields: no better); the sky + mesh scene lost 2.8 % with the
-// first split and keeps all 8
-constexpr int kGoutLdsGltf = 4, kGoutLdsSky = 8;
+// G-buffer fields in LDS (pt_program.h GOutLds: the normal and colour; the id and sharpness ride in a
+// register): the glTF / HDRI scenes' 8-wave child-pair stack walk keeps none of them there (they are
+// stored once per path to memory and read once) and has two LDS stack levels more in their place
+// (10: dragon stand-in -1.6 %, bunny x16 -1.4 % against 8 levels with 4 fields in LDS; 9 with 2 fields
+// in between; profiles/r04e_envmx_gbuffer_levels.txt); the sky + mesh scene, whose shading writes them
+// more often, keeps all 6 (its 10-level form measured +1 %)
+constexpr int kGoutLdsGltf = 0, kGoutLdsSky = 6;
 template <int P> constexpr bool kPairs8 = kPairs<P> && !kHasTex<P>;
-template <int P> constexpr int kGoutLdsOf = !(kPairs8<P> && !kTrail<P>) ? 8 : kIsGltf<P> ? kGoutLdsGltf
-                                          : kScene<P> == PROG_SKYMESH ? kGoutLdsSky : 8;
-// the G-buffer's field order (GOutLds ORDER): the sky + mesh scene keeps sharp and id in LDS first
-template <int P> constexpr int kGoutOrderOf = kScene<P> == PROG_SKYMESH ? 1 : 0;
-// BVH stack levels in LDS per lane (the rest in the global slab): fewer for the 8-wave variants,
-// one more where two G-buffer fields left LDS
-template <int P> constexpr int kStackLdsOf = kPairs8<P> ? kStackLdsPairs + (8 - kGoutLdsOf<P>) / 2 : kStackLds;
+template <int P> constexpr int kGoutLdsOf = !(kPairs8<P> && !kTrail<P>) ? 6 : kIsGltf<P> ? kGoutLdsGltf
+                                          : kScene<P> == PROG_SKYMESH ? kGoutLdsSky : 6;
+// BVH stack levels in LDS per lane (the rest in the global slab): the 8-wave variants fill 20 floats
+// per lane (160 KB per CU at 32 one-wave workgroups) with the G-buffer's LDS fields and the levels
+// (2 floats each); the 4-wave variants keep 7
+template <int P> constexpr int kStackLdsOf = kPairs8<P> ? (2 * kStackLdsPairs + 8 - kGoutLdsOf<P>) / 2 : kStackLds;
 // the restart-trail walk's LDS ring (entries per lane): the LDS of the stack walk's levels at 8
 // waves/SIMD (6 x 8 B + the 32-B G-buffer = 80 B per lane = 160 KB per CU); at 4 waves/SIMD the
 // textured variants have room for 14
@@ -99,14 +99,15 @@ typedef __attribute__((address_space(1))) vf2 glb_float2;
 struct Path {
     uint32_t s0, s1;       // uvec2 seed (js/PathTracingCommon.js:500)
     // blueNoise_rand()'s state in one register: bits 0-7 / 8-15 = the blue-noise texel's r / g bytes
-    // (randVec4.r / .g: channel = mod(counter, 2) only reaches those two), bits 16-31 = counter + 1
-    // (the GLSL's float counter starts at -1.0 and only ever steps by 1.0)
+    // (randVec4.r / .g: channel = mod(counter, 2) only reaches those two), bits 16-22 = counter + 1
+    // (the GLSL's float counter starts at -1.0 and only ever steps by 1.0, at most twice per bounce);
+    // bits 23-31 carry pt_trace's packed G-buffer fields (pt_program.h GOutLds)
     uint32_t bn;
     f3 ro, rd;             // rayOrigin, rayDirection
 };
 PT_D float unorm8(unsigned b);
-PT_D float pathCounter(const Path& p) { return (float)(p.bn >> 16) - 1.0f; }
-PT_D void setPathCounter(Path& p, float c) { p.bn = (p.bn & 0xffffu) | ((unsigned)(c + 1.0f) << 16); }
+PT_D float pathCounter(const Path& p) { return (float)((p.bn >> 16) & 0x7fu) - 1.0f; }
+PT_D void setPathCounter(Path& p, float c) { p.bn = (p.bn & 0xff80ffffu) | ((unsigned)(c + 1.0f) << 16); }
 
 PT_D float rng(Path& p)
 {

@@ -48,8 +48,9 @@ struct Cnt {
 #endif
 
 // CalculateRadiance's `out` parameters objectNormal / objectColor / objectID / pixelSharpness:
-// in registers (GOut) or, for the megakernel, in LDS [field][lane] (GOutLds), which takes eight
-// live values out of the VGPR budget of the bounce loop
+// in registers (GOut) or, for the megakernel, packed (GOutLds): the normal and colour in LDS
+// [field][lane], which takes six live values out of the VGPR budget of the bounce loop, and the id and
+// sharpness as bits of the path's blue-noise register (free bits of a value that is live anyway)
 struct GOut {
     f3 nrm, col;
     float id, sharp;
@@ -61,33 +62,61 @@ struct GOut {
 };
 typedef __attribute__((address_space(3))) float lds_float;
 typedef __attribute__((address_space(1))) float glb_float;
-// LS = lanes of the workgroup = the stride of one field; NF = fields kept in LDS, the rest (from
-// the last: sharp, id, colour, normal) in the lane's 8 - NF floats at `gx` (after the stack slab's
-// levels): where LDS caps residency that leaves room for more stack levels (kGoutLdsOf, pt_device.h)
-template <int LS, int NF = 8, int ORDER = 0>
+// The packed G-buffer of pt_trace. Path::bn bits 24-25 hold the sharpness (0: 0.0, 1: 1.01, 2: -1.0:
+// the only values the GLSL assigns), bits 26-30 objectID (an object index < 32: hitObjectID of the
+// spheres / quadric shapes, the quads, the mesh), bit 23 "objectNormal's fields beyond LDS were
+// written", bit 31 the same for objectColor; the blue-noise counter keeps bits 16-22 (at most 13
+// draws per path). LS = lanes of the workgroup = the stride of one field; NF = the normal / colour
+// fields in LDS (from the normal's x), the rest in the lane's 6 - NF floats at `gx` (after the stack
+// slab's levels): stored only by setNrm / setCol and read only when their bit says so - no clearing
+// store, no id / sharpness traffic at all.
+template <int LS, int NF = 6>
 struct GOutLds {
     lds_float* p;
     unsigned slot;
-    glb_float* gx = nullptr;
-    // ORDER 0: normal, colour, id, sharp; ORDER 1 (the sky + mesh scene, whose shading sets the
-    // sharpness often): sharp, id, normal, colour - the last 8 - NF of the order leave LDS
-    static constexpr int phys(int f) { return ORDER == 0 ? f : f == 7 ? 0 : f == 6 ? 1 : f + 2; }
+    glb_float* gx;
+    uint32_t* bn;
     PT_D void put(int f, float v)
     {
-        const int q = phys(f);
-        if (q < NF) p[q * LS + slot] = v;
-        else gx[q - NF] = v;
+        if (f < NF) p[f * LS + slot] = v;
+        else gx[f - NF] = v;
     }
-    PT_D float get(int f) const { const int q = phys(f); return q < NF ? p[q * LS + slot] : gx[q - NF]; }
-    PT_D void clear() { for (int f = 0; f < 8; f++) put(f, 0.0f); }
-    PT_D void setNrm(f3 v) { put(0, v.x); put(1, v.y); put(2, v.z); }
-    PT_D void setCol(f3 v) { put(3, v.x); put(4, v.y); put(5, v.z); }
-    PT_D void setId(float v) { put(6, v); }
-    PT_D void setSharp(float v) { put(7, v); }
+    PT_D float get(int f) const
+    {
+        if (f < NF) return p[f * LS + slot];
+        return ((*bn >> (f < 3 ? 23 : 31)) & 1u) ? gx[f - NF] : 0.0f;
+    }
+    PT_D void clear()
+    {
+        for (int f = 0; f < NF; f++) p[f * LS + slot] = 0.0f;
+        *bn &= 0x007fffffu;
+    }
+    PT_D void setNrm(f3 v)
+    {
+        put(0, v.x); put(1, v.y); put(2, v.z);
+        if (NF < 3) *bn |= 1u << 23;
+    }
+    PT_D void setCol(f3 v)
+    {
+        put(3, v.x); put(4, v.y); put(5, v.z);
+        if (NF < 6) *bn |= 1u << 31;
+    }
+    PT_D void setId(float v) { *bn = (*bn & ~(31u << 26)) | (((unsigned)(int)v & 31u) << 26); }
+    PT_D void setSharp(float v)
+    {
+        const unsigned code = v == 1.01f ? 1u : v == -1.0f ? 2u : 0u;
+        *bn = (*bn & ~(3u << 24)) | (code << 24);
+    }
+    PT_D float sharp() const
+    {
+        const unsigned code = (*bn >> 24) & 3u;
+        return code == 1u ? 1.01f : code == 2u ? -1.0f : 0.0f;
+    }
+    PT_D float id() const { return (float)((*bn >> 26) & 31u); }
     PT_D GOut load() const
     {
         GOut g;
-        g.nrm = mk(get(0), get(1), get(2)); g.col = mk(get(3), get(4), get(5)); g.id = get(6); g.sharp = get(7);
+        g.nrm = mk(get(0), get(1), get(2)); g.col = mk(get(3), get(4), get(5)); g.id = id(); g.sharp = sharp();
         return g;
     }
 };

@@ -164,74 +164,14 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, fl
     return shadeStep<PROG, COUNT, G>(a, p, s, g, accum, h, cnt);
 }
 
-// ------------------------------------------------------------------------------ late-bounce compaction
-// A path's state between two bounces as a 64-B record (pt_cont): ray, throughput, rng / blue-noise
-// state, the bounce counters and flags, and the G-buffer sharpness (the other G-buffer fields are final
-// from bounce 2 on: the GLSL writes them at bounces 0 and 1 only)
-PT_D void contStore(const TraceArgs& a, unsigned slot, const Path& p, const PState& s, float sharp)
-{
-    const unsigned bits = ((unsigned)s.diffuseCount & 0xffu) | (((unsigned)s.hitType & 0xffu) << 8) |
-                          (((unsigned)s.bounce & 0xffu) << 16) | (s.coat ? 1u << 24 : 0u) |
-                          (s.specular ? 1u << 25 : 0u) | (s.sampleLight ? 1u << 26 : 0u);
-    float4* r = a.cont_rec + 4ull * slot;
-    r[0] = make_float4(p.ro.x, p.ro.y, p.ro.z, p.rd.x);
-    r[1] = make_float4(p.rd.y, p.rd.z, s.mask.x, s.mask.y);
-    r[2] = make_float4(s.mask.z, s.roughness, __uint_as_float(p.s0), __uint_as_float(p.s1));
-    r[3] = make_float4(__uint_as_float(p.bn), __uint_as_float(bits), sharp, 0.0f);
-}
-PT_D void contLoad(const TraceArgs& a, unsigned slot, Path& p, PState& s, float& sharp)
-{
-    const float4* r = a.cont_rec + 4ull * slot;
-    const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
-    p.ro = mk(r0.x, r0.y, r0.z); p.rd = mk(r0.w, r1.x, r1.y);
-    s.mask = mk(r1.z, r1.w, r2.x); s.roughness = r2.y;
-    p.s0 = __float_as_uint(r2.z); p.s1 = __float_as_uint(r2.w); p.bn = __float_as_uint(r3.x);
-    const unsigned bits = __float_as_uint(r3.y);
-    s.diffuseCount = (int)(bits & 0xffu);
-    s.hitType = (int)(signed char)((bits >> 8) & 0xffu);
-    s.bounce = (int)((bits >> 16) & 0xffu);
-    s.coat = (bits >> 24) & 1u; s.specular = (bits >> 25) & 1u; s.sampleLight = (bits >> 26) & 1u;
-    sharp = r3.z;
-}
-// the G-buffer of a continued path: only the sharpness can still change (pt_cont)
-struct GSharp {
-    float sharp;
-    PT_D void clear() {}
-    PT_D void setNrm(f3) {}
-    PT_D void setCol(f3) {}
-    PT_D void setId(float) {}
-    PT_D void setSharp(float v) { sharp = v; }
-};
-
-// CalculateRadiance's loop. Megakernel draws with late-bounce compaction (a.cont_rec): after a bounce
-// >= cont_bounce, when at most cont_lanes of the wave's lanes are still looping, they leave the loop
-// together (the count is a ballot: wave-uniform) and store their paths for pt_cont; `slot` is then the
-// record's index (-1: the path ended here, or a helper lane outside the target, whose path no pixel
-// needs - the 2x2 derivatives only read its G-buffer, final by then). The queue slots are handed out
-// by one atomic per wave and a lane prefix (mbcnt) over the ballot of the storing lanes.
 template <int PROG, bool COUNT, int LS, class G>
-PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_slot, unsigned deep, Cnt& cnt,
-                 bool inside, int& slot)
+PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_slot, unsigned deep, Cnt& cnt)
 {
     PState s;
     pathBegin(s, g);
     f3 accum = mk(0, 0, 0);
 #pragma unroll 1
-    while (bounceStep<PROG, COUNT, LS, G>(a, p, s, g, accum, lds, lane_slot, deep, cnt)) {
-        if (!COUNT && kHasMesh<PROG> && a.cont_rec && (unsigned)s.bounce >= a.cont_bounce &&
-            (unsigned)__popcll(__ballot(1)) <= a.cont_lanes) {
-            const unsigned long long st = __ballot(inside);
-            const int lead = __ffsll((long long)__ballot(1)) - 1;
-            unsigned base = 0;
-            if (__lane_id() == lead && st) base = atomicAdd(&a.cont_count[a.cont_parity], (unsigned)__popcll(st));
-            base = __shfl(base, lead, 64);
-            if (inside) {
-                slot = (int)(base + (unsigned)__popcll(st & ((1ull << __lane_id()) - 1ull)));
-                contStore(a, (unsigned)slot, p, s, g.get(7));
-            }
-            break;
-        }
-    }
+    while (bounceStep<PROG, COUNT, LS, G>(a, p, s, g, accum, lds, lane_slot, deep, cnt)) {}
     return max3s(accum, 0.0f);
 }
 
@@ -332,8 +272,10 @@ PT_D bool tracePlace(const TraceArgs& a, int lane, TracePlace& pl)
 template <int PROG, bool COUNT>
 __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
 {
-    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];   // stack levels (+ the scratch level, kScratchOf), or the trail walk's ring
-    __shared__ float lds_gout[kGoutLdsOf<PROG> * kTraceBlock];
+    // one LDS array: the stack levels (+ the scratch level, kScratchOf) or the trail walk's ring, then
+    // the G-buffer's LDS fields (none in some variants: no zero-length array)
+    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock + (kGoutLdsOf<PROG> * kTraceBlock + 1) / 2];
+    float* const lds_gout = (float*)(lds_stack + kWalkSlotsOf<PROG> * kTraceBlock);
     const unsigned tid = threadIdx.x;
     const int lane = tid & 63;
     const unsigned long long t_start = clock64();
@@ -359,20 +301,20 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     cnt.sget = cnt.sget_slab = cnt.sput = cnt.sput_slab = 0;
     cnt.bounce = 0;
 #endif
-    // G-buffer fields beyond the LDS ones: 8 - kGoutLdsOf floats per lane after the slab's stack
+    // G-buffer fields beyond the LDS ones: 6 - kGoutLdsOf floats per lane after the slab's stack
     // levels, [lane][field] (pt_capi.cpp spill_reserve)
-    glb_float* const gx = kGoutLdsOf<PROG> < 8
-        ? (glb_float*)(a.spill + (size_t)(kStackLevels - kStackLdsMin) * a.spill_stride) + (size_t)deep * (8 - kGoutLdsOf<PROG>)
+    glb_float* const gx = kGoutLdsOf<PROG> < 6
+        ? (glb_float*)(a.spill + (size_t)(kStackLevels - kStackLdsMin) * a.spill_stride) + (size_t)deep * (6 - kGoutLdsOf<PROG>)
         : nullptr;
-    GOutLds<kTraceBlock, kGoutLdsOf<PROG>, kGoutOrderOf<PROG>> gl{ (lds_float*)lds_gout, tid, gx };
+    Path p;
+    p.bn = 0u;
+    GOutLds<kTraceBlock, kGoutLdsOf<PROG>> gl{ (lds_float*)lds_gout, tid, gx, &p.bn };
     gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
     f3 r = mk(0, 0, 0);
-    int slot = -1;   // late-bounce compaction: this lane's path record for pt_cont
     if (active) {
-        Path p;
         cameraRay(a, px, py, p);
         PT_SEC(cnt, 0);
-        r = radiance<PROG, COUNT, kTraceBlock>(a, p, gl, lds_stack, tid, deep, cnt, px < a.width && py < a.height, slot);
+        r = radiance<PROG, COUNT, kTraceBlock>(a, p, gl, lds_stack, tid, deep, cnt);
     }
     PT_SEC(cnt, 4);
     const GOut g = gl.load();
@@ -432,64 +374,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     }
     if (!active || px >= a.width || py >= a.height) return;   // quad helper outside the target, idle lane
     const bool edge = colorDiff >= 1.0f || normalDiff >= 1.0f || objectDiff >= 1.0f;
-    const long long pi = (long long)py * a.width + px;
-    if (slot >= 0) {   // the path continues in pt_cont, which accumulates the pixel
-        a.cont_aux[slot] = (unsigned)pi | (edge ? 0x80000000u : 0u);
-        return;
-    }
-    accumulate(a, pi, r, g.sharp, edge);
-}
-
-// Late-bounce compaction, the second half: the paths pt_trace stored (cont_count[cont_parity] of
-// them) run their remaining bounces packed into full waves. Each one-wave workgroup owns an equal
-// share of the records and refills its finished lanes from it (at least cont_refill of them at a
-// time, or all when none is left): a lane's path is one of the reference's per-pixel paths, resumed
-// with exactly its state, so every pixel's bits are those of the uncompacted kernel.
-template <int PROG>
-__global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_cont(TraceArgs a)
-{
-    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];
-    const unsigned lane = threadIdx.x;
-    if (blockIdx.x == 0 && lane == 0) a.cont_count[a.cont_parity ^ 1u] = 0u;   // the next draw's counter
-    const unsigned n = a.cont_count[a.cont_parity];
-    const unsigned per = (n + gridDim.x - 1) / gridDim.x;
-    unsigned next = blockIdx.x * per;
-    const unsigned end = min(next + per, n);
-    if (next >= end) return;
-    const unsigned deep = blockIdx.x * kTraceBlock + lane;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
-    Path p;
-    PState s;
-    GSharp g;
-    f3 accum = mk(0, 0, 0);
-    unsigned slot = 0;
-    bool alive = false;
-    for (;;) {
-        const unsigned long long dead = __ballot(!alive);
-        const unsigned ndead = (unsigned)__popcll(dead);
-        if (next < end && (ndead >= a.cont_refill || ndead == 64u)) {
-            if (!alive) {
-                const unsigned q = next + (unsigned)__popcll(dead & below);
-                if (q < end) {
-                    slot = q;
-                    contLoad(a, q, p, s, g.sharp);
-                    accum = mk(0, 0, 0);
-                    alive = true;
-                }
-            }
-            next += ndead;
-        }
-        if (__ballot(alive) == 0ull) {
-            if (next >= end) break;
-            continue;
-        }
-        if (alive && !bounceStep<PROG, false, kTraceBlock>(a, p, s, g, accum, lds_stack, lane, deep, cnt)) {
-            const unsigned aux = a.cont_aux[slot];
-            accumulate(a, (long long)(aux & 0x7fffffffu), max3s(accum, 0.0f), g.sharp, (aux >> 31) != 0u);
-            alive = false;
-        }
-    }
+    accumulate(a, (long long)py * a.width + px, r, g.sharp, edge);
 }
 
 // ------------------------------------------------------------------------------ persistent paths

@@ -33,25 +33,6 @@ hipError_t PT_CAT(pt_launch_trace_, PT_WALK_NAME)(int prog, int count, const pt:
     return hipGetLastError();
 }
 
-// late-bounce compaction's second kernel (mesh programs only)
-hipError_t PT_CAT(pt_launch_cont_, PT_WALK_NAME)(int prog, const pt::TraceArgs* a, dim3 grid, hipStream_t s)
-{
-    using namespace pt;
-#define PT_CASE(P)                                                                                  \
-    case P:                                                                                          \
-        if constexpr (kHasMesh<P>) {                                                                 \
-            hipLaunchKernelGGL((pt::pt_cont<P>), grid, dim3(kTraceBlock), 0, s, *a);                 \
-            break;                                                                                   \
-        } else                                                                                       \
-            return hipErrorInvalidValue;
-    switch (prog) {
-        PT_WALK_PROGS(PT_CASE)
-    default: return hipErrorInvalidValue;
-    }
-#undef PT_CASE
-    return hipGetLastError();
-}
-
 hipError_t PT_CAT(pt_launch_persist_, PT_WALK_NAME)(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w,
                                                     int tiles_x, unsigned n_wave_tiles, unsigned per_wave,
                                                     unsigned refill, dim3 grid, dim3 block, hipStream_t s)
