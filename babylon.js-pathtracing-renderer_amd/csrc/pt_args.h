@@ -105,7 +105,6 @@ struct OutputArgs {
     unsigned* ob_split;
     unsigned ob_ntiles, ob_cap, ob_dominance;
     int ob_near;
-    unsigned ob_geom;       // tiles per row | XCD region block << 16 (pt_order_build; 0 block: none)
 };
 
 // Per-draw kernel arguments. Wave-uniform: read with scalar loads from the kernarg segment; the

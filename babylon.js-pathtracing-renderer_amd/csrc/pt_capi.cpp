@@ -31,7 +31,7 @@ extern "C" {
 hipError_t pt_launch_exhaustive(int op, unsigned long long* bad, hipStream_t s);
 hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,
-                                 unsigned split_cap, unsigned dominance, int near_buckets, unsigned geom, hipStream_t s);
+                                 unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s);
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
@@ -151,10 +151,8 @@ struct Dev {
     // the order build of the last megakernel draw, deferred to run as an extra block of the next
     // screenOutput pass (pt_output) instead of a kernel of its own; any other draw, stream switch or
     // query launches it alone first (flush_order). PT_FUSE_ORDER=0: always alone, after the draw.
-    struct { bool on; unsigned n; const unsigned* cost; unsigned* order; unsigned* split; unsigned cap, dominance; int near;
-             unsigned geom; }
+    struct { bool on; unsigned n; const unsigned* cost; unsigned* order; unsigned* split; unsigned cap, dominance; int near; }
         pending_order = {};
-    unsigned xcd_block = 0;   // XCD regions of the longest-first order: blocks of this many tiles square (PT_XCD_BLOCK)
     bool fuse_order = true;
     unsigned* lpt_mem = nullptr;            // cost[4 * ntiles] | order[ntiles]
     size_t lpt_n = 0, lpt_cap = 0;
@@ -578,7 +576,7 @@ int flush_order(Dev* c)
     if (!c->pending_order.on) return PT_OK;
     c->pending_order.on = false;
     const auto& po = c->pending_order;
-    HIPCHK(c, pt_launch_order_build(po.n, po.cost, po.order, po.split, po.cap, po.dominance, po.near, po.geom, c->stream));
+    HIPCHK(c, pt_launch_order_build(po.n, po.cost, po.order, po.split, po.cap, po.dominance, po.near, c->stream));
     return PT_OK;
 }
 
@@ -768,8 +766,7 @@ int render_trace(DevFx* fx, DevTex* target)
             c->snap_tex = snap ? target : nullptr;
             if (a.cost) {
                 c->pending_order = { true, (unsigned)n, a.cost, c->lpt_mem + 4 * c->lpt_cap, c->lpt_mem + 5 * c->lpt_cap,
-                                     (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance, c->split_near,
-                                     (unsigned)gx | (c->xcd_block << 16) };
+                                     (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance, c->split_near };
                 if (!c->fuse_order) { if (int rc = flush_order(c)) return rc; }
                 c->lpt_valid = true; c->lpt_n = n; c->lpt_key_target = target; c->lpt_key_prog = fx->prog;
                 c->lpt_key_part = c->part; c->lpt_key_parts = c->num_parts;
@@ -880,7 +877,7 @@ int launch_output(Dev* c, pt::OutputArgs a, int prog)
         if (c->pending_order.on) {   // the last megakernel draw's order build rides along as one more block
             const auto& po = c->pending_order;
             a.ob_cost = po.cost; a.ob_order = po.order; a.ob_split = po.split;
-            a.ob_ntiles = po.n; a.ob_cap = po.cap; a.ob_dominance = po.dominance; a.ob_near = po.near; a.ob_geom = po.geom;
+            a.ob_ntiles = po.n; a.ob_cap = po.cap; a.ob_dominance = po.dominance; a.ob_near = po.near;
             c->pending_order.on = false;
         }
         HIPCHK(c, pt_launch_output(&a, c->stream));
@@ -975,7 +972,6 @@ Dev* dev_ctx_create(int device, int* err)
         c->bvh_layout = !std::strcmp(v, "trail") ? PT_BVH_TRAIL : !std::strcmp(v, "reference") ? PT_BVH_REFERENCE
                                                                                   : PT_BVH_PAIRS;
     if (const char* v = std::getenv("PT_RIDE")) c->ride = std::atoi(v) != 0;
-    if (const char* v = std::getenv("PT_XCD_BLOCK")) c->xcd_block = (unsigned)std::min(255, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("PT_WALK_PREFETCH")) c->walk_prefetch = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_WALK_PRIO")) c->walk_prio = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_WALK_SCALAR")) c->walk_scalar = std::atoi(v) != 0;

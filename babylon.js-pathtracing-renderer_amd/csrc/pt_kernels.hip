@@ -50,24 +50,14 @@ PT_D int costBucket(unsigned dur)
 // bucket by bucket, slowest bucket first; within a bucket the order is whatever the LDS atomics
 // give - any permutation renders the same bits, only the schedule changes.
 // (one block of 1024 threads as its own kernel, or of 256 as the extra block of pt_output)
-// XCD regions (geom >> 16 = B > 0, PT_XCD_BLOCK): the tiles fall into 8 regions of BxB-tile blocks
-// (block (bx, by) -> region (bx + 3 by) mod 8, compact and cost-balanced); workgroup slots 8 apart go
-// to one XCD (one L2), so when no tile is split the slots s = r mod 8 take region r's tiles longest
-// first: each L2 then holds the BVH records of one eighth of the frame's rays (the regions' common
-// count, then whatever is left, in any order).
 PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split, unsigned split_cap,
-                     unsigned dominance, int near_buckets, unsigned geom)
+                     unsigned dominance, int near_buckets)
 {
     __shared__ unsigned cnt[kCostBuckets];
-    __shared__ unsigned rcnt[8 * kCostBuckets];
     __shared__ unsigned long long total;
-    __shared__ unsigned slowest, rmin, rover, regions;
-    const unsigned tiles_x = geom & 0xffffu, xb = geom >> 16;
-    auto regionOf = [&](unsigned t) { return ((t % tiles_x) / xb + 3u * ((t / tiles_x) / xb)) & 7u; };
+    __shared__ unsigned slowest;
     for (int b = threadIdx.x; b < kCostBuckets; b += blockDim.x) cnt[b] = 0;
-    if (xb)
-        for (int b = threadIdx.x; b < 8 * kCostBuckets; b += blockDim.x) rcnt[b] = 0;
-    if (threadIdx.x == 0) { total = 0; slowest = 0; rover = 0; regions = 0; }
+    if (threadIdx.x == 0) { total = 0; slowest = 0; }
     __syncthreads();
     auto tileCost = [&](unsigned t) {
         const unsigned* c = cost + 4u * t;
@@ -102,16 +92,12 @@ PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, uns
                 bk[k >> 2] = (k & 3) ? (bk[k >> 2] | (b << (8 * (k & 3)))) : b;
                 part += (unsigned long long)v[j].x + v[j].y + v[j].z + v[j].w;
                 mx = max(mx, m);
-                if (t < ntiles) {
-                    atomicAdd(&cnt[b], 1u);
-                    if (xb) atomicAdd(&rcnt[regionOf(t) * kCostBuckets + b], 1u);
-                }
+                if (t < ntiles) atomicAdd(&cnt[b], 1u);
             }
         }
     } else {
         for (unsigned t = threadIdx.x; t < ntiles; t += blockDim.x) {
             atomicAdd(&cnt[tileBucket(t)], 1u);
-            if (xb) atomicAdd(&rcnt[regionOf(t) * kCostBuckets + tileBucket(t)], 1u);
             const unsigned* c = cost + 4u * t;
             part += (unsigned long long)c[0] + c[1] + c[2] + c[3];
             mx = max(mx, tileCost(t));
@@ -148,57 +134,34 @@ PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, uns
             const unsigned k = (near + 7u) & ~7u;   // split_cap: a multiple of 8, <= ntiles
             const bool dominated = (unsigned long long)slowest * 4ull * ntiles >= dominance * total && total > 0;
             *split = dominated ? min(k, split_cap) : 0u;
-            regions = (xb && !(dominated && k && split_cap)) ? 1u : 0u;
         }
         const unsigned excl = suf - c0 - c1;   // tiles in buckets above 2l + 1
         cnt[2 * l + 1] = excl;
         cnt[2 * l] = excl + c1;
-        if (xb) {   // the same exclusive positions within each region, and the regions' common count
-            unsigned m = 0xffffffffu;
-            for (int r = 0; r < 8; r++) {
-                unsigned* rc = rcnt + r * kCostBuckets;
-                const unsigned d0 = rc[2 * l], d1 = rc[2 * l + 1];
-                unsigned s = d0 + d1;
-                for (int o = 1; o < 64; o <<= 1) {
-                    const unsigned t = (unsigned)__shfl_down((int)s, o, 64);
-                    if (l + o < 64) s += t;
-                }
-                m = min(m, (unsigned)__shfl((int)s, 0, 64));
-                const unsigned ex = s - d0 - d1;
-                rc[2 * l + 1] = ex;
-                rc[2 * l] = ex + d1;
-            }
-            if (l == 0) rmin = m;
-        }
     }
     __syncthreads();
-    // a tile's slot: by bucket over the frame, or (regions) by bucket within its region, 8 apart
-    auto place = [&](unsigned t, unsigned b) {
-        unsigned pos;
-        if (regions) {
-            const unsigned r = regionOf(t);
-            const unsigned q = atomicAdd(&rcnt[r * kCostBuckets + b], 1u);
-            pos = q < rmin ? 8u * q + r : 8u * rmin + atomicAdd(&rover, 1u);
-        } else
-            pos = atomicAdd(&cnt[b], 1u);
-        if (pos < ntiles) order[pos] = t;
-    };
     if (held) {
 #pragma unroll
         for (int j = 0; j < (int)kOrderHeld; j++) {
             const unsigned t = threadIdx.x + j * blockDim.x;
-            if (t < ntiles) place(t, (bk[j >> 2] >> (8 * (j & 3))) & 255u);
+            if (t < ntiles) {
+                const unsigned pos = atomicAdd(&cnt[(bk[j >> 2] >> (8 * (j & 3))) & 255u], 1u);
+                if (pos < ntiles) order[pos] = t;
+            }
         }
         return;
     }
-    for (unsigned t = threadIdx.x; t < ntiles; t += blockDim.x) place(t, (unsigned)tileBucket(t));
+    for (unsigned t = threadIdx.x; t < ntiles; t += blockDim.x) {
+        const unsigned pos = atomicAdd(&cnt[tileBucket(t)], 1u);
+        if (pos < ntiles) order[pos] = t;
+    }
 }
 
 __global__ __launch_bounds__(1024) void pt_order_build(unsigned ntiles, const unsigned* cost, unsigned* order,
                                                         unsigned* split, unsigned split_cap, unsigned dominance,
-                                                        int near_buckets, unsigned geom)
+                                                        int near_buckets)
 {
-    orderBuild(ntiles, cost, order, split, split_cap, dominance, near_buckets, geom);
+    orderBuild(ntiles, cost, order, split, split_cap, dominance, near_buckets);
 }
 // ------------------------------------------------------------------------------ screenCopy
 __global__ __launch_bounds__(256) void pt_copy(CopyArgs a)
@@ -238,7 +201,7 @@ __global__ __launch_bounds__(256) void pt_output(OutputArgs a, int tiles_x, int 
     int bid = (int)blockIdx.x, nblk = (int)gridDim.x;
     if (a.ob_cost) {   // block 0: the next megakernel draw's order (pt_order_build), beside the tiles
         if (bid == 0) {
-            orderBuild(a.ob_ntiles, a.ob_cost, a.ob_order, a.ob_split, a.ob_cap, a.ob_dominance, a.ob_near, a.ob_geom);
+            orderBuild(a.ob_ntiles, a.ob_cost, a.ob_order, a.ob_split, a.ob_cap, a.ob_dominance, a.ob_near);
             return;
         }
         bid--; nblk--;
@@ -509,10 +472,10 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
 }
 
 hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,
-                                 unsigned split_cap, unsigned dominance, int near_buckets, unsigned geom, hipStream_t s)
+                                 unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s)
 {
     hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(1024), 0, s, ntiles, cost, order, split, split_cap, dominance,
-                       near_buckets, geom);
+                       near_buckets);
     return hipGetLastError();
 }
 
@@ -578,7 +541,7 @@ hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s)
     if (grid.y == 0) {   // no band of this part: a fused order build runs on its own
         if (a->ob_cost)
             hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(1024), 0, s, a->ob_ntiles, a->ob_cost, a->ob_order,
-                               a->ob_split, a->ob_cap, a->ob_dominance, a->ob_near, a->ob_geom);
+                               a->ob_split, a->ob_cap, a->ob_dominance, a->ob_near);
         return hipGetLastError();
     }
     // persistent screenOutput blocks: about four 16x16 tiles each, 4096..8192 (1080p 4096: 37.2 ->
