@@ -155,7 +155,6 @@ struct TraceArgs {
     int bvh_walk;              // WALK_REF / _PAIRS / _TRAIL (pt_device.h): the variant the draw takes
     int walk_prefetch;         // child-pair walk: prefetch each pushed far child's record line (PT_WALK_PREFETCH)
     int walk_prio;             // the child-pair walk at wave priority 1 (PT_WALK_PRIO)
-    int walk_scalar;           // child-pair walk: a record every active lane loads through the scalar cache (PT_WALK_SCALAR)
     float2* spill;             // megakernel BVH stack levels >= kStackLds: [level][grid lane]
     unsigned spill_stride;
     // longest-first dispatch (megakernel): order[slot] = the 16x16 tile dealt to tile slot `slot`

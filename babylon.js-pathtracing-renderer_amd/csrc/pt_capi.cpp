@@ -127,7 +127,6 @@ struct Dev {
     int bvh_layout = PT_BVH_PAIRS;
     int walk_prefetch = 0;   // PT_WALK_PREFETCH
     int walk_prio = 0;       // PT_WALK_PRIO
-    int walk_scalar = 0;     // PT_WALK_SCALAR
     int bvh_used = -1;
     int cu_count = 256;
     pt::WfBufs wf = {};
@@ -646,7 +645,6 @@ int render_trace(DevFx* fx, DevTex* target)
         a.bvh_walk = a.bvh_top_base ? pt::WALK_TRAIL : a.bvh_pairs ? pt::WALK_PAIRS : pt::WALK_REF;
         a.walk_prefetch = c->walk_prefetch;
         a.walk_prio = c->walk_prio;
-        a.walk_scalar = c->walk_scalar;
         c->bvh_used = a.bvh_top_base ? PT_BVH_TRAIL : a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
         a.albedo = tex8(sampler(fx, "tAlbedoTexture"));
         a.bump = tex8(sampler(fx, "tBumpTexture"));
@@ -974,7 +972,6 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_RIDE")) c->ride = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_WALK_PREFETCH")) c->walk_prefetch = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_WALK_PRIO")) c->walk_prio = std::atoi(v) != 0;
-    if (const char* v = std::getenv("PT_WALK_SCALAR")) c->walk_scalar = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);

@@ -528,8 +528,6 @@ PT_D PairBufs pairBufs(const TraceArgs& a)
 }
 typedef unsigned int vu4 __attribute__((ext_vector_type(4)));
 typedef unsigned int vu2 __attribute__((ext_vector_type(2)));
-typedef unsigned int vu8 __attribute__((ext_vector_type(8)));
-#define PT_CONST_AS __attribute__((address_space(4)))
 PT_D float4 ldRec4(__amdgpu_buffer_rsrc_t r, uint32_t off)
 {
     const vu4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
@@ -563,8 +561,6 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     int pop = curT < hitT ? 0 : 1;
     float tID = -1.0f, tU = 0.0f, tV = 0.0f;
     const bool prefetch = a.walk_prefetch != 0;   // wave-uniform (kernel argument)
-    const bool scalar = a.walk_scalar != 0;
-    const PT_CONST_AS char* sbase = (const PT_CONST_AS char*)a.bvh_pairs;
     uint32_t pfv = 0u;
     for (;;) {
         asm volatile("" : "+v"(pop));
@@ -579,27 +575,8 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
         secWalkStep(r, live, code & ~kLeafBit);
         if (!live) continue;
         const uint32_t off = code & ~kLeafBit;
-        float4 r0, r1, r2;
-        float2 r3;
-        // PT_WALK_SCALAR: when every active lane is at one record (the wave-uniform case: a ballot), one
-        // scalar-cache read of it instead of four vector loads (no per-lane addresses, its own counter);
-        // a leaf's 48 B only, so that the read stays inside the array
-        if (scalar && __builtin_amdgcn_ballot_w64(off == __builtin_amdgcn_readfirstlane(off)) == __builtin_amdgcn_read_exec()) {
-            const uint32_t so = __builtin_amdgcn_readfirstlane(off);
-            const vu8 v = *(const PT_CONST_AS vu8*)(sbase + so);
-            const vu4 w = *(const PT_CONST_AS vu4*)(sbase + so + 32u);
-            r0 = make_float4(__uint_as_float(v.s0), __uint_as_float(v.s1), __uint_as_float(v.s2), __uint_as_float(v.s3));
-            r1 = make_float4(__uint_as_float(v.s4), __uint_as_float(v.s5), __uint_as_float(v.s6), __uint_as_float(v.s7));
-            r2 = make_float4(__uint_as_float(w.x), __uint_as_float(w.y), __uint_as_float(w.z), __uint_as_float(w.w));
-            r3 = make_float2(0.0f, 0.0f);
-            if (!(__builtin_amdgcn_readfirstlane(code) & kLeafBit)) {
-                const vu2 c = *(const PT_CONST_AS vu2*)(sbase + so + 48u);
-                r3 = make_float2(__uint_as_float(c.x), __uint_as_float(c.y));
-            }
-        } else {
-            r0 = ldRec4(b.rec, off); r1 = ldRec4(b.rec, off + 16u); r2 = ldRec4(b.rec, off + 32u);
-            r3 = ldRec2(b.rec, off + 48u);
-        }
+        const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
+        const float2 r3 = ldRec2(b.rec, off + 48u);
         if (!(code & kLeafBit)) {
             r.nodes += 2;
             float tA, tB;

@@ -1,9 +1,9 @@
 #!/bin/bash
 # screenOutput riding: its parity tests, then whole-frame A/B (PT_RIDE=0/1, bench.py), the walk knobs
-# (kernel time)
+# (kernel time), and the evidence session of the tree
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "rides or deferred" --timeout 120 --timeout-method thread > gpurun_out/r04h_pytest_ride.log 2>&1 || exit $?
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "rides or deferred or stream" --timeout 120 --timeout-method thread > gpurun_out/r04h_pytest_ride.log 2>&1 || exit $?
 OUT=gpurun_out/r04h_ride_ab.log
 : > $OUT
 for r in 1 2; do
@@ -14,5 +14,5 @@ for r in 1 2; do
     done
   done
 done
-PT_WALK_SCALAR=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "dragon or bunny or helmet" --timeout 120 --timeout-method thread > gpurun_out/r04h_pytest_scalar.log 2>&1 || exit $?
-bash tools/gpu_env_matrix.sh r04h "dragon bunny helmet" 2 "-" "PT_WALK_SCALAR=1" "PT_WALK_PREFETCH=1" "PT_WALK_PRIO=1"
+bash tools/gpu_env_matrix.sh r04h "dragon bunny helmet" 2 "-" "PT_WALK_PREFETCH=1" "PT_WALK_PRIO=1" || exit $?
+bash tools/gpu_evidence.sh r04h
