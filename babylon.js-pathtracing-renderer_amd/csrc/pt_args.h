@@ -87,26 +87,6 @@ struct SkyArgs {
     float retExp;           // 1 / (1.2 + 1.2 * sunfade)
 };
 
-constexpr unsigned kOrderHeld = 128;   // pt_order_build: tiles per thread kept in registers (a byte each)
-struct OutputArgs {
-    int width, height;      // output (canvas or render target) size
-    int num_parts, part;    // with an output partition: only 16-row bands b % num_parts == part
-    int acc_w, acc_h;       // accumulation texture size (texelFetch bounds)
-    float one_over_n, exposure;
-    const float4* acc;
-    uchar4* canvas;         // RGBA8 target (NULL when writing float)
-    float4* out_f;          // RGBA32F target (NULL when writing the canvas)
-    float4* copy_dst;       // a deferred screenCopy of `acc` fused into this pass (NULL: none)
-    // the longest-first order build of the last megakernel draw (pt_order_build) fused into this
-    // pass as one extra block that runs beside the output tiles (NULL ob_cost: none)
-    // (fused only while each of its 256 threads holds its tiles in registers: ntiles <= kOrderHeld * 256)
-    const unsigned* ob_cost;
-    unsigned* ob_order;
-    unsigned* ob_split;
-    unsigned ob_ntiles, ob_cap, ob_dominance;
-    int ob_near;
-};
-
 // Per-draw kernel arguments. Wave-uniform: read with scalar loads from the kernarg segment; the
 // per-object loops index them dynamically so they are re-read from the scalar cache instead of
 // being hoisted into (vector) registers.
@@ -167,14 +147,6 @@ struct TraceArgs {
     // the grid carries padding rows for up to split_cap of them
     const unsigned* split;
     unsigned ntiles;       // 16x16 tiles of the draw
-    // screenOutput riding (pt_capi.cpp render_output / render_trace): the previous frame's screenOutput
-    // to the canvas (and its fused screenCopy) runs in this launch's extra workgroups after the path
-    // waves, one 16x16 output tile each, reading ride.acc = the previous draw's snapshot of its
-    // accumulation (ride.width == 0: none; ride_jobs tiles, ride_tiles_x per row); snap (or NULL): this
-    // draw's accumulation is stored there too, as the next draw's ride source
-    OutputArgs ride;
-    unsigned ride_jobs, ride_tiles_x;
-    float4* snap;
     Tex8 albedo, bump, metal, emissive;
     // diagnostics
     unsigned long long* counters;   // C_NUM entries, only with counting builds
@@ -210,6 +182,26 @@ struct WfBufs {
     unsigned* bcnt;         // [b * kShards + s]: BVH queue of shard s at bounce b
     unsigned shard_cap;     // slots per shard
     int wq, hq;             // quad-rounded frame size
+};
+
+constexpr unsigned kOrderHeld = 128;   // pt_order_build: tiles per thread kept in registers (a byte each)
+struct OutputArgs {
+    int width, height;      // output (canvas or render target) size
+    int num_parts, part;    // with an output partition: only 16-row bands b % num_parts == part
+    int acc_w, acc_h;       // accumulation texture size (texelFetch bounds)
+    float one_over_n, exposure;
+    const float4* acc;
+    uchar4* canvas;         // RGBA8 target (NULL when writing float)
+    float4* out_f;          // RGBA32F target (NULL when writing the canvas)
+    float4* copy_dst;       // a deferred screenCopy of `acc` fused into this pass (NULL: none)
+    // the longest-first order build of the last megakernel draw (pt_order_build) fused into this
+    // pass as one extra block that runs beside the output tiles (NULL ob_cost: none)
+    // (fused only while each of its 256 threads holds its tiles in registers: ntiles <= kOrderHeld * 256)
+    const unsigned* ob_cost;
+    unsigned* ob_order;
+    unsigned* ob_split;
+    unsigned ob_ntiles, ob_cap, ob_dominance;
+    int ob_near;
 };
 
 struct CopyArgs {

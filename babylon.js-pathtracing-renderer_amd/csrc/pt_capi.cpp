@@ -110,18 +110,6 @@ struct Dev {
     // screenCopy deferred to ride along with the next screenOutput of the same source (flushed as
     // its own kernel before anything else could observe the target: flush_copy)
     struct { bool on; DevTex* src; DevTex* dst; int num_parts, part; } pending_copy = {};
-    // screenOutput riding (PT_RIDE=0 disables): a screenOutput to the canvas of the accumulation the
-    // last megakernel draw wrote is deferred (with its fused screenCopy) and runs in the next
-    // path-tracing launch's extra workgroups, in that launch's tail (render_trace), from a snapshot
-    // of the accumulation that draw also stored (snap: two halves, the last one written = snap_last,
-    // mirroring snap_tex); anything else that could observe its results first launches it alone
-    // (flush_output)
-    bool ride = true;
-    struct { bool on; pt::OutputArgs a; DevTex* acc; DevTex* copy_dst; } pending_out = {};
-    void* snap_mem = nullptr;
-    size_t snap_cap = 0;
-    float4* snap_last = nullptr;
-    const DevTex* snap_tex = nullptr;
     bool canvas_external = false;     // dev_canvas_wrap: caller-owned canvas memory
     int backend = PT_BACKEND_MEGAKERNEL;
     int bvh_layout = PT_BVH_PAIRS;
@@ -350,7 +338,6 @@ void setup_scene(const DevFx* fx, pt::TraceArgs& a)
     }
 }
 
-int flush_copy(Dev* c);
 int bands_owned(const Dev* c, int height)
 {
     int nb = (height + pt::kTile - 1) / pt::kTile;
@@ -582,18 +569,9 @@ int flush_order(Dev* c)
 int render_trace(DevFx* fx, DevTex* target)
 {
     Dev* c = fx->ctx;
-    DevTex* prev = sampler(fx, "previousBuffer");
-    // the deferred screenOutput rides in this launch when it reads what this draw's snapshot source
-    // holds (the accumulation this draw overwrites) and writes nothing this draw touches: the draw
-    // then reads its history from that snapshot too (the ride writes the history texture meanwhile)
-    const auto& po = c->pending_out;
-    const bool megakernel_full = c->ride && c->backend == PT_BACKEND_MEGAKERNEL && !c->counting && c->num_parts == 1;
-    const bool ride = po.on && megakernel_full && target && target == po.acc && c->snap_tex == target && c->snap_last &&
-                      po.copy_dst != target;
-    if (!ride) { if (int rc = flush_copy(c)) return rc; }   // the deferred screenOutput / screenCopy, alone
-    c->snap_tex = nullptr;   // this draw rewrites its target: only its own snapshot (below) mirrors it
     if (int rc = flush_order(c)) return rc;   // this draw's order (before lpt_mem could be reallocated)
     if (!target || target->kind != TEX_RT) return fail(c, PT_ERR_ARG, "path tracing draws need a render target");
+    DevTex* prev = sampler(fx, "previousBuffer");
     DevTex* bn = sampler(fx, "blueNoiseTexture");
     if (!prev || prev->kind == TEX_U8 || prev->w != target->w || prev->h != target->h)
         return fail(c, PT_ERR_STATE, "previousBuffer must be an RGBA32F texture of the target's size");
@@ -734,34 +712,7 @@ int render_trace(DevFx* fx, DevTex* target)
                 a.split = (a.order && split) ? c->lpt_mem + 5 * c->lpt_cap : nullptr;
             }
             a.ntiles = (unsigned)n;
-            int rows = a.split ? gy_grid : gy;
-            // the snapshot of this draw's accumulation (the next draw's ride source): the half the
-            // riding screenOutput (if any) does not read
-            float4* snap = nullptr;
-            if (megakernel_full) {
-                const size_t px = (size_t)target->w * target->h;
-                if (c->snap_cap < px) {
-                    if (ride) { if (int rc = flush_copy(c)) return rc; }   // (cannot happen: same target size)
-                    if (c->snap_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->snap_mem)); }
-                    c->snap_mem = nullptr; c->snap_cap = 0; c->snap_last = nullptr; c->snap_tex = nullptr;
-                    HIPCHK(c, hipMalloc(&c->snap_mem, 2 * px * sizeof(float4)));
-                    c->snap_cap = px;
-                }
-                float4* half0 = (float4*)c->snap_mem;
-                snap = c->snap_last == half0 ? half0 + c->snap_cap : half0;
-                a.snap = snap;
-            }
-            if (ride && c->pending_out.on) {
-                a.ride = c->pending_out.a;
-                a.ride_tiles_x = (unsigned)((a.ride.width + pt::kTile - 1) / pt::kTile);
-                a.ride_jobs = a.ride_tiles_x * (unsigned)((a.ride.height + pt::kTile - 1) / pt::kTile);
-                if (prev == c->pending_out.copy_dst) a.prev = c->snap_last;   // the same texels, not being rewritten
-                rows += (int)((a.ride_jobs + 4u * gx - 1) / (4u * gx));
-                c->pending_out.on = false;
-            }
-            HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, rows, c->stream));
-            c->snap_last = snap;
-            c->snap_tex = snap ? target : nullptr;
+            HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, c->stream));
             if (a.cost) {
                 c->pending_order = { true, (unsigned)n, a.cost, c->lpt_mem + 4 * c->lpt_cap, c->lpt_mem + 5 * c->lpt_cap,
                                      (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance, c->split_near };
@@ -776,7 +727,6 @@ int render_trace(DevFx* fx, DevTex* target)
 
 int launch_copy(Dev* c, DevTex* src, DevTex* dst, int num_parts, int part)
 {
-    if (dst == c->snap_tex) c->snap_tex = nullptr;
     pt::CopyArgs a{ dst->w, dst->h, num_parts, part, (const float4*)src->d, (float4*)dst->d };
     const int nb = (dst->h + pt::kTile - 1) / pt::kTile;
     int gx = (dst->w + 255) / 256, gy = part < nb ? (nb - part + num_parts - 1) / num_parts : 0;
@@ -785,10 +735,8 @@ int launch_copy(Dev* c, DevTex* src, DevTex* dst, int num_parts, int part)
 }
 
 // run a deferred screenCopy now, as its own kernel (timed as a screenCopy draw)
-int flush_output(Dev* c);
 int flush_copy(Dev* c)
 {
-    if (int rc = flush_output(c)) return rc;   // a deferred screenOutput carries its screenCopy
     if (!c->pending_copy.on) return PT_OK;
     c->pending_copy.on = false;
     int rc = begin_draw(c, PT_PROG_SCREEN_COPY);
@@ -813,7 +761,6 @@ int render_copy(DevFx* fx, DevTex* target)
     return PT_OK;
 }
 
-int launch_output(Dev* c, pt::OutputArgs a, int prog);
 int render_output(DevFx* fx, DevTex* target)
 {
     Dev* c = fx->ctx;
@@ -850,26 +797,11 @@ int render_output(DevFx* fx, DevTex* target)
         }
         a.width = c->cw; a.height = c->ch; a.canvas = c->canvas;
     }
-    // riding: a screenOutput of the whole canvas from the accumulation the last megakernel draw
-    // wrote (and mirrored in its snapshot) waits for the next path-tracing launch (render_trace)
-    if (c->ride && !target && !c->canvas_external && a.num_parts == 1 && c->num_parts == 1 && c->snap_tex == acc &&
-        c->snap_last && a.width > 0 && a.height > 0 && c->backend == PT_BACKEND_MEGAKERNEL && !c->counting) {
-        a.acc = c->snap_last;
-        c->pending_out = { true, a, acc, fuse ? pc.dst : nullptr };
-        return PT_OK;
-    }
-    return launch_output(c, a, fx->prog);
-}
-
-// a screenOutput pass as its own kernel (with the pending longest-first order build riding along)
-int launch_output(Dev* c, pt::OutputArgs a, int prog)
-{
     // the order build rides along only up to 32768 tiles (4K): beyond, the block's 256 threads would
     // loop over memory and outlast the pass, so it runs alone first (1024 threads)
     if (c->pending_order.on && c->pending_order.n > pt::kOrderHeld * 256u)
         if (int frc = flush_order(c)) return frc;
-    if (a.out_f && c->snap_tex && (const void*)a.out_f == c->snap_tex->d) c->snap_tex = nullptr;
-    int rc = begin_draw(c, prog);
+    int rc = begin_draw(c, fx->prog);
     if (rc) return rc;
     if (a.width > 0 && a.height > 0) {
         if (c->pending_order.on) {   // the last megakernel draw's order build rides along as one more block
@@ -880,16 +812,7 @@ int launch_output(Dev* c, pt::OutputArgs a, int prog)
         }
         HIPCHK(c, pt_launch_output(&a, c->stream));
     }
-    return end_draw(c, prog);
-}
-
-// the deferred screenOutput alone, now (its snapshot source is still the accumulation's contents:
-// every draw or write that could change either flushes first)
-int flush_output(Dev* c)
-{
-    if (!c->pending_out.on) return PT_OK;
-    c->pending_out.on = false;
-    return launch_output(c, c->pending_out.a, PT_PROG_SCREEN_OUTPUT);
+    return end_draw(c, fx->prog);
 }
 
 DevTex* new_texture(Dev* c, int kind, int w, int h, size_t texel, int* err)
@@ -969,7 +892,6 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_BVH_LAYOUT"))   // reference | pairs | trail: the context's initial walk
         c->bvh_layout = !std::strcmp(v, "trail") ? PT_BVH_TRAIL : !std::strcmp(v, "reference") ? PT_BVH_REFERENCE
                                                                                   : PT_BVH_PAIRS;
-    if (const char* v = std::getenv("PT_RIDE")) c->ride = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_WALK_PREFETCH")) c->walk_prefetch = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_WALK_PRIO")) c->walk_prio = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
@@ -993,7 +915,6 @@ void dev_ctx_destroy(Dev* c)
     if (!c) return;
     hipSetDevice(c->device);
     c->pending_copy.on = false;   // nothing can observe its target any more
-    c->pending_out.on = false;    // ... nor the canvas
     c->pending_order.on = false;  // ... nor a next draw the order
     if (c->stream) hipStreamSynchronize(c->stream);
     std::vector<DevFx*> fx(c->effects.begin(), c->effects.end());
@@ -1009,7 +930,6 @@ void dev_ctx_destroy(Dev* c)
     if (c->wf_mem) hipFree(c->wf_mem);
     if (c->lpt_mem) hipFree(c->lpt_mem);
     if (c->mk_spill) hipFree(c->mk_spill);
-    if (c->snap_mem) hipFree(c->snap_mem);
     if (c->gb_mem) hipFree(c->gb_mem);
     if (c->d_err) hipFree(c->d_err);
     if (c->d_counters) hipFree(c->d_counters);
@@ -1039,7 +959,6 @@ int dev_canvas_resize(Dev* c, int w, int h)
     if (!c || w < 0 || h < 0) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     if (w == c->cw && h == c->ch && c->canvas && !c->canvas_external) return PT_OK;
-    if (int rc = flush_copy(c)) return rc;   // a deferred screenOutput writes the present canvas
     if (c->canvas) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
         if (!c->canvas_external) HIPCHK(c, hipFree(c->canvas));
@@ -1058,7 +977,6 @@ int dev_canvas_wrap(Dev* c, int w, int h, void* ptr)
 {
     if (!c || w <= 0 || h <= 0 || !ptr) return PT_ERR_ARG;
     HIPCHK(c, hipSetDevice(c->device));
-    if (int rc = flush_copy(c)) return rc;   // a deferred screenOutput writes the present canvas
     if (c->canvas && !c->canvas_external) {   // switching between wrapped canvases needs no sync
         HIPCHK(c, hipStreamSynchronize(c->stream));
         HIPCHK(c, hipFree(c->canvas));
@@ -1182,7 +1100,6 @@ int dev_render_target_resize(DevTex* t, int w, int h)
     if (t->d) HIPCHK(c, hipFree(t->d));
     t->d = nullptr;
     t->w = w; t->h = h; t->bytes = (size_t)w * h * 16;
-    if (c->snap_tex == t) c->snap_tex = nullptr;
     HIPCHK(c, hipMalloc(&t->d, t->bytes));
     HIPCHK(c, hipMemsetAsync(t->d, 0, t->bytes, c->stream));
     return PT_OK;
@@ -1201,10 +1118,7 @@ void dev_texture_destroy(DevTex* t)
     if (!t) return;
     Dev* c = t->ctx;
     hipSetDevice(c->device);
-    if ((c->pending_copy.on && (c->pending_copy.src == t || c->pending_copy.dst == t)) ||
-        (c->pending_out.on && (c->pending_out.acc == t || c->pending_out.copy_dst == t)))
-        flush_copy(c);
-    if (c->snap_tex == t) c->snap_tex = nullptr;
+    if (c->pending_copy.on && (c->pending_copy.src == t || c->pending_copy.dst == t)) flush_copy(c);
     for (auto* fx : c->effects)
         for (auto& kv : fx->samplers)
             if (kv.second == t) kv.second = nullptr;
@@ -1222,7 +1136,10 @@ int dev_render(DevFx* fx, DevTex* target)
     Dev* c = fx->ctx;
     if (target && target->ctx != c) return fail(c, PT_ERR_ARG, "target belongs to another context");
     HIPCHK(c, hipSetDevice(c->device));
-    // (path-tracing draws flush in render_trace, unless the deferred screenOutput rides in them)
+    if (fx->prog != PT_PROG_SCREEN_OUTPUT && fx->prog != PT_PROG_SCREEN_COPY) {
+        int rc = flush_copy(c);
+        if (rc) return rc;
+    }
     switch (fx->prog) {
     case PT_PROG_CORNELL:
     case PT_PROG_QUADRIC:
@@ -1257,7 +1174,6 @@ int dev_write_pixels(Dev* c, DevTex* t, const void* src, size_t bytes)
     HIPCHK(c, hipMemcpyAsync(t->d, src, bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     t->gen++;
-    if (c->snap_tex == t) c->snap_tex = nullptr;
     return PT_OK;
 }
 

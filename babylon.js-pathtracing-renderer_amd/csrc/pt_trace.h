@@ -9,7 +9,6 @@
 #include "pt_args.h"
 #include "pt_device.h"
 #include "pt_glsl.h"
-#include "pt_output.h"
 #include "pt_program.h"
 #ifdef PT_SECPROF
 #define PT_SECPROF_ON 1
@@ -204,27 +203,6 @@ PT_D void accumulate(const TraceArgs& a, long long pi, f3 r, float sharp, bool e
     typedef float nt4 __attribute__((ext_vector_type(4)));
     const nt4 o = { prev.x + cr, prev.y + cg, prev.z + cb, ca };
     __builtin_nontemporal_store(o, (nt4*)&a.out[pi]);
-    if (a.snap) __builtin_nontemporal_store(o, (nt4*)&a.snap[pi]);   // the next draw's screenOutput source
-}
-
-// screenOutput riding (TraceArgs::ride): output tile `job` of the previous frame, 16x16 pixels as four
-// 8x8 quadrants, each from its 12x12 neighbourhood staged in the workgroup's LDS (the stack's, unused
-// by this workgroup); the same per-pixel program as pt_output, on the snapshot of the same texels, so
-// the canvas and the fused screenCopy get the same bits
-PT_D void rideOutput(const TraceArgs& a, unsigned job, float2* lds, int lane)
-{
-    const OutputArgs& o = a.ride;
-    float4* tile = (float4*)lds;
-    const int tx = (int)(job % a.ride_tiles_x), ty = (int)(job / a.ride_tiles_x);
-    const int lx = lane & 7, ly = lane >> 3;
-    for (int q = 0; q < 4; q++) {
-        const int x0 = tx * kTile + (q & 1) * 8, y0 = ty * kTile + (q >> 1) * 8;
-        for (int i = lane; i < 144; i += 64) tile[i] = accAt(o, x0 + i % 12 - 2, y0 + i / 12 - 2);
-        __syncthreads();
-        const int x = x0 + lx, y = y0 + ly;
-        if (x < o.width && y < o.height) outputPixel<12>(o, tile, lx, ly, x, y);
-        __syncthreads();
-    }
 }
 
 PT_D float xorq(float v, int m) { return __shfl_xor(v, m, 64); }
@@ -301,7 +279,6 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     // the G-buffer's LDS fields (none in some variants: no zero-length array)
     __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock + (kGoutLdsOf<PROG> * kTraceBlock + 1) / 2];
     float* const lds_gout = (float*)(lds_stack + kWalkSlotsOf<PROG> * kTraceBlock);
-    static_assert(kWalkSlotsOf<PROG> * kTraceBlock >= 144 * 2, "rideOutput stages 12x12 float4 in the stack's LDS");
     const unsigned tid = threadIdx.x;
     const int lane = tid & 63;
     const unsigned long long t_start = clock64();
@@ -309,15 +286,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     const unsigned long long w0_ = wall_clock64();
 #endif
     TracePlace pl;
-    if (!tracePlace(a, lane, pl)) {   // the grid's padding, then the riding screenOutput tiles
-        if (a.ride.width > 0) {
-            const unsigned K = (a.order && a.split) ? *a.split : 0u;
-            const unsigned paths = 4u * kSplitParts * K + 4u * (a.ntiles - K);   // path-tracing workgroups
-            const unsigned L = blockIdx.y * gridDim.x + blockIdx.x;
-            if (L >= paths && L - paths < a.ride_jobs) rideOutput(a, L - paths, lds_stack, lane);
-        }
-        return;
-    }
+    if (!tracePlace(a, lane, pl)) return;   // the grid's padding
     const int px = pl.px, py = pl.py;
     // stack levels >= kStackLds: a global slab [level][lane of the grid] (a private array would be
     // scratch, which the runtime reserves for every resident wave)

@@ -420,44 +420,6 @@ def test_deferred_screen_copy_is_observed_exactly(engine):
     assert _bits_equal(ref[2], player.textures["pathTracingRenderTarget"].read())
 
 
-@pytest.mark.parametrize("name,size", [("cornell_256", None), ("gltf_teapot_320x180", (203, 117)),
-                                       ("hdri_helmet_320x180", None)])
-def test_screen_output_rides_next_path_tracing_draw(engine, name, size):
-    """screenOutput to the canvas is deferred and runs in the next path-tracing launch's tail
-    (render_trace, TraceArgs::ride), from a snapshot of the accumulation, with the frame's screenCopy
-    fused; that next draw reads its history from the snapshot. Frame by frame: canvas i, history i and
-    accumulation i + 1 after the draw that carried output i, all bit-exact; the timing window shows
-    that only the last output (flushed by the final sync) ran as its own kernel."""
-    import babylon_pt as bp
-    meta = H.stream(name)
-    W, Hh = size or (meta["width"], meta["height"])
-    maps = H.helmet_maps() if "helmet" in name else None
-    m = H.texture_payloads(meta, H.mesh(meta)) if meta["scene"] in ("gltf", "hdri") else None
-    player = bp.StreamPlayer(engine, meta, H.bluenoise(), m, W, Hh)
-    if maps:
-        for kind, sampler in H.PBR_SAMPLERS.items():
-            player.textures[sampler] = bp.Texture(engine, maps[kind], name=kind)
-    engine.resize_canvas(W, Hh)
-    ref_acc, ref_can, _ = H.oracle_replay(meta, width=W, height=Hh, with_output=True, maps=maps)
-    frames = meta["frames"]
-    engine.sync()
-    engine.timing_begin()
-    player.play_call(frames[0][0])
-    for i in range(len(frames) - 1):
-        player.play_call(frames[i][1])        # screenCopy: deferred
-        player.play_call(frames[i][2])        # screenOutput: deferred, carrying the copy
-        player.play_call(frames[i + 1][0])    # the next path tracing carries both
-        assert _bits_equal(ref_can[i], engine.read_canvas(W, Hh)), "frame %d canvas" % i
-        assert _bits_equal(ref_acc[i], player.textures["screenCopyRenderTarget"].read()), "frame %d history" % i
-        assert _bits_equal(ref_acc[i + 1], player.textures["pathTracingRenderTarget"].read()), "frame %d accumulation" % (i + 1)
-    for c in frames[-1][1:]:
-        player.play_call(c)
-    engine.sync()
-    assert _bits_equal(ref_can[-1], engine.read_canvas(W, Hh))
-    _, launches = engine.timing_end("screenOutput")
-    assert launches == 1, launches
-
-
 def test_odd_sizes_bitexact(engine, backend):
     """Odd target sizes: quad helpers beyond the edge, partial 16x16 tiles, partial bands."""
     meta = H.stream("gltf_teapot_320x180")
