@@ -133,8 +133,6 @@ struct TraceArgs {
     uint32_t bvh_pairs_bytes;  // size of the record array (its buffer descriptor)
     uint32_t bvh_top_base;     // PROG_TRAIL: byte offset of the restart jump table (inner-record copies) in it
     int bvh_walk;              // WALK_REF / _PAIRS / _TRAIL (pt_device.h): the variant the draw takes
-    int walk_prefetch;         // child-pair walk: prefetch each pushed far child's record line (PT_WALK_PREFETCH)
-    int walk_prio;             // the child-pair walk at wave priority 1 (PT_WALK_PRIO)
     float2* spill;             // megakernel BVH stack levels >= kStackLds: [level][grid lane]
     unsigned spill_stride;
     // longest-first dispatch (megakernel): order[slot] = the 16x16 tile dealt to tile slot `slot`

@@ -113,8 +113,6 @@ struct Dev {
     bool canvas_external = false;     // dev_canvas_wrap: caller-owned canvas memory
     int backend = PT_BACKEND_MEGAKERNEL;
     int bvh_layout = PT_BVH_PAIRS;
-    int walk_prefetch = 0;   // PT_WALK_PREFETCH
-    int walk_prio = 0;       // PT_WALK_PRIO
     int bvh_used = -1;
     int cu_count = 256;
     pt::WfBufs wf = {};
@@ -621,8 +619,6 @@ int render_trace(DevFx* fx, DevTex* target)
         }
         if (prc) return prc;
         a.bvh_walk = a.bvh_top_base ? pt::WALK_TRAIL : a.bvh_pairs ? pt::WALK_PAIRS : pt::WALK_REF;
-        a.walk_prefetch = c->walk_prefetch;
-        a.walk_prio = c->walk_prio;
         c->bvh_used = a.bvh_top_base ? PT_BVH_TRAIL : a.bvh_pairs ? PT_BVH_PAIRS : PT_BVH_REFERENCE;
         a.albedo = tex8(sampler(fx, "tAlbedoTexture"));
         a.bump = tex8(sampler(fx, "tBumpTexture"));
@@ -892,8 +888,6 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_BVH_LAYOUT"))   // reference | pairs | trail: the context's initial walk
         c->bvh_layout = !std::strcmp(v, "trail") ? PT_BVH_TRAIL : !std::strcmp(v, "reference") ? PT_BVH_REFERENCE
                                                                                   : PT_BVH_PAIRS;
-    if (const char* v = std::getenv("PT_WALK_PREFETCH")) c->walk_prefetch = std::atoi(v) != 0;
-    if (const char* v = std::getenv("PT_WALK_PRIO")) c->walk_prio = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);

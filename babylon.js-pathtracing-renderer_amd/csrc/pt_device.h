@@ -560,8 +560,6 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
     int sp = 0;
     int pop = curT < hitT ? 0 : 1;
     float tID = -1.0f, tU = 0.0f, tV = 0.0f;
-    const bool prefetch = a.walk_prefetch != 0;   // wave-uniform (kernel argument)
-    uint32_t pfv = 0u;
     for (;;) {
         asm volatile("" : "+v"(pop));
         const int sp2 = sp - pop;
@@ -587,13 +585,9 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
             const float tN = sw ? tB : tA, tF = sw ? tA : tB;
             const bool hitN = tN < hT, hitF = tF < hT;
             const float cN = sw ? r3.y : r3.x, cF = sw ? r3.x : r3.y;   // codes as float bits: only moved
-            if (prefetch) asm volatile("" ::"v"(pfv));   // the last prefetch has landed (older than this step's loads)
             if (hitN && hitF) {
                 stackPush(a, st, sp, make_float2(tF, cF), r.ovf);
                 sp++;
-                // PT_WALK_PREFETCH: the pushed far child's record line towards the caches now, so that its
-                // pop later finds it there (a first dword whose value is never used)
-                if (prefetch) pfv = __builtin_amdgcn_raw_buffer_load_b32(b.rec, (int)(__float_as_uint(cF) & ~kLeafBit), 0, 0);
             }
             code = __float_as_uint(hitN ? cN : hitF ? cF : __uint_as_float(code));
             pop = (hitN || hitF) ? 0 : 1;

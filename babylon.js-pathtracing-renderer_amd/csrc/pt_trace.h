@@ -124,11 +124,8 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
         const float* rb = a.bvh_root_box;
         const float rootT = box(mk(rb[0], rb[1], rb[2]), mk(rb[3], rb[4], rb[5]), O, inv);
         auto walk = [&]() {
-            // PT_WALK_PRIO: the walk's dependent chain issues ahead of other waves' shading
-            if (a.walk_prio) __builtin_amdgcn_s_setprio(1);
             if (kTrail<PROG>) bvhWalkTrail<kRingOf<PROG>>(a, O, D, inv, dbl, rootT, h.t, (lds_float2*)lds, LS, lane_slot, br);
             else bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
-            if (a.walk_prio) __builtin_amdgcn_s_setprio(0);
         };
 #ifdef PT_SECPROF
         if (cnt.sec) {

@@ -11,6 +11,7 @@ rm -rf "$OUT"; mkdir -p "$OUT/pkg" "$OUT/include"
 cp -r "$ROOT/babylon.js-pathtracing-renderer_amd/csrc" "$ROOT/babylon.js-pathtracing-renderer_amd/Makefile" "$OUT/pkg/"
 cp "$ROOT/include/pt.h" "$OUT/include/"
 if [ -n "$3" ]; then sed -i "$3" "$OUT"/pkg/csrc/*.h "$OUT"/pkg/csrc/*.hip "$OUT"/pkg/csrc/*.cpp; fi
+if [ -n "$4" ]; then python3 "$4" "$OUT/pkg/csrc" $5; fi
 make -s -C "$OUT/pkg" -j8 libpt.so \
   HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-function -Wno-unused-result -Wno-unused-value $FLAGS" >/dev/null
 mv "$OUT/pkg/libpt.so" "$OUT/libpt.so"
