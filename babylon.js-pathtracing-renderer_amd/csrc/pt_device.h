@@ -551,7 +551,7 @@ PT_D bool pairWalkFast(f3 O, f3 inv)
 // the next record's first 8 B (or 0 past the end of the array) and is not used.
 template <class Stk>
 PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float curT, float& hitT, Stk& st,
-                       BvhResult& r)
+                       BvhResult& r, bool anyHit = false)
 {
     const bool fast = pairWalkFast(O, inv);
     const PairBufs b = pairBufs(a);
@@ -595,7 +595,10 @@ PT_D void bvhWalkPairs(const TraceArgs& a, f3 O, f3 D, f3 inv, bool dbl, float c
             r.leaves++;
             float tu, tv;
             const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
-            if (d < hT) { hT = d; tID = 8.0f * r2.y; tU = tu; tV = tv; }
+            if (d < hT) {
+                hT = d; tID = 8.0f * r2.y; tU = tu; tV = tv;
+                if (anyHit) sp = 0;   // the first occluder ends the walk: the next step's pop finds it empty
+            }
             // a use on this side too keeps the codes' load with the other three: sunk into the inner-node
             // branch, it was issued only after a mixed wave's leaf tests (-3 % kernel time)
             asm volatile("" ::"v"(r3.x));

@@ -102,8 +102,18 @@ PT_D void meshHit(const TraceArgs& a, float triID, float triU, float triV, Hit& 
 // js/GLTFModelPathTracing_FragmentShader.js:116-346 (glTF, with the BVH walk)
 template <int PROG, bool COUNT, int LS>
 PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* lds, unsigned lane_slot,
-                         unsigned deep, Cnt& cnt)
+                         unsigned deep, Cnt& cnt, bool shadow)
 {
+    // A shadow ray (CalculateRadiance's sampleLight) ends its path at whatever it hits first: the
+    // light's colour is added when that is the light (glTF / Cornell), the environment's when it is
+    // nothing (HDRI / sky), and nothing else of the hit is read (shadeStep: `if (s.sampleLight) return
+    // false` comes before any use of the hit's normal, uv or material maps; the G-buffer is written at
+    // bounce 0, or at bounce 1 after METAL, which never samples the light). So for it the walk may stop
+    // at the first triangle closer than the analytic winner - the reference's walk, visiting the same
+    // nodes in the same order up to there, also ends with the mesh in front - and the hit needs no
+    // lookup: the mesh's type and colour are the same for every triangle. The counting variant keeps
+    // the reference's full closest-hit walk and lookup: it prices the reference's work.
+    const bool anyHit = !COUNT && shadow;
     if (COUNT) cnt.seg++;
     // the analytic winner's t, id and object-space normal; its other attributes are resolved after
     // the walk, and only if the mesh does not win (meshHit sets them all): fewer values live across
@@ -125,7 +135,7 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
         const float rootT = box(mk(rb[0], rb[1], rb[2]), mk(rb[3], rb[4], rb[5]), O, inv);
         auto walk = [&]() {
             if (kTrail<PROG>) bvhWalkTrail<kRingOf<PROG>>(a, O, D, inv, dbl, rootT, h.t, (lds_float2*)lds, LS, lane_slot, br);
-            else bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);
+            else bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br, anyHit);
         };
 #ifdef PT_SECPROF
         if (cnt.sec) {
@@ -149,7 +159,12 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     br.ws.flush(a.walk_stat, cnt.bounce++);
 #endif
     PT_SEC(cnt, 2);
-    if (br.lookup) meshHit<PROG, COUNT>(a, br.triID, br.triU, br.triV, h, cnt);
+    if (br.lookup && anyHit) {   // the mesh occludes: what shadeStep reads of a mesh hit, no lookup
+        h.normal = mk(0.0f, 0.0f, 1.0f);
+        h.type = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
+        h.color = mk(1.0f, 1.0f, 1.0f);
+        h.id = meshObjectId<PROG>(a);
+    } else if (br.lookup) meshHit<PROG, COUNT>(a, br.triID, br.triU, br.triV, h, cnt);
     else analyticAttributes<PROG>(a, h, sn);
     PT_SEC(cnt, 3);
 }
@@ -160,7 +175,7 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, fl
                      unsigned deep, Cnt& cnt)
 {
     Hit h;
-    sceneIntersect<PROG, COUNT, LS>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt);
+    sceneIntersect<PROG, COUNT, LS>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt, s.sampleLight);
     return shadeStep<PROG, COUNT, G>(a, p, s, g, accum, h, cnt);
 }
 
