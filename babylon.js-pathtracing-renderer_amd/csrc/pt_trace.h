@@ -112,8 +112,11 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     // at the first triangle closer than the analytic winner - the reference's walk, visiting the same
     // nodes in the same order up to there, also ends with the mesh in front - and the hit needs no
     // lookup: the mesh's type and colour are the same for every triangle. The counting variant keeps
-    // the reference's full closest-hit walk and lookup: it prices the reference's work.
-    const bool anyHit = !COUNT && shadow;
+    // the reference's full closest-hit walk and lookup: it prices the reference's work. Only in the
+    // textured (4-wave) variants: helmet + HDRI -3.5 %; in the 8-wave ones the dragon stand-in and the
+    // sky composite gain nothing (few of their shadow rays are occluded by the mesh) and the bunny
+    // loses 1.3 % to the extra code (profiles/r04k_envmx_anyhit.txt).
+    const bool anyHit = !COUNT && kHasTex<PROG> && shadow;
     if (COUNT) cnt.seg++;
     // the analytic winner's t, id and object-space normal; its other attributes are resolved after
     // the walk, and only if the mesh does not win (meshHit sets them all): fewer values live across
