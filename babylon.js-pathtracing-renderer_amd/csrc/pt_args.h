@@ -182,7 +182,7 @@ struct WfBufs {
     int wq, hq;             // quad-rounded frame size
 };
 
-constexpr unsigned kOrderHeld = 32;    // pt_order_build: tiles per thread kept in registers (a byte each)
+constexpr unsigned kOrderHeld = 128;   // pt_order_build: tiles per thread kept in registers (a byte each)
 struct OutputArgs {
     int width, height;      // output (canvas or render target) size
     int num_parts, part;    // with an output partition: only 16-row bands b % num_parts == part

@@ -66,11 +66,11 @@ PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, uns
     auto tileBucket = [&](unsigned t) { return costBucket(tileCost(t)); };
     unsigned long long part = 0;
     unsigned mx = 0;
-    // up to kOrderHeld tiles per thread (32: a 1080p frame with 256 threads, 4K with 1024) go through registers,
+    // up to kOrderHeld tiles per thread (128: a 4K frame with 256 threads) go through registers,
     // their buckets four to a register: all the cost loads of a chunk are issued before its LDS
     // atomics (a loop with the atomic inside waits one HBM round trip per iteration), and the
     // scatter reuses the buckets instead of reloading
-    constexpr int kOrderChunk = 4;
+    constexpr int kOrderChunk = 8;
     const bool held = ntiles <= kOrderHeld * blockDim.x;
     unsigned bk[(int)kOrderHeld / 4];
     if (held) {
@@ -195,15 +195,14 @@ PT_D float4 accAt(const OutputArgs& a, int x, int y)
 // pixel's place in the 16x16 tile)
 PT_D void outputPixel(const OutputArgs& a, const float4* tile, int lx, int ly, int x, int y)
 {
-    // tap k of the 5x5 (row-major from the top, GL's y up): read from LDS where it is used, not all
-    // 25 into registers first (124 -> VGPRs, 4 -> waves per SIMD)
-    const float4* t0 = tile + (ly + 4) * 20 + lx;
-    auto m25 = [&](int k) { return t0[(k % 5) - (k / 5) * 20]; };
+    float4 m25[25];
+#pragma unroll
+    for (int k = 0; k < 25; k++) m25[k] = tile[(ly + 2 + 2 - (k / 5)) * 20 + (lx + 2 + (k % 5) - 2)];
     // the frame's screenCopy (js/PathTracingCommon.js:1-16), deferred by the host to ride along:
     // the same texel of the same source, written to the copy target
-    const float4 cp = m25(12);
-    if (a.copy_dst) a.copy_dst[(long long)y * a.acc_w + x] = cp;
+    if (a.copy_dst) a.copy_dst[(long long)y * a.acc_w + x] = m25[12];
     const float th = 1.0f;
+    float4 cp = m25[12];
     float fr = cp.x, fg = cp.y, fb = cp.z;
     int count = 1;
     // first-ring tap, then its two outer taps, in the reference's order (js/PathTracingCommon.js:82-209)
@@ -211,12 +210,10 @@ PT_D void outputPixel(const OutputArgs& a, const float4* tile, int lx, int ly, i
                                { 6, 0, 1 }, { 8, 4, 9 }, { 16, 15, 20 }, { 18, 23, 24 } };
 #pragma unroll
     for (int r = 0; r < 8; r++) {
-        const float4 q0 = m25(T5[r][0]);
-        if (q0.w < th) {
-            fr += q0.x; fg += q0.y; fb += q0.z; count++;
-            const float4 q1 = m25(T5[r][1]), q2 = m25(T5[r][2]);
-            if (q1.w < th) { fr += q1.x; fg += q1.y; fb += q1.z; count++; }
-            if (q2.w < th) { fr += q2.x; fg += q2.y; fb += q2.z; count++; }
+        if (m25[T5[r][0]].w < th) {
+            fr += m25[T5[r][0]].x; fg += m25[T5[r][0]].y; fb += m25[T5[r][0]].z; count++;
+            if (m25[T5[r][1]].w < th) { fr += m25[T5[r][1]].x; fg += m25[T5[r][1]].y; fb += m25[T5[r][1]].z; count++; }
+            if (m25[T5[r][2]].w < th) { fr += m25[T5[r][2]].x; fg += m25[T5[r][2]].y; fb += m25[T5[r][2]].z; count++; }
         }
     }
     fr /= (float)count; fg /= (float)count; fb /= (float)count;
@@ -225,10 +222,8 @@ PT_D void outputPixel(const OutputArgs& a, const float4* tile, int lx, int ly, i
         count = 1;
         fr = cp.x; fg = cp.y; fb = cp.z;
 #pragma unroll
-        for (int r = 0; r < 8; r++) {
-            const float4 q = m25(R3[r]);
-            if (q.w < th) { fr += q.x; fg += q.y; fb += q.z; count++; }
-        }
+        for (int r = 0; r < 8; r++)
+            if (m25[R3[r]].w < th) { fr += m25[R3[r]].x; fg += m25[R3[r]].y; fb += m25[R3[r]].z; count++; }
         fr /= (float)count; fg /= (float)count; fb /= (float)count;
         fr = gmix(fr, cp.x, 0.5f); fg = gmix(fg, cp.y, 0.5f); fb = gmix(fb, cp.z, 0.5f);
     }
