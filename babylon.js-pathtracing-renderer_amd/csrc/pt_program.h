@@ -67,24 +67,34 @@ typedef __attribute__((address_space(1))) float glb_float;
 // spheres / quadric shapes, the quads, the mesh), bit 23 "objectNormal's fields beyond LDS were
 // written", bit 31 the same for objectColor; the blue-noise counter keeps bits 16-22 (at most 13
 // draws per path). LS = lanes of the workgroup = the stride of one field; NF = the normal / colour
-// fields in LDS (from the normal's x), the rest in the lane's 6 - NF floats at `gx` (after the stack
-// slab's levels): stored only by setNrm / setCol and read only when their bit says so - no clearing
-// store, no id / sharpness traffic at all.
+// fields in LDS (from the normal's x), the rest at `gx` (after the stack slab's levels), field-major
+// [field][lane of the grid] with `gs` lanes per field, so that a wave's store of one field is one
+// contiguous 256-B run: stored only by setNrm / setCol and read only when their bit says so - no
+// clearing store, no id / sharpness traffic at all.
 template <int LS, int NF = 6>
 struct GOutLds {
     lds_float* p;
     unsigned slot;
-    glb_float* gx;
+    glb_float* gx;    // wave-uniform base ...
+    unsigned gi, gs;  // ... this lane's index, lanes per field (32-bit: one VGPR, shared with the stack slab's)
     uint32_t* bn;
+    // the address formed where it is used (the empty asm keeps it from being hoisted out of the
+    // bounce loop as six 64-bit pointers)
+    PT_D unsigned at(int f) const
+    {
+        unsigned i = gi;
+        asm volatile("" : "+v"(i));
+        return i + (unsigned)(f - NF) * gs;
+    }
     PT_D void put(int f, float v)
     {
         if (f < NF) p[f * LS + slot] = v;
-        else gx[f - NF] = v;
+        else gx[at(f)] = v;
     }
     PT_D float get(int f) const
     {
         if (f < NF) return p[f * LS + slot];
-        return ((*bn >> (f < 3 ? 23 : 31)) & 1u) ? gx[f - NF] : 0.0f;
+        return ((*bn >> (f < 3 ? 23 : 31)) & 1u) ? gx[at(f)] : 0.0f;
     }
     PT_D void clear()
     {

@@ -320,13 +320,13 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     cnt.bounce = 0;
 #endif
     // G-buffer fields beyond the LDS ones: 6 - kGoutLdsOf floats per lane after the slab's stack
-    // levels, [lane][field] (pt_capi.cpp spill_reserve)
+    // levels, [field][lane] (pt_capi.cpp spill_reserve)
     glb_float* const gx = kGoutLdsOf<PROG> < 6
-        ? (glb_float*)(a.spill + (size_t)(kStackLevels - kStackLdsMin) * a.spill_stride) + (size_t)deep * (6 - kGoutLdsOf<PROG>)
+        ? (glb_float*)(a.spill + (size_t)(kStackLevels - kStackLdsMin) * a.spill_stride)
         : nullptr;
     Path p;
     p.bn = 0u;
-    GOutLds<kTraceBlock, kGoutLdsOf<PROG>> gl{ (lds_float*)lds_gout, tid, gx, &p.bn };
+    GOutLds<kTraceBlock, kGoutLdsOf<PROG>> gl{ (lds_float*)lds_gout, tid, gx, deep, a.spill_stride, &p.bn };
     gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
     f3 r = mk(0, 0, 0);
     if (active) {
