@@ -74,16 +74,17 @@ template <int P> constexpr int kMinWaves = kHasTex<P> ? kMinWavesTex : kPairs<P>
 // more often, keeps all 6 (its 10-level form measured +1 %)
 constexpr int kGoutLdsGltf = 0, kGoutLdsSky = 6;
 template <int P> constexpr bool kPairs8 = kPairs<P> && !kHasTex<P>;
-template <int P> constexpr int kGoutLdsOf = !(kPairs8<P> && !kTrail<P>) ? 6 : kIsGltf<P> ? kGoutLdsGltf
+template <int P> constexpr int kGoutLdsOf = !kPairs8<P> ? 6 : kIsGltf<P> ? kGoutLdsGltf
                                           : kScene<P> == PROG_SKYMESH ? kGoutLdsSky : 6;
 // BVH stack levels in LDS per lane (the rest in the global slab): the 8-wave variants fill 20 floats
 // per lane (160 KB per CU at 32 one-wave workgroups) with the G-buffer's LDS fields and the levels
 // (2 floats each); the 4-wave variants keep 7
 template <int P> constexpr int kStackLdsOf = kPairs8<P> ? (2 * kStackLdsPairs + 8 - kGoutLdsOf<P>) / 2 : kStackLds;
-// the restart-trail walk's LDS ring (entries per lane): the LDS of the stack walk's levels at 8
-// waves/SIMD (6 x 8 B + the 32-B G-buffer = 80 B per lane = 160 KB per CU); at 4 waves/SIMD the
-// textured variants have room for 14
-template <int P> constexpr int kRingOf = kHasTex<P> ? 14 : 6;
+// the restart-trail walk's LDS ring (entries per lane): at 8 waves/SIMD the 80 B per lane (160 KB per
+// CU) the stack walk's levels and G-buffer fields take (the glTF / HDRI scenes: 10 entries, the
+// G-buffer in memory as for the stack walk; the sky + mesh scene: 7); at 4 waves/SIMD the textured
+// variants have room for 14
+template <int P> constexpr int kRingOf = kHasTex<P> ? 14 : kPairs8<P> ? (2 * kStackLdsPairs + 8 - kGoutLdsOf<P>) / 2 : 6;
 // the stack walk's push form (pt_trace.h MegaStack::push): a scratch level and unmasked stores for
 // the textured 4-wave variants (1 % faster there), masked stores into one more real level where LDS
 // caps residency (the 8-wave variants: dragon stand-in +1.5 %, sky + dragon +2.2 %)
