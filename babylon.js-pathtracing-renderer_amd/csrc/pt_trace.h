@@ -102,21 +102,15 @@ PT_D void meshHit(const TraceArgs& a, float triID, float triU, float triV, Hit& 
 // js/GLTFModelPathTracing_FragmentShader.js:116-346 (glTF, with the BVH walk)
 template <int PROG, bool COUNT, int LS>
 PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* lds, unsigned lane_slot,
-                         unsigned deep, Cnt& cnt, bool shadow)
+                         unsigned deep, Cnt& cnt, bool firstHit)
 {
-    // A shadow ray (CalculateRadiance's sampleLight) ends its path at whatever it hits first: the
-    // light's colour is added when that is the light (glTF / Cornell), the environment's when it is
-    // nothing (HDRI / sky), and nothing else of the hit is read (shadeStep: `if (s.sampleLight) return
-    // false` comes before any use of the hit's normal, uv or material maps; the G-buffer is written at
-    // bounce 0, or at bounce 1 after METAL, which never samples the light). So for it the walk may stop
-    // at the first triangle closer than the analytic winner - the reference's walk, visiting the same
-    // nodes in the same order up to there, also ends with the mesh in front - and the hit needs no
-    // lookup: the mesh's type and colour are the same for every triangle. The counting variant keeps
-    // the reference's full closest-hit walk and lookup: it prices the reference's work. Only in the
-    // textured (4-wave) variants: helmet + HDRI -3.5 %; in the 8-wave ones the dragon stand-in and the
-    // sky composite gain nothing (few of their shadow rays are occluded by the mesh) and the bunny
-    // loses 1.3 % to the extra code (profiles/r04k_envmx_anyhit.txt).
-    const bool anyHit = !COUNT && kHasTex<PROG> && shadow;
+    // `firstHit`: of this segment's hit only "the light / nothing / something else" is read (bounceStep
+    // decides which segments). The walk may then stop at the first triangle closer than the analytic
+    // winner - the reference's walk, visiting the same nodes in the same order up to there, also ends
+    // with the mesh in front, as its hitT only falls - and the hit needs no lookup: the mesh's type and
+    // colour are the same for every triangle. The counting variant keeps the reference's full
+    // closest-hit walk and lookup: it prices the reference's work.
+    const bool anyHit = !COUNT && firstHit;
     if (COUNT) cnt.seg++;
     // the analytic winner's t, id and object-space normal; its other attributes are resolved after
     // the walk, and only if the mesh does not win (meshHit sets them all): fewer values live across
@@ -178,7 +172,16 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, fl
                      unsigned deep, Cnt& cnt)
 {
     Hit h;
-    sceneIntersect<PROG, COUNT, LS>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt, s.sampleLight);
+    // segments that read only whether their hit is the light, nothing, or something else:
+    //  * a shadow ray (the GLSL's sampleLight) ends its path at whatever it hits: `if (sampleLight)
+    //    return false` comes before any use of the hit's normal, uv or material maps, and the G-buffer
+    //    is written only at bounce 0, or at bounce 1 after METAL, which never samples the light;
+    //  * the sixth segment of a path whose mesh is DIFFUSE, METAL or glass without PBR maps: its
+    //    shading only updates state that ends with the path (mask, direction, counters) and, for glass,
+    //    the sharpness from the path's counters alone - a clear coat's depends on the Fresnel term of
+    //    the hit's normal, and a PBR hit reads its maps.
+    const bool lastOk = !a.uses_albedo && (a.model_mat == DIFFUSE || a.model_mat == METAL || a.model_mat == TRANSPARENT);
+    sceneIntersect<PROG, COUNT, LS>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt, s.sampleLight || (s.bounce == 5 && lastOk));
     return shadeStep<PROG, COUNT, G>(a, p, s, g, accum, h, cnt);
 }
 
