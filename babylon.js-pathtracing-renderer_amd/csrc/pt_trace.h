@@ -179,8 +179,11 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, fl
     //  * the sixth segment of a path whose mesh is DIFFUSE, METAL or glass without PBR maps: its
     //    shading only updates state that ends with the path (mask, direction, counters) and, for glass,
     //    the sharpness from the path's counters alone - a clear coat's depends on the Fresnel term of
-    //    the hit's normal, and a PBR hit reads its maps.
-    const bool lastOk = !a.uses_albedo && (a.model_mat == DIFFUSE || a.model_mat == METAL || a.model_mat == TRANSPARENT);
+    //    the hit's normal, and a PBR hit reads its maps. Not in the textured variants (their PBR meshes
+    //    never qualify, and the test alone costs the helmet 1 %).
+    // (profiles/r04k_envmx_anyhit.txt, r04q_envmx_anyhit_last.txt)
+    const bool lastOk = !kHasTex<PROG> && !a.uses_albedo &&
+                        (a.model_mat == DIFFUSE || a.model_mat == METAL || a.model_mat == TRANSPARENT);
     sceneIntersect<PROG, COUNT, LS>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt, s.sampleLight || (s.bounce == 5 && lastOk));
     return shadeStep<PROG, COUNT, G>(a, p, s, g, accum, h, cnt);
 }
