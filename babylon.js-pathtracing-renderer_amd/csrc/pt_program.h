@@ -52,9 +52,11 @@ struct Cnt {
 // [field][lane], which takes six live values out of the VGPR budget of the bounce loop, and the id and
 // sharpness as bits of the path's blue-noise register (free bits of a value that is live anyway)
 struct GOut {
+    static constexpr bool kColById = false;
     f3 nrm, col;
     float id, sharp;
     PT_D void clear() { nrm = mk(0, 0, 0); col = mk(0, 0, 0); id = 0.0f; sharp = 0.0f; }
+    PT_D void pinCol(f3) {}
     PT_D void setNrm(f3 v) { nrm = v; }
     PT_D void setCol(f3 v) { col = v; }
     PT_D void setId(float v) { id = v; }
@@ -71,8 +73,13 @@ typedef __attribute__((address_space(1))) float glb_float;
 // [field][lane of the grid] with `gs` lanes per field, so that a wave's store of one field is one
 // contiguous 256-B run: stored only by setNrm / setCol and read only when their bit says so - no
 // clearing store, no id / sharpness traffic at all.
+// With the colour wholly outside LDS (NF <= 3) it is not stored at all: objectColor is the bounce-0
+// hit's colour, and every object's hit colour is a constant of the object (objectMaterial), so the
+// end of the path recomputes it from the bounce-0 id - unless bounce 1 after METAL replaced the id,
+// when pinCol stores it first (bit 31 then says so).
 template <int LS, int NF = 6>
 struct GOutLds {
+    static constexpr bool kColById = NF <= 3;
     lds_float* p;
     unsigned slot;
     glb_float* gx;    // wave-uniform base ...
@@ -108,8 +115,15 @@ struct GOutLds {
     }
     PT_D void setCol(f3 v)
     {
+        if (kColById) return;
         put(3, v.x); put(4, v.y); put(5, v.z);
         if (NF < 6) *bn |= 1u << 31;
+    }
+    PT_D void pinCol(f3 v)
+    {
+        if (!kColById) return;
+        put(3, v.x); put(4, v.y); put(5, v.z);
+        *bn |= 1u << 31;
     }
     PT_D void setId(float v) { *bn = (*bn & ~(31u << 26)) | (((unsigned)(int)v & 31u) << 26); }
     PT_D void setSharp(float v)
@@ -123,10 +137,15 @@ struct GOutLds {
         return code == 1u ? 1.01f : code == 2u ? -1.0f : 0.0f;
     }
     PT_D float id() const { return (float)((*bn >> 26) & 31u); }
-    PT_D GOut load() const
+    // colOfId(id): the hit colour of object `id` (kColById)
+    template <class F>
+    PT_D GOut load(F colOfId) const
     {
         GOut g;
-        g.nrm = mk(get(0), get(1), get(2)); g.col = mk(get(3), get(4), get(5)); g.id = id(); g.sharp = sharp();
+        g.nrm = mk(get(0), get(1), get(2)); g.id = id(); g.sharp = sharp();
+        if (!kColById) g.col = mk(get(3), get(4), get(5));
+        else if (!((*bn >> 23) & 1u)) g.col = mk(0.0f, 0.0f, 0.0f);   // no bounce-0 hit: the pinned zeros
+        else g.col = ((*bn >> 31) & 1u) ? mk(get(3), get(4), get(5)) : colOfId(g.id);
         return g;
     }
 };
@@ -328,7 +347,15 @@ PT_D bool shadeStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, Hit
     f3 nl = dot(n, p.rd) < 0.0f ? normalize(n) : normalize(-n);
     f3 x = p.ro + p.rd * h.t;
     if (bounces == 0) { g.setNrm(nl); g.setCol(h.color); g.setId((float)h.id); }
-    if (bounces == 1 && prevType == METAL) { g.setNrm(nl); g.setId((float)h.id); }
+    if (bounces == 1 && prevType == METAL) {
+        if constexpr (G::kColById) {   // objectColor stays bounce 0's: keep it before the id changes
+            f3 c0 = mk(0.0f, 0.0f, 0.0f);
+            int t0;
+            objectMaterial<PROG>(a, (int)g.id(), c0, t0);
+            g.pinCol(c0);
+        }
+        g.setNrm(nl); g.setId((float)h.id);
+    }
 
     if (!sky && !hdri && hitType == LIGHT) {   // (commented out / removed in the sky and HDRI shaders)
         if (s.diffuseCount == 0) g.setSharp(1.01f);

@@ -341,7 +341,12 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
         r = radiance<PROG, COUNT, kTraceBlock>(a, p, gl, lds_stack, tid, deep, cnt);
     }
     PT_SEC(cnt, 4);
-    const GOut g = gl.load();
+    const GOut g = gl.load([&](float id) {
+        f3 c = mk(0.0f, 0.0f, 0.0f);
+        int t;
+        objectMaterial<PROG>(a, (int)id, c, t);
+        return c;
+    });
 
     // ---- 2x2 fine derivatives (js/PathTracingCommon.js:1306-1320): partner lanes ^1 (x) and ^2 (y)
     const bool xodd = lane & 1, yodd = lane & 2;

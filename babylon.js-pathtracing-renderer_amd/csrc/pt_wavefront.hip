@@ -281,10 +281,12 @@ __global__ __launch_bounds__(kBlock, 4) void wf_bvh(TraceArgs a, WfBufs w, int b
 // ============================================================================ shade (one loop iteration)
 // CalculateRadiance's G-buffer outputs go straight to the pixel's gb0 / gb1 records
 struct GOutPix {
+    static constexpr bool kColById = false;
     float4* gb0;
     float4* gb1;
     unsigned pix;
     PT_D void clear() {}
+    PT_D void pinCol(f3) {}
     PT_D void setNrm(f3 v) { gb0[pix].x = v.x; gb0[pix].y = v.y; gb0[pix].z = v.z; }
     PT_D void setCol(f3 v) { gb1[pix].x = v.x; gb1[pix].y = v.y; gb1[pix].z = v.z; }
     PT_D void setId(float v) { gb0[pix].w = v; }
