@@ -213,13 +213,6 @@ PT_D f3 skyColor(const SkyArgs& k, f3 rayDir)
 template <int PROG>
 PT_D int meshObjectId(const TraceArgs& a) { return kQuadId0<PROG> + a.nquads; }
 
-// a wave-uniform kernel argument as a scalar register value: selecting between two of these per lane
-// is a v_cndmask, where a select between two kernarg loads becomes one vector load of the selected
-// address (objectMaterial, analyticAttributes)
-PT_D float sreg(float x) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x))); }
-PT_D int sreg(int x) { return __builtin_amdgcn_readfirstlane(x); }
-PT_D f3 sreg(f3 v) { return mk(sreg(v.x), sreg(v.y), sreg(v.z)); }
-
 // hitColor / hitType of analytic object `id` (the values SceneIntersect writes with it)
 template <int PROG>
 PT_D void objectMaterial(const TraceArgs& a, int id, f3& color, int& type)
@@ -232,19 +225,11 @@ PT_D void objectMaterial(const TraceArgs& a, int id, f3& color, int& type)
         const float cb[12] = { 0.0f, 0.0f, 0.0f, 1.0f, 0.0f, 0.0f, 1.0f, 1.0f, 1.0f, 0.5f, 0.0f, 1.0f };
         color = mk(cr[id], cg[id], cb[id]);
         type = a.shape_mat;
-    }
-    // the spheres' and quads' attributes are wave-uniform kernel arguments: read with scalar loads and
-    // selected per lane (indexed by the lane's id they would be vector loads from the kernarg segment,
-    // one memory round trip per segment); the id ranges are disjoint, as in the GLSL's if-chain
-    if (!kIsQuadric<PROG>) {
-#pragma unroll
-        for (int s = 0; s < 2; s++)
-            if (id == s) { color = sreg(a.sph[s].color); type = sreg(a.sph[s].type); }
-    }
-#pragma unroll
-    for (int i = 0; i < 6; i++)
-        if (i < a.nquads && id == q0 + i) { color = sreg(a.qcolor[i]); type = sreg(a.qtype[i]); }
-    if (kHasMesh<PROG> && id == meshObjectId<PROG>(a)) {
+    } else if (!kIsQuadric<PROG> && id >= 0 && id < 2) {
+        color = a.sph[id].color; type = a.sph[id].type;
+    } else if (id >= q0 && id < q0 + a.nquads) {
+        color = a.qcolor[id - q0]; type = a.qtype[id - q0];
+    } else if (kHasMesh<PROG> && id == meshObjectId<PROG>(a)) {
         color = mk(1.0f, 1.0f, 1.0f); type = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
     }
 }
@@ -296,21 +281,12 @@ PT_D void analyticAttributes(const TraceArgs& a, Hit& h, f3 sn)
 {
     constexpr int q0 = kQuadId0<PROG>;
     if (h.id >= 0 && h.id < q0) {
+        const m4& M = kIsQuadric<PROG> ? a.shape_inv[h.id] : a.sph[h.id].inv;
         // disk and rectangle: hitNormal = vec3(0,-1,0), not normalized before the transform
         const f3 n0 = (kIsQuadric<PROG> && (h.id == 9 || h.id == 10)) ? mk(0.0f, -1.0f, 0.0f) : normalize(sn);
-        if (kIsQuadric<PROG>) h.normal = normalize(mul3t(a.shape_inv[h.id], n0));
-        else {   // the two spheres' transforms selected per lane from scalar loads (objectMaterial)
-            m4 M;
-#pragma unroll
-            for (int k = 0; k < 16; k++) M.m[k] = h.id == 1 ? sreg(a.sph[1].inv.m[k]) : sreg(a.sph[0].inv.m[k]);
-            h.normal = normalize(mul3t(M, n0));
-        }
+        h.normal = normalize(mul3t(M, n0));
     } else if (h.id >= q0) {
-        f3 qn = mk(0.0f, 0.0f, 0.0f);
-#pragma unroll
-        for (int i = 0; i < 6; i++)
-            if (i < a.nquads && h.id == q0 + i) qn = sreg(a.qnormal[i]);
-        h.normal = normalize(qn);
+        h.normal = normalize(a.qnormal[h.id - q0]);
     }
     if (h.id >= 0) objectMaterial<PROG>(a, h.id, h.color, h.type);
 }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# One evidence session for a tree: the GPU parity suite, the driver's exact bench command, bench.py on
+# One evidence session for a tree: smoke(), the GPU parity suite, the driver's exact bench command, bench.py on
 # every workload, a rocprofv3 kernel trace + stats of the default bench, and the PMC passes of the
 # dragon stand-in (tools/gpu_pmc.sh groups). Every GPU step has its own time limit; anything but
 # pytest's 0 ends the session. usage: gpu_evidence.sh TAG
@@ -7,6 +7,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 R=$GRAFT_REPO_ROOT
 TAG=${1:-r04}
 mkdir -p gpurun_out
+timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
 timeout -k 10 600 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/pytest_$TAG.log
 if [ $rc -ne 0 ]; then exit $rc; fi
