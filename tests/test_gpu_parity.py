@@ -620,6 +620,39 @@ def test_sky_mesh_bitexact_and_counters(engine, backend, material):
     assert sum(c["hit_lookups"] for c in ref_cnt) > 0
 
 
+def _with_material(meta, material):
+    """A recorded glTF stream with the model's material switched (uModelMaterialType)."""
+    frames = []
+    for f in meta["frames"]:
+        fr = []
+        for c in f:
+            if c["shader"] == "pathTracingFragmentShader":
+                c = dict(c, uniforms=dict(c["uniforms"], uModelMaterialType=["i", [material]]))
+            fr.append(c)
+        frames.append(fr)
+    return dict(meta, frames=frames)
+
+
+@pytest.mark.parametrize("scene", ["gltf_teapot", "sky_dragon"])
+@pytest.mark.parametrize("material", [1, 2, 4])
+def test_mesh_materials_any_hit_bitexact(engine, backend, scene, material):
+    """The production kernels (no counting) under the mesh materials the recorded streams do not
+    carry - Diffuse, Transparent (double-sided leaves), ClearCoat_Diffuse: shadow rays and the sixth
+    segment of Diffuse / glass paths end their walk at the first occluder and skip the hit lookup
+    (pt_trace.h bounceStep), which must leave every accumulation and canvas bit as the oracle's
+    full closest-hit walk has it (the counting variant, used by the tests that compare counters,
+    keeps the full walk)."""
+    if scene == "gltf_teapot":
+        meta, mesh, W, Hh = _with_material(H.stream("gltf_teapot_320x180"), material), None, 320, 180
+    else:
+        meta, mesh, W, Hh = H.sky_mesh_stream(material), _dragon(), 160, 90
+    ref_acc, ref_can, _ = H.oracle_replay(meta, None, width=W, height=Hh, with_output=True, mesh=mesh)
+    got_acc, got_can, _ = _replay_gpu(engine, meta, None, W, Hh, mesh=mesh)
+    for i, (ra, ga, rc, gc) in enumerate(zip(ref_acc, got_acc, ref_can, got_can)):
+        assert _bits_equal(ra, ga), "frame %d accumulation: %s" % (i, _diff_report(ra, ga))
+        assert _bits_equal(rc, gc), "frame %d canvas: %s" % (i, _diff_report(rc, gc))
+
+
 def test_sky_mesh_effect_from_shader_text(engine):
     """The composite is recognised from its fragment source: the sky shader text with the glTF
     model's samplers declared -> PT_PROG_SKY_MESH; the sky shader alone stays PT_PROG_SKY."""
