@@ -166,11 +166,6 @@ PT_D void sceneIntersect(const TraceArgs& a, f3 rayO, f3 rayD, Hit& h, float2* l
     PT_SEC(cnt, 3);
 }
 
-// the G-buffer's sharpness as the path holds it so far
-PT_D float sharpOf(const GOut& g) { return g.sharp; }
-template <int LS, int NF>
-PT_D float sharpOf(const GOutLds<LS, NF>& g) { return g.sharp(); }
-
 // One iteration of CalculateRadiance's loop: SceneIntersect, then the shading step
 template <int PROG, bool COUNT, int LS, class G>
 PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, float2* lds, unsigned lane_slot,
@@ -184,16 +179,11 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, fl
     //  * the sixth segment of a path whose mesh is DIFFUSE, METAL or glass without PBR maps: its
     //    shading only updates state that ends with the path (mask, direction, counters) and, for glass,
     //    the sharpness from the path's counters alone - a clear coat's depends on the Fresnel term of
-    //    the hit's normal, and a PBR hit reads its maps;
-    //  * in the textured variants also the sixth segment of a path past its first diffuse bounce
-    //    whose sharpness is already 0, whatever the mesh: a PBR hit's emission counts only while the
-    //    path is specular, its maps then choose DIFFUSE / CLEARCOAT / METAL, and of those only a clear
-    //    coat touches the G-buffer - setting the sharpness to 0, which it already is (the coat's other
-    //    sharpness write needs diffuseCount == 0).
-    // (profiles/r04k_envmx_anyhit.txt, r04q_envmx_anyhit_last.txt, r04y_envmx_anyhit_pbr.txt)
-    const bool lastOk = kHasTex<PROG>
-        ? !s.specular && s.diffuseCount >= 1 && sharpOf(g) == 0.0f
-        : !a.uses_albedo && (a.model_mat == DIFFUSE || a.model_mat == METAL || a.model_mat == TRANSPARENT);
+    //    the hit's normal, and a PBR hit reads its maps. Not in the textured variants (their PBR meshes
+    //    never qualify, and the test alone costs the helmet 1 %).
+    // (profiles/r04k_envmx_anyhit.txt, r04q_envmx_anyhit_last.txt)
+    const bool lastOk = !kHasTex<PROG> && !a.uses_albedo &&
+                        (a.model_mat == DIFFUSE || a.model_mat == METAL || a.model_mat == TRANSPARENT);
     sceneIntersect<PROG, COUNT, LS>(a, p.ro, p.rd, h, lds, lane_slot, deep, cnt, s.sampleLight || (s.bounce == 5 && lastOk));
     return shadeStep<PROG, COUNT, G>(a, p, s, g, accum, h, cnt);
 }
