@@ -670,7 +670,10 @@ def main():
                                    "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 B per launch (gfx950 correction)")
                 if traffic else pmc_note,
                 "kernel": kernel, "bvh_walk": layout, "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                "counts_per_launch": {k: v / nc for k, v in cnt.items()}}
+                "counts_per_launch": {k: v / nc for k, v in cnt.items()},
+                "pricing": ("the reference's work (counting variant: full closest-hit walks and hit lookups); the "
+                            "timed kernel ends shadow rays and eligible last segments at their first occluder "
+                            "(same image bits, DESIGN.md §6), so 'achieved' is reference work per second")}
     ms_per_step = elapsed / args.steps * 1e3
     ksum = sum(kernel_ms.values())
     line = {
