@@ -111,7 +111,7 @@ struct GOutLds {
     PT_D void setNrm(f3 v)
     {
         put(0, v.x); put(1, v.y); put(2, v.z);
-        if (NF < 3) *bn |= 1u << 23;
+        if (NF < 3 || kColById) *bn |= 1u << 23;   // (kColById: also "bounce 0 hit something" for load)
     }
     PT_D void setCol(f3 v)
     {
