@@ -67,12 +67,12 @@ __host__ __device__ inline int resolveProgram(int prog, bool textured, int walk)
 constexpr int kMinWavesTex = 4, kMinWavesPairs = 8, kMinWavesRef = 4;
 template <int P> constexpr int kMinWaves = kHasTex<P> ? kMinWavesTex : kPairs<P> ? kMinWavesPairs : kMinWavesRef;
 // G-buffer fields in LDS (pt_program.h GOutLds: the normal and colour; the id and sharpness ride in a
-// register): the glTF / HDRI scenes' 8-wave child-pair stack walk keeps none of them there (they are
-// stored once per path to memory and read once) and has two LDS stack levels more in their place
-// (10: dragon stand-in -1.6 %, bunny x16 -1.4 % against 8 levels with 4 fields in LDS; 9 with 2 fields
-// in between; profiles/r04e_envmx_gbuffer_levels.txt); the sky + mesh scene, whose shading writes them
-// more often, keeps all 6 (its 10-level form measured +1 %)
-constexpr int kGoutLdsGltf = 0, kGoutLdsSky = 6;
+// register): the 8-wave child-pair walks keep none of them there - the normal is stored once per path
+// to memory and read once, the colour is recomputed from the bounce-0 object id - and have two LDS
+// stack levels more in their place (10: dragon stand-in -1.6 %, bunny x16 -1.4 % against 8 levels with 4
+// fields in LDS, profiles/r04e_envmx_gbuffer_levels.txt; sky + dragon 4K -2.7 % against all 6 fields
+// and 7 levels, -2.1 % for the normal in LDS and 8 levels, profiles/r04aa_envmx_sky_gbuffer.txt)
+constexpr int kGoutLdsGltf = 0, kGoutLdsSky = 0;
 template <int P> constexpr bool kPairs8 = kPairs<P> && !kHasTex<P>;
 template <int P> constexpr int kGoutLdsOf = !kPairs8<P> ? 6 : kIsGltf<P> ? kGoutLdsGltf
                                           : kScene<P> == PROG_SKYMESH ? kGoutLdsSky : 6;
