@@ -11,7 +11,7 @@ old = """    int diffuseCount, hitType, bounce;
 new = """    // the counters and flags packed into one register (bit-fields): diffuseCount <= 6, bounce <= 6,
     // hitType in [-100, 10]
     int diffuseCount : 4, hitType : 8, bounce : 4;
-    unsigned coat : 1, specular : 1, sampleLight : 1;
+    bool coat : 1, specular : 1, sampleLight : 1;
 };"""
 assert old in s
 s = s.replace(old, new, 1)
