@@ -10,7 +10,7 @@ namespace pt {
 
 constexpr int kBlock = 256;          // 4 waves; a block shades a 16x16 pixel tile
 constexpr int kTile = 16;            // tile edge == row-band height used for sharding
-constexpr int kWaveLogSlots = 12;   // experiment builds (PT_SECPROF): u64 per workgroup in TraceArgs::wave_log
+constexpr int kWaveLogSlots = 13;   // experiment builds (PT_SECPROF): u64 per workgroup in TraceArgs::wave_log
 // split tiles (pt_trace, longest-first): each 8x8 quadrant of a split 16x16 tile is shaded by this
 // many waves of 64 / kSplitParts lanes (4x4-pixel waves of 16 lanes; one 2x2 quad per wave measured
 // slower)

@@ -81,9 +81,9 @@ template <int P> constexpr int kGoutLdsOf = !kPairs8<P> ? 6 : kIsGltf<P> ? kGout
 // (2 floats each); the 4-wave variants keep 7
 template <int P> constexpr int kStackLdsOf = kPairs8<P> ? (2 * kStackLdsPairs + 8 - kGoutLdsOf<P>) / 2 : kStackLds;
 // the restart-trail walk's LDS ring (entries per lane): at 8 waves/SIMD the 80 B per lane (160 KB per
-// CU) the stack walk's levels and G-buffer fields take (the glTF / HDRI scenes: 10 entries, the
-// G-buffer in memory as for the stack walk; the sky + mesh scene: 7); at 4 waves/SIMD the textured
-// variants have room for 14
+// CU) the stack walk's levels take - 10 entries for every 8-wave mesh scene (glTF, HDRI, sky + mesh),
+// whose G-buffer lives in memory (the normal in the spill slab, the colour recomputed) for the trail
+// walk as for the stack walk; at 4 waves/SIMD the textured variants have room for 14
 template <int P> constexpr int kRingOf = kHasTex<P> ? 14 : kPairs8<P> ? (2 * kStackLdsPairs + 8 - kGoutLdsOf<P>) / 2 : 6;
 // the stack walk's push form (pt_trace.h MegaStack::push): a scratch level and unmasked stores for
 // the textured 4-wave variants (1 % faster there), masked stores into one more real level where LDS

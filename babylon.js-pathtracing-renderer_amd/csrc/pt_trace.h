@@ -376,6 +376,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
             wl[2] = lds_sec[10];
             wl[3] = lds_sec[11];
             for (int k = 0; k < 8; k++) wl[4 + k] = lds_sec[k];   // section cycle sums (shader clock)
+            wl[12] = __smid();   // the CU that ran the wave (XCC, SE, CU id bits): CU occupancy over time
         }
     }
     if (COUNT && active) {   // stack traffic: pops beyond the LDS levels, pushes beyond; node fetches, leaf tests

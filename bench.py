@@ -244,7 +244,9 @@ def plan(args, world):
     fixed = world > 1 and (args.scaling == "strong" or args.size is not None or args.workload == "sky_dragon")
     return {"width": W, "height": Hh, "scaling": None if world == 1 else "strong" if fixed else "weak",
             "event_every": args.event_every or max(1, args.steps // 10),
-            "parity_frames": PARITY_FRAMES if world > 1 and not getattr(args, "no_check", False) else 0}
+            # --no-output renders no canvas and gathers nothing: there is no N-GPU frame to compare
+            "parity_frames": (PARITY_FRAMES if world > 1 and not getattr(args, "no_check", False)
+                              and not getattr(args, "no_output", False) else 0)}
 
 
 # ------------------------------------------------------------------------------ N-GPU parity check
@@ -730,6 +732,8 @@ def main():
 if __name__ == "__main__":
     try:
         rc = main()
+    except SystemExit:      # argparse's --help and usage errors exit as they always do
+        raise
     except BaseException:   # noqa: BLE001 - any failure of a rank ends it at once, non-zero
         import traceback
         traceback.print_exc()

@@ -172,7 +172,10 @@ int pt_set_backend(pt_ctx* ctx, int backend);
  * links are not exact in-range integers keeps PT_BVH_REFERENCE, the walk over the reference's own
  * texel pairs. Same nodes, same order, same results every way
  * (js/GLTFModelPathTracing_FragmentShader.js:211-298). Other values: PT_ERR_ARG.
- * pt_bvh_layout_used reports what the last glTF draw of the context walked (-1: none yet). */
+ * pt_bvh_layout_used reports what the last glTF draw of the context walked (-1: none yet).
+ * API change (round 4): the two-level layout PT_BVH_QUADS (3) was removed - it was slower on every
+ * workload; pt_set_bvh_layout(ctx, 3) now returns PT_ERR_ARG and the Python
+ * set_bvh_layout("quads") raises KeyError. */
 enum pt_bvh_layout { PT_BVH_REFERENCE = 0, PT_BVH_PAIRS = 1, PT_BVH_TRAIL = 2 };
 int pt_set_bvh_layout(pt_ctx* ctx, int layout);
 int pt_bvh_layout_used(pt_ctx* ctx);

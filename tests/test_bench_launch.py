@@ -58,7 +58,7 @@ def _plan(argv, world):
     ap = argparse.ArgumentParser()
     for a, kw in (("--size", {}), ("--workload", {"default": "dragon"}), ("--scaling", {"default": "strong"}),
                   ("--steps", {"type": int, "default": 200}), ("--event-every", {"type": int, "default": None}),
-                  ("--no-check", {"action": "store_true"})):
+                  ("--no-check", {"action": "store_true"}), ("--no-output", {"action": "store_true"})):
         ap.add_argument(a, **kw)
     return bench.plan(ap.parse_args(argv), world)
 
@@ -78,6 +78,8 @@ def test_plan_headline_and_scaling_configs():
     assert (_plan(["--size", "640x480"], 2)["width"], _plan(["--size", "640x480"], 2)["scaling"]) == (640, "strong")
     assert (_plan(["--workload", "sky_dragon"], 1)["width"], _plan(["--workload", "sky_dragon"], 1)["height"]) == (3840, 2160)
     assert _plan(["--no-check"], 8)["parity_frames"] == 0
+    assert _plan(["--no-output"], 8)["parity_frames"] == 0   # no canvas gathered: nothing to compare
+    assert _plan([], 8)["parity_frames"] > 0
 
 
 def test_compare_frames_reports_bitwise_equality():

@@ -293,6 +293,31 @@ def test_dragon_standin_1080p_bitexact_and_counters(engine, backend):
     assert cnt == {k: sum(c[k] for c in ref_cnt) for k in ref_cnt[0]}
 
 
+@pytest.mark.parametrize("layout", ["pairs", "trail"])
+@pytest.mark.parametrize("workload", ["bunny", "dragon"])
+def test_timed_kernel_1080p_bitexact(engine, workload, layout):
+    """The kernels the bench times, at the configurations it times them on: the production
+    (non-counting) megakernel - any-hit shadow rays and last segments, longest-first order and split
+    tiles from the second frame on - over whole 1920x1080 frames of StanfordBunny (BASELINE
+    configs[1]) and the dragon stand-in (the headline), all four recorded frames (the first clears
+    the history, the rest blend), accumulation and canvas bit-exact with the oracle."""
+    meta = H.stream("gltf_bunny_1080p")
+    mesh = H.synthetic_dragon() if workload == "dragon" else H.mesh(meta)
+    ref_acc, ref_can, _ = H.oracle_replay(meta, None, with_output=True, mesh=mesh)
+    engine.set_backend("megakernel")
+    engine.set_bvh_layout(layout)
+    engine.set_counting(False)
+    try:
+        got_acc, got_can, _ = _replay_gpu(engine, meta, None, mesh=mesh)
+        assert engine.bvh_layout_used() == layout
+    finally:
+        engine.set_bvh_layout("pairs")
+    assert len(got_acc) == len(meta["frames"]) == 4
+    for i, (ra, ga, rc, gc) in enumerate(zip(ref_acc, got_acc, ref_can, got_can)):
+        assert _bits_equal(ra, ga), "%s frame %d: %s" % (workload, i, _diff_report(ra, ga))
+        assert _bits_equal(rc, gc), "%s frame %d canvas: %s" % (workload, i, _diff_report(rc, gc))
+
+
 @pytest.mark.parametrize("key", ["bookcase", "twoparts"])
 def test_reference_multimesh_models_bitexact(engine, backend, key):
     """The reference's two other models (150 / 5 merged meshes, mixed vertex-attribute sets, so

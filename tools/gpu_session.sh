@@ -1,0 +1,77 @@
+#!/bin/bash
+# One GPU session (run through gpurun): a list of steps, each under its own time limit; the first
+# failing step ends the session (no GPU step after a fault, abort, or time limit). Every step's
+# output lands in gpurun_out/<TAG>_<n>_<step>.log; the session log lists the steps and their exit codes.
+#
+# usage: tools/gpu_session.sh TAG STEP [STEP ...]
+#   smoke                      __graft_entry__.smoke()
+#   pytest[:K]                 the GPU parity suite (pytest -m gpu), or only the tests matching -k K
+#   exact                      the driver's exact bench command (bench.py --gpus 1 --steps 20 --warmup 5)
+#   bench:W[:ARGS]             bench.py --workload W (ARGS: extra bench flags, commas for spaces)
+#   envmx:ROUNDS:WLS:ENVS      path-tracing kernel ms per workload under environment settings, alternating
+#                              rounds (WLS comma-separated; ENVS '|'-separated, each space-free K=V[,K=V] or -)
+#   frames:ROUNDS:WLS:ENVS     the same for whole frames (bench.py --no-pmc --cpu-budget 0 per setting)
+#   wavetime:LIB:WLS           wave timeline + CU occupancy of a -DPT_SECPROF build (tools/wavetime.py)
+#   prof                       rocprofv3 --kernel-trace --stats of the default bench
+#   pmc[:W]                    the five PMC passes over tools/prof_frames.py (default workload dragon)
+cd "$GRAFT_REPO_ROOT" || exit 1
+R=$GRAFT_REPO_ROOT
+TAG=$1; shift
+mkdir -p gpurun_out
+SLOG=gpurun_out/${TAG}_session.log
+: > "$SLOG"
+n=0
+run() {   # run LIMIT LOG CMD...  (the step's own time limit)
+  local lim=$1 log=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$log" 2>&1
+}
+for step in "$@"; do
+  n=$((n + 1))
+  IFS=':' read -r kind a1 a2 a3 <<< "$step"
+  LOG="gpurun_out/${TAG}_${n}_${kind}.log"
+  echo "step $n: $step" >> "$SLOG"
+  case $kind in
+    smoke) run 300 "$LOG" python -u -c 'import __graft_entry__ as g; g.smoke()' ;;
+    pytest)
+      if [ -n "$a1" ]; then run 900 "$LOG" python -u -m pytest tests -m gpu -q -rf -x --timeout 300 --timeout-method thread -k "$a1"
+      else run 900 "$LOG" python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread; fi ;;
+    exact) run 300 "$LOG" python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    bench) run 400 "$LOG" python3 bench.py --workload "$a1" ${a2//,/ } ;;
+    envmx|frames)
+      : > "$LOG"; rc=0
+      for r in $(seq "$a1"); do
+        IFS='|' read -ra ENVS <<< "$a3"
+        for cfg in "${ENVS[@]}"; do
+          for w in ${a2//,/ }; do
+            envs=""; [ "$cfg" != "-" ] && envs="${cfg//,/ }"
+            if [ $kind = envmx ]; then
+              res=$(env $envs timeout -k 10 120 python tools/exp_timing.py --workload "$w" --frames 30 --backends megakernel --layouts pairs --no-mesh-variant 2>&1 | tail -1); rc=$?
+            else
+              res=$(env $envs timeout -k 10 200 python3 bench.py --workload "$w" --no-pmc --cpu-budget 0 --no-check 2>&1 | tail -1); rc=$?
+            fi
+            echo "r$r [$cfg] $w $res" >> "$LOG"
+            [ $rc -ne 0 ] && break 3
+          done
+        done
+      done
+      (exit $rc) ;;
+    wavetime) mkdir -p "gpurun_out/wt_$TAG"; PT_LIBPT=$a1 run 300 "$LOG" python3 tools/wavetime.py "gpurun_out/wt_$TAG" ${a2//,/ } ;;
+    prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$R/gpurun_out/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 50 --warmup 5 --cpu-budget 0 --no-pmc --no-anchors) > "$LOG" 2>&1 ;;
+    pmc)
+      W=${a1:-dragon}; OUT="$R/gpurun_out/pmc_$TAG"; mkdir -p "$OUT"; i=0; rc=0
+      for C in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES" \
+               "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH"; do
+        i=$((i + 1))
+        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $C --output-format csv -d "$OUT/p$i" -o run \
+          -- python3 "$R/tools/prof_frames.py" --workload "$W" --frames 10) > "$OUT/p$i.log" 2>&1 || { rc=$?; break; }
+      done
+      (exit $rc) ;;
+    *) echo "unknown step $step" >> "$SLOG"; exit 2 ;;
+  esac
+  rc=$?
+  echo "step $n rc=$rc" >> "$SLOG"
+  if [ $rc -ne 0 ]; then tail -30 "$LOG"; exit $rc; fi
+done
+echo "session $TAG done" >> "$SLOG"

@@ -53,6 +53,22 @@ CHECKPOINTS = (1, 64, 1024)
 REROUTE_REL = 1e-3
 
 
+def toolchain():
+    """What the fma / libm / gpu builds' bits depend on besides the source: the C compiler (how
+    -ffp-contract=fast fuses), the C library (its expf / sinf / atan2f / powf ...) and the ISA (-mfma)."""
+    import platform
+    import subprocess
+    try:
+        gcc = subprocess.run(["gcc", "-dumpfullversion"], capture_output=True, text=True, timeout=30).stdout.strip()
+    except (OSError, subprocess.SubprocessError):
+        gcc = None
+    try:
+        libc = os.confstr("CS_GNU_LIBC_VERSION")
+    except (ValueError, OSError):
+        libc = None
+    return {"gcc": gcc, "libc": libc, "machine": platform.machine()}
+
+
 def frame_uniforms(meta, k, W, Hh, seed=12345):
     """Frame k (1-based) of a still-camera progressive run from a cleared history: the last recorded
     frame's uniforms with uFrameCounter = uSampleCounter = k and a fresh uRandomVec2."""
@@ -131,7 +147,7 @@ def main():
     a = ap.parse_args()
     names = a.names or list(CASES)
     report = {"frames": a.frames, "checkpoints": [k for k in CHECKPOINTS if k <= a.frames],
-              "reroute_rel": REROUTE_REL, "variants": a.variants.split(","), "cases": {}}
+              "reroute_rel": REROUTE_REL, "variants": a.variants.split(","), "toolchain": toolchain(), "cases": {}}
     if os.path.exists(a.out) and a.names:
         with open(a.out) as f:
             report["cases"] = json.load(f).get("cases", {})

@@ -42,8 +42,8 @@ if only_notex:
     s = s.replace("template <class Stk>\nPT_D void bvhWalkPairs(", "template <bool kScalarWalk = false, class Stk>\nPT_D void bvhWalkPairs(", 1)
     t = os.path.join(d, "pt_trace.h")
     ts = open(t).read()
-    o2 = "else bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br);"
+    o2 = "else bvhWalkPairs(a, O, D, inv, dbl, rootT, h.t, st, br, anyHit);"
     assert o2 in ts
-    ts = ts.replace(o2, "else bvhWalkPairs<!kHasTex<PROG>>(a, O, D, inv, dbl, rootT, h.t, st, br);")
+    ts = ts.replace(o2, "else bvhWalkPairs<!kHasTex<PROG>>(a, O, D, inv, dbl, rootT, h.t, st, br, anyHit);")
     open(t, "w").write(ts)
 open(p, "w").write(s)
