@@ -119,8 +119,13 @@ struct TraceArgs {
     // glTF material switches (js/GLTFModelPathTracing_FragmentShader.js:21-25)
     int model_mat, uses_albedo, uses_bump, uses_metal, uses_emissive;
     // samplers
-    const float4* prev;
-    float4* out;
+    const float4* prev;     // the wavefront / persistent schedules' finish pass: history in,
+    float4* out;            // accumulation out
+    // the megakernel: per pixel (py * width + px) CalculateRadiance()'s result and the pre-history
+    // alpha flag (0, 1.01 or -1: the G-buffer sharpness and the 2x2 edge test); pt_blend folds in the
+    // history (js/PathTracingCommon.js:1326-1357), so the kernel never reads it and consecutive frames'
+    // path tracing may overlap
+    float4* rad;
     Tex8 bluenoise;
     const float4* aabb;
     long long aabb_texels;
@@ -200,6 +205,19 @@ struct OutputArgs {
     unsigned* ob_split;
     unsigned ob_ntiles, ob_cap, ob_dominance;
     int ob_near;
+};
+
+// pt_blend: the progressive accumulation of a megakernel draw (js/PathTracingCommon.js:1326-1357) over
+// the owned 16-row bands: out = history (x 0.5 when the camera moved, 0 at frame 1) + radiance, alpha
+// from the radiance's pre-history flag and the history's
+struct BlendArgs {
+    int width, height;
+    int num_parts, part;
+    float frame;
+    int moving;
+    const float4* rad;
+    const float4* prev;
+    float4* out;
 };
 
 struct CopyArgs {

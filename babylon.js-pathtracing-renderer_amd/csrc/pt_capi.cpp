@@ -33,6 +33,7 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
 hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,
                                  unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s);
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
+hipError_t pt_launch_blend(const pt::BlendArgs* a, int bands, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
 hipError_t pt_launch_persist(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x,
@@ -48,6 +49,12 @@ hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, 
                                 unsigned* parent, unsigned* refs, unsigned* flag, const float4* rec, uint32_t root,
                                 float4* top, hipStream_t s);
 }
+
+#ifdef PT_SECPROF
+#define PT_SECPROF_BUILD true
+#else
+#define PT_SECPROF_BUILD false
+#endif
 
 namespace {
 
@@ -118,8 +125,23 @@ struct Dev {
     pt::WfBufs wf = {};
     void* wf_mem = nullptr;
     size_t wf_pixels = 0, wf_slots = 0, wf_spill = 0;
-    float2* mk_spill = nullptr;   // megakernel BVH stack spill slab
+    float2* mk_spill = nullptr;   // megakernel BVH stack spill slabs (two: one per draw parity)
     size_t mk_spill_lanes = 0;
+    // Frame overlap (megakernel draws; PT_OVERLAP=0 turns it off). pt_trace never reads the history:
+    // it writes radiance + the pre-history flag to rad[parity], and pt_blend folds in the history on
+    // the main stream. So draw k's path tracing runs on side stream ts[k & 1] and waits only for the
+    // main stream's state when draw k - 1 began (mark[(k - 1) & 1]: draw k - 2's blend, its order build,
+    // the output that read rad / the order), never for draw k - 1's kernel: consecutive frames' path
+    // tracing overlap, and the next frame's waves fill the launch tail of this one. Per parity: the
+    // radiance buffer, the spill slab and the longest-first cost / order / split (each parity is its own
+    // longest-first pipeline, draw k ordered by draw k - 2's costs).
+    bool overlap = true;
+    hipStream_t ts[2] = {};
+    hipEvent_t ev_mark[2] = {}, ev_traced[2] = {};
+    unsigned mk_seq = 0;          // megakernel draws so far (parity = mk_seq & 1)
+    bool mark_valid = false;      // mark[(mk_seq - 1) & 1] may gate the next draw (else it waits for a fresh mark)
+    float4* rad_mem = nullptr;    // rad[2]: radiance + flag per pixel
+    size_t rad_pixels = 0;
     pt::WfBufs gb = {};           // persistent backend: per-pixel G-buffer + radiance
     void* gb_mem = nullptr;
     size_t gb_pixels = 0;
@@ -139,11 +161,13 @@ struct Dev {
     struct { bool on; unsigned n; const unsigned* cost; unsigned* order; unsigned* split; unsigned cap, dominance; int near; }
         pending_order = {};
     bool fuse_order = true;
-    unsigned* lpt_mem = nullptr;            // cost[4 * ntiles] | order[ntiles]
-    size_t lpt_n = 0, lpt_cap = 0;
-    bool lpt_valid = false;
-    const void* lpt_key_target = nullptr;
-    int lpt_key_prog = -1, lpt_key_part = -1, lpt_key_parts = -1;
+    unsigned* lpt_mem = nullptr;            // cost[2][4 * cap] | order[2][cap] | split[2]
+    size_t lpt_cap = 0;
+    struct LptKey { bool valid; size_t n; const void* target; int prog, part, parts; };
+    LptKey lpt_key[2] = {};                 // what cost[p] / order[p] were last written for
+    unsigned* lpt_cost(int p) const { return lpt_mem + 4 * lpt_cap * p; }
+    unsigned* lpt_order(int p) const { return lpt_mem + 8 * lpt_cap + lpt_cap * p; }
+    unsigned* lpt_split(int p) const { return lpt_mem + 10 * lpt_cap + p; }
     // per-draw events for pt_last_render_ms: off until its first call (or PT_DRAW_EVENTS=1). Each
     // hipEventRecord costs ~5 us of stream time between two kernels on MI355X (r02h: two pairs per
     // frame were +19 us per frame, +1.7 % dragon stand-in, +3.8 % bunny)
@@ -343,14 +367,15 @@ int bands_owned(const Dev* c, int height)
     return (nb - c->part + c->num_parts - 1) / c->num_parts;
 }
 
-int begin_draw(Dev* c, int prog)
+int begin_draw(Dev* c, int prog, hipStream_t s = nullptr)
 {
+    if (!s) s = c->stream;
     if (c->draw_events) {
         if (!c->ev0[prog]) {
             HIPCHK(c, hipEventCreate(&c->ev0[prog]));
             HIPCHK(c, hipEventCreate(&c->ev1[prog]));
         }
-        HIPCHK(c, hipEventRecord(c->ev0[prog], c->stream));
+        HIPCHK(c, hipEventRecord(c->ev0[prog], s));
     }
     c->window_rec = c->window && c->window_seen[prog]++ % c->timing_every == 0;
     if (c->window_rec) {
@@ -361,19 +386,20 @@ int begin_draw(Dev* c, int prog)
             HIPCHK(c, hipEventCreate(&b));
             c->pool.emplace_back(a, b);
         }
-        HIPCHK(c, hipEventRecord(c->pool[k].first, c->stream));
+        HIPCHK(c, hipEventRecord(c->pool[k].first, s));
         c->window_draws.emplace_back(prog, (int)k);
     }
     return PT_OK;
 }
-int end_draw(Dev* c, int prog)
+int end_draw(Dev* c, int prog, hipStream_t s = nullptr)
 {
+    if (!s) s = c->stream;
     if (c->draw_events) {
-        HIPCHK(c, hipEventRecord(c->ev1[prog], c->stream));
+        HIPCHK(c, hipEventRecord(c->ev1[prog], s));
         c->ev_used[prog] = true;
     }
     if (c->window_rec)
-        HIPCHK(c, hipEventRecord(c->pool[c->window_draws.back().second].second, c->stream));
+        HIPCHK(c, hipEventRecord(c->pool[c->window_draws.back().second].second, s));
     return PT_OK;
 }
 
@@ -410,15 +436,42 @@ int wf_reserve(Dev* c, int wq, int hq, int tiles, int blocks)
     return PT_OK;
 }
 
+constexpr size_t kSpillPerLane = pt::kStackLevels - pt::kStackLdsMin + 4;   // float2 per lane of one slab
+
+// the megakernel's spill slabs, one per draw parity (overlapping draws must not share one): stack
+// levels kStackLdsMin..27, then up to 8 floats per lane for the G-buffer fields kept out of LDS
+// (pt_trace.h); slab p starts at spill_slab(c, p)
 int spill_reserve(Dev* c, size_t lanes)
 {
     if (lanes <= c->mk_spill_lanes) return PT_OK;
     if (c->mk_spill) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->mk_spill)); c->mk_spill = nullptr; }
     c->mk_spill_lanes = 0;
-    // stack levels kStackLdsMin..27, then up to 8 floats per lane for the G-buffer fields kept out
-    // of LDS (pt_trace.h)
-    HIPCHK(c, hipMalloc(&c->mk_spill, lanes * (pt::kStackLevels - pt::kStackLdsMin + 4) * sizeof(float2)));
+    HIPCHK(c, hipMalloc(&c->mk_spill, 2 * lanes * kSpillPerLane * sizeof(float2)));
     c->mk_spill_lanes = lanes;
+    return PT_OK;
+}
+float2* spill_slab(Dev* c, int p) { return c->mk_spill + (size_t)p * c->mk_spill_lanes * kSpillPerLane; }
+
+// rad[2] (pt_trace -> pt_blend) for a frame of `pixels`
+int rad_reserve(Dev* c, size_t pixels)
+{
+    if (pixels <= c->rad_pixels) return PT_OK;
+    if (c->rad_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->rad_mem)); c->rad_mem = nullptr; }
+    c->rad_pixels = 0;
+    HIPCHK(c, hipMalloc(&c->rad_mem, 2 * pixels * sizeof(float4)));
+    c->rad_pixels = pixels;
+    return PT_OK;
+}
+
+// the side streams and events of frame overlap (created at the first overlapped draw)
+int overlap_init(Dev* c)
+{
+    if (c->ts[0]) return PT_OK;
+    for (int p = 0; p < 2; p++) {
+        HIPCHK(c, hipStreamCreateWithFlags(&c->ts[p], hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_mark[p], hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&c->ev_traced[p], hipEventDisableTiming));
+    }
     return PT_OK;
 }
 
@@ -636,8 +689,11 @@ int render_trace(DevFx* fx, DevTex* target)
         hipMemsetAsync(g_wave_log, 0, need * 8, c->stream);   // padding workgroups leave zero rows
         g_wave_log_n = need / pt::kWaveLogSlots;
         a.wave_log = g_wave_log;
-        if (!g_walk_stat && hipMalloc(&g_walk_stat, 40 * 8) == hipSuccess) hipMemset(g_walk_stat, 0, 40 * 8);
-        a.walk_stat = g_walk_stat;
+        // the walk statistics' global atomics (every wave, every bounce) slow the launch ~4x and skew
+        // the timeline by XCD: only when asked for (tools/walkstat.py sets PT_WALKSTAT=1)
+        static const bool walkstat = std::getenv("PT_WALKSTAT") && std::atoi(std::getenv("PT_WALKSTAT")) != 0;
+        if (walkstat && !g_walk_stat && hipMalloc(&g_walk_stat, 40 * 8) == hipSuccess) hipMemset(g_walk_stat, 0, 40 * 8);
+        a.walk_stat = walkstat ? g_walk_stat : nullptr;
     }
 #endif
     int gx = (target->w + pt::kTile - 1) / pt::kTile;
@@ -654,71 +710,101 @@ int render_trace(DevFx* fx, DevTex* target)
         if (rc) return rc;
         const unsigned waves = (n_wave_tiles + c->persist_tiles - 1) / c->persist_tiles;
         const size_t lanes = (size_t)((waves + 3) / 4) * pt::kBlock;
-        if (lanes * (pt::kStackLevels - pt::kStackLdsMin + 4) > 0xffffffffull)   // 32-bit slab index
+        if (lanes * kSpillPerLane > 0xffffffffull)   // 32-bit slab index
             return fail(c, PT_ERR_ARG, "render target too large for the BVH stack slab");
         if (mesh && (rc = spill_reserve(c, lanes))) return rc;
         a.spill = c->mk_spill;
         a.spill_stride = lanes;
     }
-    // megakernel: the longest-first order of the last draw (if it applies) and the tiles to split;
-    // split tiles take 12 more workgroups each, in padding rows of the grid
-    const size_t n_tiles = (size_t)gx * gy;
-    const bool lpt_same = c->lpt_valid && c->lpt_n == n_tiles && c->lpt_key_target == target &&
-                          c->lpt_key_prog == fx->prog && c->lpt_key_part == c->part && c->lpt_key_parts == c->num_parts;
-    const unsigned split = (c->backend == PT_BACKEND_MEGAKERNEL && c->lpt && !c->counting && lpt_same)
-                               ? (unsigned)std::min<size_t>(c->split_tiles, n_tiles) & ~7u : 0u;   // the cap
-    const unsigned extra = 4u * pt::kSplitParts - 4u;   // more workgroups per split tile
-    const int gy_grid = gy + (int)((extra * split + 4u * gx - 1) / (4u * gx));
-    if (c->backend == PT_BACKEND_MEGAKERNEL && mesh) {
-        const size_t lanes = (size_t)gx * gy_grid * pt::kBlock;
-        if (lanes * (pt::kStackLevels - pt::kStackLdsMin + 4) > 0xffffffffull)   // 32-bit slab index
-            return fail(c, PT_ERR_ARG, "render target too large for the BVH stack slab");
-        int rc = spill_reserve(c, lanes);
+    if (c->backend != PT_BACKEND_MEGAKERNEL || gy <= 0) {
+        // the wavefront / persistent schedules: on the main stream, their finish pass accumulating;
+        // the next megakernel draw waits for all of it (they share the spill slab)
+        if (c->backend != PT_BACKEND_MEGAKERNEL) c->mark_valid = false;
+        int rc = begin_draw(c, fx->prog);
         if (rc) return rc;
-        a.spill = c->mk_spill;
-        a.spill_stride = lanes;
-    }
-    int rc = begin_draw(c, fx->prog);
-    if (rc) return rc;
-    if (gy > 0) {
-        if (c->backend == PT_BACKEND_WAVEFRONT) {
+        if (gy > 0 && c->backend == PT_BACKEND_WAVEFRONT) {
             HIPCHK(c, hipMemsetAsync(c->wf.cnt, 0, 16 * pt::kShards * sizeof(unsigned), c->stream));
             HIPCHK(c, pt_launch_wavefront(fx->prog, c->counting ? 1 : 0, &a, &c->wf, gx, gy, persist, c->stream));
-        } else if (c->backend == PT_BACKEND_PERSISTENT) {
+        } else if (gy > 0) {
             HIPCHK(c, pt_launch_persist(fx->prog, c->counting ? 1 : 0, &a, &c->gb, gx, n_wave_tiles, c->persist_tiles,
                                         c->persist_refill, c->stream));
             HIPCHK(c, pt_launch_finish(&a, &c->gb, gx, gy, c->stream));
-        } else {
-            // longest-first: the previous draw's wave durations order this one's workgroups
-            const size_t n = n_tiles;   // 16x16 tiles
-            const bool same = lpt_same;
-            if (c->lpt && !c->counting) {
-                if (c->lpt_cap < n) {
-                    if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
-                    HIPCHK(c, hipMalloc(&c->lpt_mem, (5 * n + 1) * sizeof(unsigned)));   // cost | order | split
-                    HIPCHK(c, hipMemsetAsync(c->lpt_mem, 0, 4 * n * sizeof(unsigned), c->stream));
-                    c->lpt_cap = n;
-                    c->lpt_valid = false;
-                } else if (!same) {   // another grid, target or program: its wave costs start afresh
-                    HIPCHK(c, hipMemsetAsync(c->lpt_mem, 0, 4 * n * sizeof(unsigned), c->stream));
-                }
-                a.order = same ? c->lpt_mem + 4 * c->lpt_cap : nullptr;
-                a.cost = c->lpt_mem;
-                a.prio_tiles = a.order ? c->prio_tiles : 0u;
-                a.split = (a.order && split) ? c->lpt_mem + 5 * c->lpt_cap : nullptr;
-            }
-            a.ntiles = (unsigned)n;
-            HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, c->stream));
-            if (a.cost) {
-                c->pending_order = { true, (unsigned)n, a.cost, c->lpt_mem + 4 * c->lpt_cap, c->lpt_mem + 5 * c->lpt_cap,
-                                     (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance, c->split_near };
-                if (!c->fuse_order) { if (int rc = flush_order(c)) return rc; }
-                c->lpt_valid = true; c->lpt_n = n; c->lpt_key_target = target; c->lpt_key_prog = fx->prog;
-                c->lpt_key_part = c->part; c->lpt_key_parts = c->num_parts;
-            }
         }
+        return end_draw(c, fx->prog);
     }
-    return end_draw(c, fx->prog);
+
+    // ---- the megakernel: draw k = mk_seq uses the buffers of parity k & 1
+    const int par = (int)(c->mk_seq & 1u);
+    // longest-first: the wave durations of draw k - 2 (same parity) order this draw's workgroups when it
+    // drew the same grid, target and program; split tiles take 12 more workgroups each, in padding rows
+    const size_t n = (size_t)gx * gy;   // 16x16 tiles
+    const Dev::LptKey& key = c->lpt_key[par];
+    const bool lpt = c->lpt && !c->counting;
+    const bool same = lpt && key.valid && key.n == n && key.target == target && key.prog == fx->prog &&
+                      key.part == c->part && key.parts == c->num_parts && c->lpt_cap >= n;
+    const unsigned split = same ? (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u : 0u;   // the cap
+    const unsigned extra = 4u * pt::kSplitParts - 4u;   // more workgroups per split tile
+    const int gy_grid = gy + (int)((extra * split + 4u * gx - 1) / (4u * gx));
+    if (mesh) {
+        const size_t lanes = (size_t)gx * gy_grid * pt::kBlock;
+        if (lanes * kSpillPerLane > 0xffffffffull)   // 32-bit slab index
+            return fail(c, PT_ERR_ARG, "render target too large for the BVH stack slab");
+        int rc = spill_reserve(c, lanes);
+        if (rc) return rc;
+        a.spill = spill_slab(c, par);
+        a.spill_stride = lanes;
+    }
+    if (int rc = rad_reserve(c, (size_t)target->w * target->h)) return rc;
+    a.rad = c->rad_mem + (size_t)par * c->rad_pixels;
+    if (lpt && c->lpt_cap < n) {
+        if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
+        HIPCHK(c, hipMalloc(&c->lpt_mem, (10 * n + 2) * sizeof(unsigned)));   // cost[2] | order[2] | split[2]
+        c->lpt_cap = n;
+        c->lpt_key[0].valid = c->lpt_key[1].valid = false;
+    }
+    // where the path tracing runs: a side stream gated by the main stream's state when the previous
+    // megakernel draw began (or now: the first draw, after another schedule or a stream switch, with
+    // counting kernels, or when a sampler is a render target, which draws on the main stream may write)
+    bool overlap = c->overlap && !c->counting && !PT_SECPROF_BUILD;   // (experiment builds: one wave log)
+    for (const auto& kv : fx->samplers)
+        if (kv.second && kv.second->kind == TEX_RT && kv.first != "previousBuffer") overlap = false;
+    hipStream_t ts = c->stream;
+    if (overlap) {
+        if (int rc = overlap_init(c)) return rc;
+        HIPCHK(c, hipEventRecord(c->ev_mark[par], c->stream));
+        ts = c->ts[par];
+        HIPCHK(c, hipStreamWaitEvent(ts, c->mark_valid ? c->ev_mark[par ^ 1] : c->ev_mark[par], 0));
+        c->mark_valid = true;
+    } else {
+        c->mark_valid = false;
+    }
+    if (lpt) {
+        if (!same) HIPCHK(c, hipMemsetAsync(c->lpt_cost(par), 0, 4 * n * sizeof(unsigned), ts));   // costs start afresh
+        a.order = same ? c->lpt_order(par) : nullptr;
+        a.cost = c->lpt_cost(par);
+        a.prio_tiles = a.order ? c->prio_tiles : 0u;
+        a.split = (a.order && split) ? c->lpt_split(par) : nullptr;
+    }
+    a.ntiles = (unsigned)n;
+    if (int rc = begin_draw(c, fx->prog, ts)) return rc;
+    HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, ts));
+    if (int rc = end_draw(c, fx->prog, ts)) return rc;
+    if (overlap) {
+        HIPCHK(c, hipEventRecord(c->ev_traced[par], ts));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_traced[par], 0));
+    }
+    // the history half of main() on the main stream, where the copy / output draws that read the
+    // accumulation follow
+    pt::BlendArgs b{ a.width, a.height, a.num_parts, a.part, a.frame, a.moving, a.rad, a.prev, a.out };
+    HIPCHK(c, pt_launch_blend(&b, gy, c->stream));
+    if (a.cost) {   // this draw's costs order draw k + 2: the build rides along with the next screenOutput
+        c->pending_order = { true, (unsigned)n, a.cost, c->lpt_order(par), c->lpt_split(par),
+                             (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance, c->split_near };
+        if (!c->fuse_order) { if (int rc = flush_order(c)) return rc; }
+        c->lpt_key[par] = { true, n, target, fx->prog, c->part, c->num_parts };
+    }
+    c->mk_seq++;
+    return PT_OK;
 }
 
 int launch_copy(Dev* c, DevTex* src, DevTex* dst, int num_parts, int part)
@@ -883,6 +969,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_PRIO_TILES")) c->prio_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_SPLIT_NEAR")) c->split_near = std::max(1, std::min(128, std::atoi(v)));
     if (const char* v = std::getenv("PT_SPLIT_ALWAYS")) c->split_dominance = std::atoi(v) ? 0u : 8u;
     if (const char* v = std::getenv("PT_BVH_LAYOUT"))   // reference | pairs | trail: the context's initial walk
@@ -924,6 +1011,12 @@ void dev_ctx_destroy(Dev* c)
     if (c->wf_mem) hipFree(c->wf_mem);
     if (c->lpt_mem) hipFree(c->lpt_mem);
     if (c->mk_spill) hipFree(c->mk_spill);
+    if (c->rad_mem) hipFree(c->rad_mem);
+    for (int p = 0; p < 2; p++) {   // (every side-stream draw was waited for by a blend on the main stream)
+        if (c->ts[p]) { hipStreamSynchronize(c->ts[p]); hipStreamDestroy(c->ts[p]); }
+        if (c->ev_mark[p]) hipEventDestroy(c->ev_mark[p]);
+        if (c->ev_traced[p]) hipEventDestroy(c->ev_traced[p]);
+    }
     if (c->gb_mem) hipFree(c->gb_mem);
     if (c->d_err) hipFree(c->d_err);
     if (c->d_counters) hipFree(c->d_counters);
@@ -1179,6 +1272,7 @@ int dev_set_stream(Dev* c, void* stream)
     if (int rc = flush_order(c)) return rc;        // on the stream its draw ran on
     HIPCHK(c, hipStreamSynchronize(c->stream));   // work already queued finishes first
     c->stream = stream ? (hipStream_t)stream : c->own_stream;
+    c->mark_valid = false;   // the next megakernel draw waits for the new stream's state
     return PT_OK;
 }
 
@@ -1284,8 +1378,9 @@ int dev_queue_stats(Dev* c, uint32_t out[16])
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = flush_order(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (c->lpt_mem && c->lpt_valid)   // the tiles the next megakernel draw of the same grid splits
-        HIPCHK(c, hipMemcpy(&out[7], c->lpt_mem + 5 * c->lpt_cap, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    const int p = (int)(c->mk_seq & 1u);   // the tiles the next megakernel draw of the same grid splits
+    if (c->lpt_mem && c->lpt_key[p].valid)
+        HIPCHK(c, hipMemcpy(&out[7], c->lpt_split(p), sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (!c->wf_mem) return PT_OK;
     std::vector<unsigned> h(16 * pt::kShards);
     HIPCHK(c, hipMemcpy(h.data(), c->wf.cnt, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));

@@ -178,6 +178,47 @@ __global__ __launch_bounds__(256) void pt_copy(CopyArgs a)
     }
 }
 
+// ------------------------------------------------------------------------------ accumulation
+// The history half of main() (js/PathTracingCommon.js:1326-1357) for a megakernel draw: the pixel's
+// history texel (previousBuffer = the screenCopy target), cleared at frame 1 and halved while the camera
+// moves, plus the radiance pt_trace left in `rad`; alpha = the radiance's pre-history flag unless the
+// history's says 1.01 (stays sharp) or -1 (0). Each pixel reads only its own texels, so `prev` may be
+// `out` (in-place history). A block covers 64 columns x one 16-row band, each thread 4 rows, loads first.
+__global__ __launch_bounds__(256) void pt_blend(BlendArgs a)
+{
+    const int band = blockIdx.y * a.num_parts + a.part;
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int r0 = band * kTile + (threadIdx.x >> 6);
+    if (x >= a.width) return;
+    typedef float nt4 __attribute__((ext_vector_type(4)));
+    nt4 rv[4], pv[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int y = r0 + 4 * k;
+        if (y < a.height) {
+            const long long i = (long long)y * a.width + x;
+            rv[k] = __builtin_nontemporal_load((const nt4*)&a.rad[i]);
+            pv[k] = __builtin_nontemporal_load((const nt4*)&a.prev[i]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int y = r0 + 4 * k;
+        if (y >= a.height) break;
+        float4 prev = make_float4(pv[k].x, pv[k].y, pv[k].z, pv[k].w);
+        float cr = rv[k].x, cg = rv[k].y, cb = rv[k].z, ca = rv[k].w;
+        if (a.frame == 1.0f) prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        else if (a.moving) {
+            prev.x *= 0.5f; prev.y *= 0.5f; prev.z *= 0.5f;
+            cr *= 0.5f; cg *= 0.5f; cb *= 0.5f;
+            prev.w = 0.0f;
+        }
+        if (prev.w == 1.01f) ca = 1.01f;
+        if (prev.w == -1.0f) ca = 0.0f;
+        a.out[(long long)y * a.width + x] = make_float4(prev.x + cr, prev.y + cg, prev.z + cb, ca);
+    }
+}
+
 // ------------------------------------------------------------------------------ screenOutput
 // the texel texelFetch(accumulationBuffer, ivec2(gl_FragCoord.xy + vec2(dx, dy)), 0) reads for the
 // tap at integer position (x, y) = pixel + (dx, dy) (js/PathTracingCommon.js:44-72): ivec2() of a
@@ -590,6 +631,13 @@ hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, 
     case 3: hipLaunchKernelGGL(pt::pt_pairs_top, dim3(1), b256, 0, s, rec, root, top); break;
     default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t pt_launch_blend(const pt::BlendArgs* a, int bands, hipStream_t s)
+{
+    if (bands <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pt::pt_blend, dim3((a->width + 63) / 64, bands), dim3(256), 0, s, *a);
     return hipGetLastError();
 }
 

@@ -199,31 +199,20 @@ PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_s
     return max3s(accum, 0.0f);
 }
 
-// progressive accumulation of pixel `pi` (js/PathTracingCommon.js:1326-1357): the history texel, the
-// radiance r, the G-buffer sharpness and whether any 2x2 derivative marked the pixel an edge
-PT_D void accumulate(const TraceArgs& a, long long pi, f3 r, float sharp, bool edge)
+// what main() computes of pixel `pi` without the history (js/PathTracingCommon.js:1304-1349): the
+// radiance r and the alpha flag from the G-buffer sharpness and the 2x2 edge test - the first three of
+// the reference's five `currentPixel.a` assignments (:1339, :1347, :1349); pt_blend applies the two
+// that read the history (:1352, :1355) and the blend itself (:1326-1337, :1357). Streamed once per
+// frame: a non-temporal store, so that it displaces fewer BVH records in L2.
+PT_D void radianceOut(const TraceArgs& a, long long pi, f3 r, float sharp, bool edge)
 {
-    // history and accumulation stream once per frame: non-temporal loads and stores, so that they
-    // displace fewer BVH records in L2 (helmet -2 %, sky+dragon -1.5 %, bunny -1 %, dragon +-0)
-    float4 prev;
-    prev.x = __builtin_nontemporal_load(&a.prev[pi].x); prev.y = __builtin_nontemporal_load(&a.prev[pi].y);
-    prev.z = __builtin_nontemporal_load(&a.prev[pi].z); prev.w = __builtin_nontemporal_load(&a.prev[pi].w);
-    float cr = r.x, cg = r.y, cb = r.z, ca;
-    if (a.frame == 1.0f) prev = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    else if (a.moving) {
-        prev.x *= 0.5f; prev.y *= 0.5f; prev.z *= 0.5f;
-        cr *= 0.5f; cg *= 0.5f; cb *= 0.5f;
-        prev.w = 0.0f;
-    }
-    ca = 0.0f;
+    float ca = 0.0f;
     if (edge) sharp = 1.01f;
     if (sharp == 1.01f) ca = 1.01f;
     if (sharp == -1.0f) ca = -1.0f;
-    if (prev.w == 1.01f) ca = 1.01f;
-    if (prev.w == -1.0f) ca = 0.0f;
     typedef float nt4 __attribute__((ext_vector_type(4)));
-    const nt4 o = { prev.x + cr, prev.y + cg, prev.z + cb, ca };
-    __builtin_nontemporal_store(o, (nt4*)&a.out[pi]);
+    const nt4 o = { r.x, r.y, r.z, ca };
+    __builtin_nontemporal_store(o, (nt4*)&a.rad[pi]);
 }
 
 PT_D float xorq(float v, int m) { return __shfl_xor(v, m, 64); }
@@ -404,7 +393,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     }
     if (!active || px >= a.width || py >= a.height) return;   // quad helper outside the target, idle lane
     const bool edge = colorDiff >= 1.0f || normalDiff >= 1.0f || objectDiff >= 1.0f;
-    accumulate(a, (long long)py * a.width + px, r, g.sharp, edge);
+    radianceOut(a, (long long)py * a.width + px, r, g.sharp, edge);
 }
 
 // ------------------------------------------------------------------------------ persistent paths

@@ -293,6 +293,41 @@ def test_dragon_standin_1080p_bitexact_and_counters(engine, backend):
     assert cnt == {k: sum(c[k] for c in ref_cnt) for k in ref_cnt[0]}
 
 
+@pytest.mark.parametrize("size", [(480, 272), (203, 117)])
+def test_overlapped_frames_observed_between_draws(engine, size):
+    """Frame overlap: the path tracing of draw k + 1 runs beside draw k's, gated only by
+    the main stream's state two draws back, and the history blend follows on the main stream. Sixteen
+    frames of the dragon stand-in (the recording, then still-camera frames) are issued with no sync
+    between them, except that the accumulation is read right after the path-tracing draw of frames 3
+    and 9 (before their copy / output), the screenCopy target right after frame 5's copy draw (a deferred
+    copy) and the canvas after frame 7's output. Every read, and the last frame's accumulation and
+    canvas, equal the oracle's bits."""
+    import copy
+    import babylon_pt as bp
+    W, Hh = size
+    meta = copy.deepcopy(H.stream("gltf_bunny_1080p"))
+    mesh = H.synthetic_dragon()
+    player = bp.StreamPlayer(engine, meta, H.bluenoise(), H.texture_payloads(meta, mesh), W, Hh)
+    meta["frames"] = meta["frames"] + [player.synth_frame(k) for k in range(12)]
+    ref_acc, ref_can, _ = H.oracle_replay(meta, None, W, Hh, with_output=True, mesh=mesh)
+    engine.resize_canvas(W, Hh)
+    seen = []
+    for i, calls in enumerate(meta["frames"]):
+        for call in calls:
+            player.play_call(call)
+            if call["shader"] == "pathTracingFragmentShader" and i in (3, 9):
+                seen.append(("acc after path tracing", i, player.textures["pathTracingRenderTarget"].read(), ref_acc[i]))
+            if call["shader"] == "screenCopyFragmentShader" and i == 5:
+                seen.append(("screenCopy target", i, player.textures["screenCopyRenderTarget"].read(), ref_acc[i]))
+            if call["shader"] == "screenOutputFragmentShader" and i == 7:
+                seen.append(("canvas", i, engine.read_canvas(W, Hh), ref_can[i]))
+    engine.sync()
+    seen.append(("final acc", len(meta["frames"]) - 1, player.textures["pathTracingRenderTarget"].read(), ref_acc[-1]))
+    seen.append(("final canvas", len(meta["frames"]) - 1, engine.read_canvas(W, Hh), ref_can[-1]))
+    for what, i, got, want in seen:
+        assert _bits_equal(want, got), "%s, frame %d: %s" % (what, i, _diff_report(want, got))
+
+
 @pytest.mark.parametrize("layout", ["pairs", "trail"])
 @pytest.mark.parametrize("workload", ["bunny", "dragon"])
 def test_timed_kernel_1080p_bitexact(engine, workload, layout):

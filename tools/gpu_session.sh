@@ -47,7 +47,7 @@ for step in "$@"; do
             if [ $kind = envmx ]; then
               res=$(env $envs timeout -k 10 120 python tools/exp_timing.py --workload "$w" --frames 30 --backends megakernel --layouts pairs --no-mesh-variant 2>&1 | tail -1); rc=$?
             else
-              res=$(env $envs timeout -k 10 200 python3 bench.py --workload "$w" --no-pmc --cpu-budget 0 --no-check 2>&1 | tail -1); rc=$?
+              res=$(env $envs timeout -k 10 200 python3 bench.py --workload "$w" --no-pmc --cpu-budget 0 --no-check --no-anchors 2>&1 | tail -1); rc=$?
             fi
             echo "r$r [$cfg] $w $res" >> "$LOG"
             [ $rc -ne 0 ] && break 3

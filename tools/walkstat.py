@@ -12,6 +12,7 @@ import sys
 
 import numpy as np
 
+os.environ.setdefault("PT_WALKSTAT", "1")   # the SECPROF build's walk statistics are opt-in (pt_capi.cpp)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "babylon.js-pathtracing-renderer_amd", "python"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
