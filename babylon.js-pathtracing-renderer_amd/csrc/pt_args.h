@@ -126,6 +126,13 @@ struct TraceArgs {
     // history (js/PathTracingCommon.js:1326-1357), so the kernel never reads it and consecutive frames'
     // path tracing may overlap
     float4* rad;
+    // late-bounce compaction (megakernel mesh draws; pt_cont): after a bounce >= cont_bounce,
+    // a wave with at most cont_lanes live paths stores them as 64-B records and ends; pt_cont runs them
+    // packed into full waves (cont_rec NULL: off)
+    float4* cont_rec;
+    unsigned* cont_aux;     // per record: the pixel (py * width + px) | the 2x2 edge flag << 31
+    unsigned* cont_count;   // records stored by this draw (zeroed by the draw's pt_blend for the next user)
+    unsigned cont_bounce, cont_lanes, cont_refill;
     Tex8 bluenoise;
     const float4* aabb;
     long long aabb_texels;
@@ -145,6 +152,8 @@ struct TraceArgs {
     const unsigned* order;
     unsigned* cost;
     unsigned prio_tiles;   // the first prio_tiles tiles of `order` (the slowest last frame) run at s_setprio 3
+    unsigned order_zig;    // 1: after the split tiles, slots take `order` from both ends alternately (slowest,
+                           // cheapest, 2nd slowest, ...): the slowest still start first, cheap tiles mix in
     // *split (written by the previous pt_order_build; a multiple of 8): the first *split tiles of
     // `order` are shaded by 16 waves of 16 lanes (4x4 pixels) instead of 4 waves of 64 (pt_trace);
     // the grid carries padding rows for up to split_cap of them
@@ -179,7 +188,14 @@ struct WfBufs {
     unsigned* bvhq;         // per shard: slots whose ray enters the model's root box this bounce
     float4* gb0;            // per pixel: objectNormal.xyz, objectID
     float4* gb1;            // per pixel: objectColor.xyz, pixelSharpness
-    float4* rad;            // per pixel: CalculateRadiance() result
+    float4* rad;
+    // late-bounce compaction (megakernel mesh draws; pt_cont): after a bounce >= cont_bounce,
+    // a wave with at most cont_lanes live paths stores them as 64-B records and ends; pt_cont runs them
+    // packed into full waves (cont_rec NULL: off)
+    float4* cont_rec;
+    unsigned* cont_aux;     // per record: the pixel (py * width + px) | the 2x2 edge flag << 31
+    unsigned* cont_count;   // records stored by this draw (zeroed by the draw's pt_blend for the next user)
+    unsigned cont_bounce, cont_lanes, cont_refill;            // per pixel: CalculateRadiance() result
     float2* spill;          // BVH stack levels >= kStackLds: [level][persistent lane]
     unsigned* cnt;          // [b * kShards + s]: live paths of shard s entering bounce b (b = 0..6)
     unsigned* bcnt;         // [b * kShards + s]: BVH queue of shard s at bounce b
@@ -218,6 +234,7 @@ struct BlendArgs {
     const float4* rad;
     const float4* prev;
     float4* out;
+    unsigned* cont_count;   // late-bounce compaction: the draw's record counter, zeroed here (NULL: none)
 };
 
 struct CopyArgs {

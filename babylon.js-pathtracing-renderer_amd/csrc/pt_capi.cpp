@@ -34,6 +34,7 @@ hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned
                                  unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s);
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_blend(const pt::BlendArgs* a, int bands, hipStream_t s);
+hipError_t pt_launch_cont(int prog, const pt::TraceArgs* a, int waves, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
 hipError_t pt_launch_persist(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x,
@@ -142,6 +143,13 @@ struct Dev {
     bool mark_valid = false;      // mark[(mk_seq - 1) & 1] may gate the next draw (else it waits for a fresh mark)
     float4* rad_mem = nullptr;    // rad[2]: radiance + flag per pixel
     size_t rad_pixels = 0;
+    // late-bounce compaction of the megakernel's mesh draws (pt_trace -> pt_cont; PT_CONT=1 enables):
+    // per parity 64-B path records, their pixels and a counter; the bounce from which, and the live lanes
+    // at or below which, a wave hands its paths on; the refill batch and pt_cont's one-wave workgroups
+    bool cont = false;
+    void* cont_mem = nullptr;
+    size_t cont_cap = 0;
+    unsigned cont_bounce = 3, cont_lanes = 16, cont_refill = 16, cont_waves = 2048;
     pt::WfBufs gb = {};           // persistent backend: per-pixel G-buffer + radiance
     void* gb_mem = nullptr;
     size_t gb_pixels = 0;
@@ -150,6 +158,7 @@ struct Dev {
     // longest-first dispatch of the megakernel (PT_LPT=0 disables): cost[] / order[] of the last
     // path-tracing draw, reused when the next draw has the same grid, target and program
     bool lpt = true;
+    bool lpt_zig = false;     // PT_LPT=2: the order taken from both ends alternately (TraceArgs::order_zig)
     unsigned prio_tiles = 0;   // longest-first: the first prio_tiles 16x16 tiles run at raised wave priority
     unsigned split_tiles = 32; // longest-first: at most this many of the slowest tiles shaded by 16-lane waves
                                // (pt_trace, pt_order_build; PT_SPLIT_TILES)
@@ -448,6 +457,7 @@ int spill_reserve(Dev* c, size_t lanes)
     c->mk_spill_lanes = 0;
     HIPCHK(c, hipMalloc(&c->mk_spill, 2 * lanes * kSpillPerLane * sizeof(float2)));
     c->mk_spill_lanes = lanes;
+    c->mark_valid = false;   // new memory: the next draw waits for everything before it
     return PT_OK;
 }
 float2* spill_slab(Dev* c, int p) { return c->mk_spill + (size_t)p * c->mk_spill_lanes * kSpillPerLane; }
@@ -460,7 +470,37 @@ int rad_reserve(Dev* c, size_t pixels)
     c->rad_pixels = 0;
     HIPCHK(c, hipMalloc(&c->rad_mem, 2 * pixels * sizeof(float4)));
     c->rad_pixels = pixels;
+    c->mark_valid = false;
     return PT_OK;
+}
+
+// pt_cont's records for frames of up to `paths` pixels, per parity: records [cap x 64 B] | pixels [cap x 4 B]
+// | counter; the counters start at zero here, afterwards each draw's pt_blend zeroes its own
+int cont_reserve(Dev* c, size_t paths)
+{
+    if (paths <= c->cont_cap) return PT_OK;
+    if (c->cont_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->cont_mem)); c->cont_mem = nullptr; }
+    c->cont_cap = 0;
+    const size_t per = paths * 64 + ((paths * 4 + 255) & ~(size_t)255) + 256;
+    HIPCHK(c, hipMalloc(&c->cont_mem, 2 * per));
+    // on the main stream (hipMemset would go to the null stream, which the non-blocking side streams do
+    // not wait for: the next draw's atomics raced with it); the next draw's path tracing waits for a mark
+    // recorded after it
+    HIPCHK(c, hipMemsetAsync(c->cont_mem, 0, 2 * per, c->stream));
+    c->cont_cap = paths;
+    c->mark_valid = false;
+    return PT_OK;
+}
+void cont_args(Dev* c, int p, pt::TraceArgs& a)
+{
+    const size_t per = c->cont_cap * 64 + ((c->cont_cap * 4 + 255) & ~(size_t)255) + 256;
+    char* m = (char*)c->cont_mem + (size_t)p * per;
+    a.cont_rec = (float4*)m;
+    a.cont_aux = (unsigned*)(m + c->cont_cap * 64);
+    a.cont_count = (unsigned*)(m + per - 256);
+    a.cont_bounce = std::max(2u, c->cont_bounce);   // the G-buffer's normal / colour / id are final from bounce 2
+    a.cont_lanes = c->cont_lanes;
+    a.cont_refill = c->cont_refill;
 }
 
 // the side streams and events of frame overlap (created at the first overlapped draw)
@@ -756,10 +796,16 @@ int render_trace(DevFx* fx, DevTex* target)
     }
     if (int rc = rad_reserve(c, (size_t)target->w * target->h)) return rc;
     a.rad = c->rad_mem + (size_t)par * c->rad_pixels;
+    const bool cont = c->cont && mesh && !c->counting && !PT_SECPROF_BUILD;
+    if (cont) {
+        if (int rc = cont_reserve(c, (size_t)target->w * target->h)) return rc;
+        cont_args(c, par, a);
+    }
     if (lpt && c->lpt_cap < n) {
         if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
         HIPCHK(c, hipMalloc(&c->lpt_mem, (10 * n + 2) * sizeof(unsigned)));   // cost[2] | order[2] | split[2]
         c->lpt_cap = n;
+        c->mark_valid = false;
         c->lpt_key[0].valid = c->lpt_key[1].valid = false;
     }
     // where the path tracing runs: a side stream gated by the main stream's state when the previous
@@ -783,11 +829,14 @@ int render_trace(DevFx* fx, DevTex* target)
         a.order = same ? c->lpt_order(par) : nullptr;
         a.cost = c->lpt_cost(par);
         a.prio_tiles = a.order ? c->prio_tiles : 0u;
+        a.order_zig = c->lpt_zig ? 1u : 0u;
         a.split = (a.order && split) ? c->lpt_split(par) : nullptr;
     }
     a.ntiles = (unsigned)n;
     if (int rc = begin_draw(c, fx->prog, ts)) return rc;
     HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, ts));
+    if (cont)   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
+        HIPCHK(c, pt_launch_cont(fx->prog, &a, (int)std::min<size_t>(c->cont_waves, (size_t)gx * gy * 4), ts));
     if (int rc = end_draw(c, fx->prog, ts)) return rc;
     if (overlap) {
         HIPCHK(c, hipEventRecord(c->ev_traced[par], ts));
@@ -795,7 +844,7 @@ int render_trace(DevFx* fx, DevTex* target)
     }
     // the history half of main() on the main stream, where the copy / output draws that read the
     // accumulation follow
-    pt::BlendArgs b{ a.width, a.height, a.num_parts, a.part, a.frame, a.moving, a.rad, a.prev, a.out };
+    pt::BlendArgs b{ a.width, a.height, a.num_parts, a.part, a.frame, a.moving, a.rad, a.prev, a.out, a.cont_count };
     HIPCHK(c, pt_launch_blend(&b, gy, c->stream));
     if (a.cost) {   // this draw's costs order draw k + 2: the build rides along with the next screenOutput
         c->pending_order = { true, (unsigned)n, a.cost, c->lpt_order(par), c->lpt_split(par),
@@ -965,11 +1014,20 @@ Dev* dev_ctx_create(int device, int* err)
     c->cu_count = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     if (const char* v = std::getenv("PT_PERSIST_TILES")) c->persist_tiles = (unsigned)std::max(1, std::atoi(v));
     if (const char* v = std::getenv("PT_DRAW_EVENTS")) c->draw_events = std::atoi(v) != 0;
-    if (const char* v = std::getenv("PT_LPT")) c->lpt = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PT_LPT")) { c->lpt = std::atoi(v) != 0; c->lpt_zig = std::atoi(v) == 2; }
     if (const char* v = std::getenv("PT_PRIO_TILES")) c->prio_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
+    // split tiles shorten a launch's critical path; with frames overlapping, the next frame's waves fill
+    // it instead, and the split waves only cost issue (profiles/r05c_frames_ab.txt: helmet +2.6 %,
+    // sky + dragon +1 %, the rest +-0.3 % without them): off unless PT_SPLIT_TILES asks for them
+    if (c->overlap && !std::getenv("PT_SPLIT_TILES")) c->split_tiles = 0;
+    if (const char* v = std::getenv("PT_CONT")) c->cont = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PT_CONT_BOUNCE")) c->cont_bounce = (unsigned)std::max(2, std::atoi(v));
+    if (const char* v = std::getenv("PT_CONT_LANES")) c->cont_lanes = (unsigned)std::min(64, std::max(1, std::atoi(v)));
+    if (const char* v = std::getenv("PT_CONT_REFILL")) c->cont_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
+    if (const char* v = std::getenv("PT_CONT_WAVES")) c->cont_waves = (unsigned)std::max(1, std::atoi(v));
     if (const char* v = std::getenv("PT_SPLIT_NEAR")) c->split_near = std::max(1, std::min(128, std::atoi(v)));
     if (const char* v = std::getenv("PT_SPLIT_ALWAYS")) c->split_dominance = std::atoi(v) ? 0u : 8u;
     if (const char* v = std::getenv("PT_BVH_LAYOUT"))   // reference | pairs | trail: the context's initial walk
@@ -981,8 +1039,9 @@ Dev* dev_ctx_create(int device, int* err)
     c->stream = c->own_stream;
     if (e == hipSuccess) e = hipMalloc(&c->d_err, 256);
     if (e == hipSuccess) e = hipMalloc(&c->d_counters, pt::C_NUM * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipMemset(c->d_err, 0, 256);
-    if (e == hipSuccess) e = hipMemset(c->d_counters, 0, pt::C_NUM * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_err, 0, 256, c->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_counters, 0, pt::C_NUM * sizeof(unsigned long long), c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) {
         if (err) *err = PT_ERR_HIP;
         dev_ctx_destroy(c);
@@ -1012,6 +1071,7 @@ void dev_ctx_destroy(Dev* c)
     if (c->lpt_mem) hipFree(c->lpt_mem);
     if (c->mk_spill) hipFree(c->mk_spill);
     if (c->rad_mem) hipFree(c->rad_mem);
+    if (c->cont_mem) hipFree(c->cont_mem);
     for (int p = 0; p < 2; p++) {   // (every side-stream draw was waited for by a blend on the main stream)
         if (c->ts[p]) { hipStreamSynchronize(c->ts[p]); hipStreamDestroy(c->ts[p]); }
         if (c->ev_mark[p]) hipEventDestroy(c->ev_mark[p]);
@@ -1034,8 +1094,10 @@ int dev_sync(Dev* c)
     HIPCHK(c, hipStreamSynchronize(c->stream));
     unsigned flags = 0;
     HIPCHK(c, hipMemcpy(&flags, c->d_err, sizeof(flags), hipMemcpyDeviceToHost));
-    if (flags) {
-        HIPCHK(c, hipMemset(c->d_err, 0, sizeof(unsigned)));
+    if (flags) {   // (on the main stream, which the next draw's path tracing waits for: not the null stream)
+        HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(unsigned), c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->mark_valid = false;
         if (flags & pt::E_STACK) return fail(c, PT_ERR_DATA, "BVH traversal needed more than stackLevels[28]");
     }
     return PT_OK;

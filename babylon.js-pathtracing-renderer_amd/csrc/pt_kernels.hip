@@ -189,6 +189,7 @@ __global__ __launch_bounds__(256) void pt_blend(BlendArgs a)
     const int band = blockIdx.y * a.num_parts + a.part;
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int r0 = band * kTile + (threadIdx.x >> 6);
+    if (a.cont_count && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.cont_count = 0u;   // (pt_cont has read it)
     if (x >= a.width) return;
     typedef float nt4 __attribute__((ext_vector_type(4)));
     nt4 rv[4], pv[4];
@@ -554,7 +555,8 @@ __global__ void pt_math_probe_kernel(int op, const float* x, const float* y, flo
     hipError_t pt_launch_trace_##W(int prog, int count, const pt::TraceArgs* a, dim3 grid, dim3 block, hipStream_t s); \
     hipError_t pt_launch_persist_##W(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x,   \
                                      unsigned n_wave_tiles, unsigned per_wave, unsigned refill, dim3 grid, dim3 block, \
-                                     hipStream_t s);
+                                     hipStream_t s);                                                                \
+    hipError_t pt_launch_cont_##W(int prog, const pt::TraceArgs* a, dim3 grid, hipStream_t s);
 PT_WALK_LAUNCHERS(ref)
 PT_WALK_LAUNCHERS(pairs)
 PT_WALK_LAUNCHERS(trail)
@@ -573,6 +575,19 @@ hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid
     case pt::WALK_REF: return pt_launch_trace_ref(prog, count, a, grid, block, s);
     case pt::WALK_PAIRS: return pt_launch_trace_pairs(prog, count, a, grid, block, s);
     case pt::WALK_TRAIL: return pt_launch_trace_trail(prog, count, a, grid, block, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// late-bounce compaction: pt_cont over the paths the draw's pt_trace stored (`waves` one-wave workgroups)
+hipError_t pt_launch_cont(int prog, const pt::TraceArgs* a, int waves, hipStream_t s)
+{
+    prog = pt::resolveProgram(prog, a->uses_albedo || a->uses_bump, a->bvh_walk);
+    const dim3 grid(waves);
+    switch (prog / pt::PROG_PAIRS) {
+    case pt::WALK_REF: return pt_launch_cont_ref(prog, a, grid, s);
+    case pt::WALK_PAIRS: return pt_launch_cont_pairs(prog, a, grid, s);
+    case pt::WALK_TRAIL: return pt_launch_cont_trail(prog, a, grid, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -188,14 +188,87 @@ PT_D bool bounceStep(const TraceArgs& a, Path& p, PState& s, G& g, f3& accum, fl
     return shadeStep<PROG, COUNT, G>(a, p, s, g, accum, h, cnt);
 }
 
+// ------------------------------------------------------------------------------ late-bounce compaction
+// A path's state between two bounces as a 64-B record (pt_cont): ray, throughput, rng / blue-noise state
+// (whose bits 24-30 carry the G-buffer sharpness and id, pt_program.h GOutLds), the bounce counters and
+// flags. The radiance so far is not stored: CalculateRadiance only ever assigns it when the path ends.
+// The G-buffer's normal, colour and id are final from bounce 2 on (the GLSL writes them at bounces 0 and 1).
+PT_D void contStore(const TraceArgs& a, unsigned slot, const Path& p, const PState& s)
+{
+    const unsigned bits = ((unsigned)s.diffuseCount & 0xffu) | (((unsigned)s.hitType & 0xffu) << 8) |
+                          (((unsigned)s.bounce & 0xffu) << 16) | (s.coat ? 1u << 24 : 0u) |
+                          (s.specular ? 1u << 25 : 0u) | (s.sampleLight ? 1u << 26 : 0u);
+    float4* r = a.cont_rec + 4ull * slot;
+    r[0] = make_float4(p.ro.x, p.ro.y, p.ro.z, p.rd.x);
+    r[1] = make_float4(p.rd.y, p.rd.z, s.mask.x, s.mask.y);
+    r[2] = make_float4(s.mask.z, s.roughness, __uint_as_float(p.s0), __uint_as_float(p.s1));
+    r[3] = make_float4(__uint_as_float(p.bn), __uint_as_float(bits), 0.0f, 0.0f);
+}
+PT_D void contLoad(const TraceArgs& a, unsigned slot, Path& p, PState& s)
+{
+    const float4* r = a.cont_rec + 4ull * slot;
+    const float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3];
+    p.ro = mk(r0.x, r0.y, r0.z); p.rd = mk(r0.w, r1.x, r1.y);
+    s.mask = mk(r1.z, r1.w, r2.x); s.roughness = r2.y;
+    p.s0 = __float_as_uint(r2.z); p.s1 = __float_as_uint(r2.w); p.bn = __float_as_uint(r3.x);
+    const unsigned bits = __float_as_uint(r3.y);
+    s.diffuseCount = (int)(bits & 0xffu);
+    s.hitType = (int)(signed char)((bits >> 8) & 0xffu);
+    s.bounce = (int)((bits >> 16) & 0xffu);
+    s.coat = (bits >> 24) & 1u; s.specular = (bits >> 25) & 1u; s.sampleLight = (bits >> 26) & 1u;
+}
+// the G-buffer of a continued path: only the sharpness can still change, in the same bits of Path::bn
+// as pt_trace keeps it (GOutLds)
+struct GBits {
+    static constexpr bool kColById = false;
+    uint32_t* bn;
+    PT_D void clear() {}
+    PT_D void pinCol(f3) {}
+    PT_D void setNrm(f3) {}
+    PT_D void setCol(f3) {}
+    PT_D void setId(float) {}
+    PT_D float id() const { return 0.0f; }
+    PT_D void setSharp(float v)
+    {
+        const unsigned code = v == 1.01f ? 1u : v == -1.0f ? 2u : 0u;
+        *bn = (*bn & ~(3u << 24)) | (code << 24);
+    }
+    PT_D float sharp() const
+    {
+        const unsigned code = (*bn >> 24) & 3u;
+        return code == 1u ? 1.01f : code == 2u ? -1.0f : 0.0f;
+    }
+};
+
+// CalculateRadiance's loop. With late-bounce compaction (a.cont_rec): after a bounce >= cont_bounce, when
+// at most cont_lanes of the wave's lanes are still looping (all at the same bounce: a ballot, wave-uniform),
+// they leave the loop together and store their paths for pt_cont; `slot` is then the record's index (-1:
+// the path ended here, or a helper lane outside the target, whose path no pixel needs - the 2x2
+// derivatives only read its G-buffer, final by then). Slots: one atomic per wave, a lane prefix (mbcnt)
+// over the ballot of the storing lanes.
 template <int PROG, bool COUNT, int LS, class G>
-PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_slot, unsigned deep, Cnt& cnt)
+PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_slot, unsigned deep, Cnt& cnt,
+                 bool inside, int& slot)
 {
     PState s;
     pathBegin(s, g);
     f3 accum = mk(0, 0, 0);
 #pragma unroll 1
-    while (bounceStep<PROG, COUNT, LS, G>(a, p, s, g, accum, lds, lane_slot, deep, cnt)) {}
+    while (bounceStep<PROG, COUNT, LS, G>(a, p, s, g, accum, lds, lane_slot, deep, cnt)) {
+        if (!COUNT && kHasMesh<PROG> && a.cont_rec && (unsigned)s.bounce >= a.cont_bounce &&
+            (unsigned)__popcll(__ballot(1)) <= a.cont_lanes) {
+            const unsigned long long st = __ballot(inside);
+            const int lead = __ffsll((long long)__ballot(1)) - 1;
+            unsigned base = 0;
+            if (__lane_id() == lead && st) base = atomicAdd(a.cont_count, (unsigned)__popcll(st));
+            base = __shfl(base, lead, 64);
+            if (inside) {
+                slot = (int)(base + (unsigned)__popcll(st & ((1ull << __lane_id()) - 1ull)));
+                contStore(a, (unsigned)slot, p, s);
+            }
+            break;
+        }
+    }
     return max3s(accum, 0.0f);
 }
 
@@ -263,8 +336,13 @@ PT_D bool tracePlace(const TraceArgs& a, int lane, TracePlace& pl)
         slot = K + g * 8u + r % T;
         wave = (int)(r / T);
     }
-    const unsigned tile = a.order ? a.order[slot] : slot;
-    if (slot < a.prio_tiles) __builtin_amdgcn_s_setprio(3);   // the critical path: issue first
+    unsigned rank = slot;   // the slot's place in the longest-first order
+    if (a.order_zig && slot >= K) {
+        const unsigned j = slot - K, m = ntiles - K;
+        rank = K + ((j & 1u) ? m - 1u - (j >> 1) : (j >> 1));
+    }
+    const unsigned tile = a.order ? a.order[rank] : slot;
+    if (rank < a.prio_tiles) __builtin_amdgcn_s_setprio(3);   // the critical path: issue first
     const int tx = (int)(tile % tiles_x);
     const unsigned bY = tile / tiles_x;
     // lane bits (x0, y0, x1, x2, y1, y2) of an 8x8 block, or (x0, y0, x1, y1) of a split tile's 4x4
@@ -324,10 +402,11 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     GOutLds<kTraceBlock, kGoutLdsOf<PROG>> gl{ (lds_float*)lds_gout, tid, gx, deep, a.spill_stride, &p.bn };
     gl.clear();   // pinned: the `out` parameters of CalculateRadiance start at 0 (also lanes without a path)
     f3 r = mk(0, 0, 0);
+    int slot = -1;   // late-bounce compaction: this lane's path record for pt_cont
     if (active) {
         cameraRay(a, px, py, p);
         PT_SEC(cnt, 0);
-        r = radiance<PROG, COUNT, kTraceBlock>(a, p, gl, lds_stack, tid, deep, cnt);
+        r = radiance<PROG, COUNT, kTraceBlock>(a, p, gl, lds_stack, tid, deep, cnt, px < a.width && py < a.height, slot);
     }
     PT_SEC(cnt, 4);
     const GOut g = gl.load([&](float id) {
@@ -393,7 +472,66 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     }
     if (!active || px >= a.width || py >= a.height) return;   // quad helper outside the target, idle lane
     const bool edge = colorDiff >= 1.0f || normalDiff >= 1.0f || objectDiff >= 1.0f;
-    radianceOut(a, (long long)py * a.width + px, r, g.sharp, edge);
+    const long long pi = (long long)py * a.width + px;
+    if (slot >= 0) {   // the path continues in pt_cont, which writes the pixel's radiance
+        a.cont_aux[slot] = (unsigned)pi | (edge ? 0x80000000u : 0u);
+        return;
+    }
+    radianceOut(a, pi, r, g.sharp, edge);
+}
+
+// Late-bounce compaction, the second half: the paths pt_trace stored (*cont_count of them) run their
+// remaining bounces packed into full waves. Each one-wave workgroup owns an equal share of the records
+// and refills its finished lanes from it (at least cont_refill of them at a time, or all when none is
+// left): a lane's path is one of the reference's per-pixel paths, resumed with exactly its state, so every
+// pixel's bits are those of the uncompacted kernel. It runs after its draw's pt_trace on the same side
+// stream, beside the next frame's pt_trace (frame overlap), so its own tail - a wave waits for the longest
+// chain of dependent walks among its paths - is filled by that frame's waves.
+template <int PROG>
+__global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_cont(TraceArgs a)
+{
+    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];
+    const unsigned lane = threadIdx.x;
+    const unsigned n = *a.cont_count;
+    const unsigned per = (n + gridDim.x - 1) / gridDim.x;
+    unsigned next = blockIdx.x * per;
+    const unsigned end = min(next + per, n);
+    if (next >= end) return;
+    const unsigned deep = blockIdx.x * kTraceBlock + lane;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
+    Path p;
+    p.bn = 0u;
+    PState s;
+    GBits g{ &p.bn };
+    f3 accum = mk(0, 0, 0);
+    unsigned slot = 0;
+    bool alive = false;
+    for (;;) {
+        const unsigned long long dead = __ballot(!alive);
+        const unsigned ndead = (unsigned)__popcll(dead);
+        if (next < end && (ndead >= a.cont_refill || ndead == 64u)) {
+            if (!alive) {
+                const unsigned q = next + (unsigned)__popcll(dead & below);
+                if (q < end) {
+                    slot = q;
+                    contLoad(a, q, p, s);
+                    accum = mk(0, 0, 0);
+                    alive = true;
+                }
+            }
+            next += ndead;
+        }
+        if (__ballot(alive) == 0ull) {
+            if (next >= end) break;
+            continue;
+        }
+        if (alive && !bounceStep<PROG, false, kTraceBlock>(a, p, s, g, accum, lds_stack, lane, deep, cnt)) {
+            const unsigned aux = a.cont_aux[slot];
+            radianceOut(a, (long long)(aux & 0x7fffffffu), max3s(accum, 0.0f), g.sharp(), (aux >> 31) != 0u);
+            alive = false;
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------ persistent paths

@@ -11,7 +11,8 @@ namespace pt {
     template __global__ void pt_trace<P, false>(TraceArgs);                                                 \
     template __global__ void pt_trace<P, true>(TraceArgs);                                                  \
     template __global__ void pt_persist<P, false>(TraceArgs, WfBufs, int, unsigned, unsigned, unsigned);    \
-    template __global__ void pt_persist<P, true>(TraceArgs, WfBufs, int, unsigned, unsigned, unsigned);
+    template __global__ void pt_persist<P, true>(TraceArgs, WfBufs, int, unsigned, unsigned, unsigned);    \
+    template __global__ void pt_cont<P>(TraceArgs);
 PT_WALK_PROGS(PT_INST)
 #undef PT_INST
 } // namespace pt
@@ -43,6 +44,18 @@ hipError_t PT_CAT(pt_launch_persist_, PT_WALK_NAME)(int prog, int count, const p
         if (count) hipLaunchKernelGGL((pt::pt_persist<P, true>), grid, block, 0, s, *a, *w, tiles_x, n_wave_tiles, per_wave, refill); \
         else hipLaunchKernelGGL((pt::pt_persist<P, false>), grid, block, 0, s, *a, *w, tiles_x, n_wave_tiles, per_wave, refill); \
         break;
+    switch (prog) {
+        PT_WALK_PROGS(PT_CASE)
+    default: return hipErrorInvalidValue;
+    }
+#undef PT_CASE
+    return hipGetLastError();
+}
+
+hipError_t PT_CAT(pt_launch_cont_, PT_WALK_NAME)(int prog, const pt::TraceArgs* a, dim3 grid, hipStream_t s)
+{
+    using namespace pt;
+#define PT_CASE(P) case P: hipLaunchKernelGGL((pt::pt_cont<P>), grid, dim3(kTraceBlock), 0, s, *a); break;
     switch (prog) {
         PT_WALK_PROGS(PT_CASE)
     default: return hipErrorInvalidValue;

@@ -561,6 +561,12 @@ def padded_bands(height, world):
     return ((nb + world - 1) // world) * world
 
 
+def bands_owned(height, world, rank):
+    """How many 16-row bands rank `rank` shades (pt_set_row_partition: bands b with b % world == rank)."""
+    nb = (height + BAND - 1) // BAND
+    return (nb - rank + world - 1) // world if rank < nb else 0
+
+
 def owned_rows(height, world, rank):
     """Rows of the frame this rank shades (bands b with b % world == rank)."""
     rows = []

@@ -57,6 +57,11 @@ PEAK_HBM_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-le
 # algorithmic bytes per counted event
 BYTES = {"node_fetches": 32, "leaf_tests": 48, "hit_lookups": 128, "rgba8_taps": 4, "hdr_taps": 16}
 PIXEL_IO = 32                  # previousBuffer texel read + accumulation texel write (+4 B blue noise = an rgba8 tap)
+# the walk's memory-pipe cost per lane-step at full waves (tools/ubench/td_width.hip,
+# profiles/r03_ubench_td_width.txt, 48 MiB table, 64 active lanes): a child-pair inner step (3 x dwordx4 +
+# dwordx2) 243.8 CU cycles per wave-step, a leaf step (3 x dwordx4) 189.2, at 2.4 GHz
+PIPE_CYC_PER_LANE_STEP = {"inner": 243.8 / 64, "leaf": 189.2 / 64}
+CUS, CLOCK_GHZ = 256, 2.4
 CONVERGED_SPP = 1024           # BASELINE configs[4]
 PG_TIMEOUT_S = 240             # N > 1: process-group / store timeout, well inside the driver's per-run budget
 PARITY_FRAMES = 2              # N > 1: recorded frames replayed after the timed region and compared with one GPU
@@ -90,6 +95,31 @@ def frame_size(n):
 
 def algorithmic_bytes(cnt):
     return sum(cnt[k] * b for k, b in BYTES.items()) + PIXEL_IO * cnt["paths"]
+
+
+def roofline_fracs(bytes_per_launch, counts, kernel_ms, frame_ms, traffic):
+    """The bounds the path-tracing kernel can be held against, as fractions:
+    frac          SURVEY §8d: reference-priced algorithmic bytes per launch / the launch's average HIP-event
+                  span / 8 TB/s (with frames overlapping, a span includes time shared with the neighbouring
+                  frames' launches);
+    frac_frame    the same bytes per displayed frame / ms_per_step (one launch per frame): the rate the
+                  job sustains;
+    counter_frac  the measured L2-to-fabric bytes (2 x FETCH_SIZE + WRITE_SIZE) per launch / ms_per_step / 8 TB/s
+                  (null without the PMC passes);
+    pipe_frac     the walk's lane-steps (node fetches / 2 inner steps + leaf tests) x the memory pipe's cost per
+                  lane-step at full waves (PIPE_CYC_PER_LANE_STEP) / (256 CUs x ms_per_step x 2.4 GHz): how busy
+                  the vector-memory path would be if every load instruction ran 64 lanes."""
+    peak = PEAK_HBM_GBS * 1e9
+    inner, leaf = counts["node_fetches"] / 2.0, counts["leaf_tests"]
+    pipe_cycles = inner * PIPE_CYC_PER_LANE_STEP["inner"] + leaf * PIPE_CYC_PER_LANE_STEP["leaf"]
+    return {"frac": round(bytes_per_launch / (kernel_ms * 1e-3) / peak, 4),
+            "frac_frame": round(bytes_per_launch / (frame_ms * 1e-3) / peak, 4),
+            "counter_frac": round(traffic / (frame_ms * 1e-3) / peak, 4) if traffic else None,
+            "pipe_frac": round(pipe_cycles / (CUS * frame_ms * 1e-3 * CLOCK_GHZ * 1e9), 4),
+            "pipe_model": {"lane_steps_per_launch": int(inner + leaf),
+                           "cycles_per_lane_step": {k: round(v, 3) for k, v in PIPE_CYC_PER_LANE_STEP.items()},
+                           "source": "tools/ubench/td_width.hip (profiles/r03_ubench_td_width.txt), 64 active lanes",
+                           "cus": CUS, "clock_ghz": CLOCK_GHZ}}
 
 
 def baseline_metric():
@@ -451,6 +481,53 @@ def multipart_child(args, world, W, Hh):
         return {"error": repr(e)[-300:]}
 
 
+# ------------------------------------------------------------------------------ N-GPU per-rank detail
+def rank_fields(rows):
+    """The line's `rank_detail` from one row per rank: [path-tracing kernel ms, halo exchange ms,
+    band gather ms, bands owned] (NaN = not measured). A load imbalance shows as a spread of the kernel
+    ms (and a slowest rank), a slow collective as its ms against the frame's."""
+    def mm(i):
+        v = [r[i] for r in rows if r[i] == r[i]]
+        return {"min": round(min(v), 4), "max": round(max(v), 4)} if v else None
+    k = [r[0] for r in rows]
+    return {"pathtrace_kernel_ms": mm(0), "halo_ms": mm(1), "gather_ms": mm(2),
+            "bands_per_rank": [int(r[3]) for r in rows],
+            "slowest_rank": int(max(range(len(rows)), key=lambda i: k[i])) if all(x == x for x in k) else None,
+            "method": ("path-tracing kernel: each rank's HIP-event windows in the timed region; halo exchange "
+                       "(RCCL P2P) and RGBA8 band gather: timed alone after the timed region, CUDA events around "
+                       "10 of each on the rank's stream")}
+
+
+def rank_detail(dist, torch, device, row):
+    """Every rank passes its row (rank_fields); rank 0 gets the assembled rank_detail, the others None."""
+    t = torch.tensor([float(x) for x in row], dtype=torch.float64, device=device)
+    g = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(g, t)
+    return rank_fields([x.cpu().tolist() for x in g]) if dist.get_rank() == 0 else None
+
+
+def collective_costs(dist, torch, bp, acc_t, halo, gather, world, rank, reps=10):
+    """N > 1, after the timed region: ms per halo exchange and per RGBA8 band gather, each timed alone
+    (CUDA events on this rank's stream around `reps` of them, every rank in step)."""
+    def timed(fn):
+        torch.cuda.synchronize()
+        dist.barrier()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps
+
+    def one_gather():
+        gather.target()
+        gather.submit()
+        gather.drain()
+
+    return (timed(lambda: bp.exchange_halos(dist, acc_t, world, rank, halo)), timed(one_gather))
+
+
 def nrank_check(dist, torch, engine, player, route, barrier_sync, gather, acc_t, workload, W, Hh, world, rank, device):
     """After the timed region: the first PARITY_FRAMES recorded frames (the first clears the history)
     through the N-rank route - path tracing of each rank's bands, RCCL halos, screenOutput of own
@@ -616,6 +693,14 @@ def main():
         check = nrank_check(dist, torch, engine, player, route, barrier_sync, gather, acc_t, args.workload, W, Hh,
                             world, rank, local)
 
+    detail = None
+    if dist is not None:
+        import babylon_pt as bp
+        halo_ms, gather_ms = (float("nan"), float("nan")) if args.no_output else \
+            collective_costs(dist, torch, bp, acc_t, halo, gather, world, rank)
+        detail = rank_detail(dist, torch, "cuda", [kernel_ms["pathtrace"], halo_ms, gather_ms,
+                                                   bp.bands_owned(Hh, world, rank)])
+
     ranks_seen = world
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
@@ -665,8 +750,12 @@ def main():
             pmc_note = "skipped (running under rocprofv3)"
         else:
             traffic, pmc_note = live_traffic(args.workload, W, Hh)
+    ms_per_step = elapsed / args.steps * 1e3
+    fr = roofline_fracs(bytes_per_launch, {k: v / nc for k, v in cnt.items()}, avg_launch_ms, ms_per_step, traffic)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 4), "traffic": traffic,
+                "frac": fr["frac"], "traffic": traffic,
+                "frac_frame": fr["frac_frame"], "counter_frac": fr["counter_frac"], "pipe_frac": fr["pipe_frac"],
+                "pipe_model": fr["pipe_model"],
                 "achieved_counter_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic else None,
                 "traffic_source": ("live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over 5 frames of this workload, "
                                    "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 B per launch (gfx950 correction)")
@@ -675,8 +764,10 @@ def main():
                 "counts_per_launch": {k: v / nc for k, v in cnt.items()},
                 "pricing": ("the reference's work (counting variant: full closest-hit walks and hit lookups); the "
                             "timed kernel ends shadow rays and eligible last segments at their first occluder "
-                            "(same image bits, DESIGN.md §6), so 'achieved' is reference work per second")}
-    ms_per_step = elapsed / args.steps * 1e3
+                            "(same image bits, DESIGN.md §6), so 'achieved' is reference work per second"),
+                "spans": ("frames overlap (pt_trace of frame k+1 runs beside frame k's, DESIGN.md §4): the HIP-event "
+                          "span of a launch includes time shared with its neighbours, so frac (per span) is below "
+                          "frac_frame (per displayed frame)")}
     ksum = sum(kernel_ms.values())
     line = {
         "metric": baseline_metric() if args.workload == "dragon" else METRICS[args.workload],
@@ -706,6 +797,8 @@ def main():
         "roofline": roofline,
     }
     line.update(anchors)
+    if detail is not None:
+        line["rank_detail"] = detail
     if check is not None:
         line["n_gpu_bitexact"] = check["n_gpu_bitexact"]
         line["n_gpu_check"] = check

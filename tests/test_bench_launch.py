@@ -137,3 +137,20 @@ def test_multipart_devices_fall_back_to_device_zero(monkeypatch):
     monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
     assert bench.multipart_devices(a) == [0, 1, 2]
     assert bench.multipart_devices(argparse.Namespace(devices="0,1", gpus=2)) == [0, 1]
+
+
+def test_roofline_fracs_formulas():
+    """The roofline's bounds (bench.roofline_fracs) on round 4's dragon stand-in numbers:
+    frac per HIP-event span, frac_frame per displayed frame, counter_frac from the PMC bytes, pipe_frac
+    from the walk's lane-steps priced by the td_width microbenchmark."""
+    sys.path.insert(0, ROOT)
+    import bench
+    counts = {"node_fetches": 90965227.8, "leaf_tests": 4669916.4}
+    f = bench.roofline_fracs(3285147468, counts, 0.9827, 1.0273, 1088e6)
+    assert f["frac"] == round(3285147468 / 0.9827e-3 / 8e12, 4) == 0.4179
+    assert f["frac_frame"] == round(3285147468 / 1.0273e-3 / 8e12, 4)
+    assert f["counter_frac"] == round(1088e6 / 1.0273e-3 / 8e12, 4)
+    cyc = 90965227.8 / 2 * 243.8 / 64 + 4669916.4 * 189.2 / 64
+    assert f["pipe_frac"] == round(cyc / (256 * 1.0273e-3 * 2.4e9), 4)
+    assert 0.29 < f["pipe_frac"] < 0.31 and f["pipe_model"]["lane_steps_per_launch"] == int(90965227.8 / 2 + 4669916.4)
+    assert bench.roofline_fracs(1.0, counts, 1.0, 1.0, None)["counter_frac"] is None

@@ -149,3 +149,44 @@ def test_pipelined_band_gather(tmp_path, world):
         for r in range(world):
             want[bp.owned_rows(h, world, r)] = [k % 251, r, 7, 255]
         assert np.array_equal(got[k], want), k
+
+
+def _worker_rank_detail(rank, world, port, out_path):
+    """bench.rank_detail over gloo: every rank hands in its own row, rank 0 gets the line's field."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import babylon_pt as bp
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        row = [0.5 + 0.25 * rank, 0.01 * (rank + 1), float("nan") if rank == 1 else 0.02, bp.bands_owned(2160, world, rank)]
+        d = bench.rank_detail(dist, torch, "cpu", row)
+        if rank == 0:
+            with open(out_path, "w") as f:
+                json.dump(d, f)
+        else:
+            assert d is None
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_rank_detail_fields(tmp_path, world):
+    """The N > 1 line's rank_detail (bench.py): min / max over ranks of the path-tracing kernel ms, the
+    halo and gather ms (unmeasured ranks left out), the bands each rank owns and the slowest rank."""
+    import json
+    out = str(tmp_path / "detail.json")
+    mp.spawn(_worker_rank_detail, args=(world, _free_port(), out), nprocs=world, join=True)
+    with open(out) as f:
+        d = json.load(f)
+    assert set(d) == {"pathtrace_kernel_ms", "halo_ms", "gather_ms", "bands_per_rank", "slowest_rank", "method"}
+    assert d["pathtrace_kernel_ms"] == {"min": 0.5, "max": 0.5 + 0.25 * (world - 1)}
+    assert d["slowest_rank"] == world - 1
+    assert d["halo_ms"] == {"min": 0.01, "max": round(0.01 * world, 4)}
+    assert d["gather_ms"] == {"min": 0.02, "max": 0.02}   # rank 1's NaN: not measured
+    nb = (2160 + 15) // 16
+    assert d["bands_per_rank"] == [len(range(r, nb, world)) for r in range(world)] and sum(d["bands_per_rank"]) == nb
+    assert all(isinstance(x, int) for x in d["bands_per_rank"]) and isinstance(d["method"], str)

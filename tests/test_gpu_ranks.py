@@ -127,3 +127,48 @@ def test_bench_n_gpu_check_with_torch_copies(workload, world, size):
     can2 = can.copy()
     can2[Hh - 1, W - 1, 0] ^= 4
     assert bench.compare_frames(can2, acc, *ref)["n_gpu_bitexact"] is False
+
+
+def test_rank_detail_filled_on_the_rehearsal():
+    """bench.py's N > 1 rank_detail filled on the one-GPU lease: each rehearsed rank's path-tracing
+    kernel ms from its own timing window, the halo exchange and the RGBA8 band gather (torch copies in
+    place of RCCL) timed with CUDA events on the shared stream, the bands each rank owns: the fields
+    bench.rank_fields assembles are all present and positive, and the bands add up to the frame."""
+    import torch
+    import bench
+    import babylon_pt as bp
+    world, W, Hh = 3, 480, 270
+    rk = _Ranks(world, W, Hh, lambda e, rt: bench.make_player(e, "bunny", W, Hh, rt)[0])
+    try:
+        player = rk.ranks[0][1]
+        for e, *_ in rk.ranks:
+            e.timing_begin()
+        for k in range(4):
+            rk.frame(player.synth_frame(k))
+        kernel = []
+        for e, *_ in rk.ranks:
+            ms, n = e.timing_end("gltf")
+            assert n == 4
+            kernel.append(ms / n)
+
+        def timed(fn):
+            s, t = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            fn()
+            t.record()
+            torch.cuda.synchronize()
+            return s.elapsed_time(t)
+
+        rows = []
+        for r, (e, _, acc, canvas, _) in enumerate(rk.ranks):
+            lo, hi = (r - 1) % world, (r + 1) % world
+            halo = timed(lambda: (_band_copy(acc, rk.ranks[lo][2], world, lo, slice(14, 16)),
+                                  _band_copy(acc, rk.ranks[hi][2], world, hi, slice(0, 2))))
+            gather = timed(lambda: _band_copy(rk.full_can, canvas, world, r))
+            rows.append([kernel[r], halo, gather, bp.bands_owned(Hh, world, r)])
+    finally:
+        rk.close()
+    d = bench.rank_fields(rows)
+    for k in ("pathtrace_kernel_ms", "halo_ms", "gather_ms"):
+        assert 0.0 < d[k]["min"] <= d[k]["max"], (k, d)
+    assert sum(d["bands_per_rank"]) == (Hh + 15) // 16 and d["slowest_rank"] in range(world)

@@ -5,12 +5,14 @@
 #
 # usage: tools/gpu_session.sh TAG STEP [STEP ...]
 #   smoke                      __graft_entry__.smoke()
-#   pytest[:K]                 the GPU parity suite (pytest -m gpu), or only the tests matching -k K
+#   pytest[:K[:ENV]]           the GPU parity suite (pytest -m gpu), or only the tests matching -k K (- = all),
+#                              under environment ENV (K=V[,K=V])
 #   exact                      the driver's exact bench command (bench.py --gpus 1 --steps 20 --warmup 5)
 #   bench:W[:ARGS]             bench.py --workload W (ARGS: extra bench flags, commas for spaces)
 #   envmx:ROUNDS:WLS:ENVS      path-tracing kernel ms per workload under environment settings, alternating
 #                              rounds (WLS comma-separated; ENVS '|'-separated, each space-free K=V[,K=V] or -)
-#   frames:ROUNDS:WLS:ENVS     the same for whole frames (bench.py --no-pmc --cpu-budget 0 per setting)
+#   frames:ROUNDS:WLS:ENVS     the same for whole frames (bench.py --no-pmc --cpu-budget 0 per setting);
+#                              a workload W@WxH runs at that frame size
 #   wavetime:LIB:WLS           wave timeline + CU occupancy of a -DPT_SECPROF build (tools/wavetime.py)
 #   prof                       rocprofv3 --kernel-trace --stats of the default bench
 #   pmc[:W]                    the five PMC passes over tools/prof_frames.py (default workload dragon)
@@ -33,8 +35,9 @@ for step in "$@"; do
   case $kind in
     smoke) run 300 "$LOG" python -u -c 'import __graft_entry__ as g; g.smoke()' ;;
     pytest)
-      if [ -n "$a1" ]; then run 900 "$LOG" python -u -m pytest tests -m gpu -q -rf -x --timeout 300 --timeout-method thread -k "$a1"
-      else run 900 "$LOG" python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread; fi ;;
+      envs=""; [ -n "$a2" ] && envs="${a2//,/ }"
+      if [ -n "$a1" ] && [ "$a1" != "-" ]; then run 900 "$LOG" env $envs python -u -m pytest tests -m gpu -q -rf -x --timeout 300 --timeout-method thread -k "$a1"
+      else run 900 "$LOG" env $envs python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread; fi ;;
     exact) run 300 "$LOG" python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench) run 400 "$LOG" python3 bench.py --workload "$a1" ${a2//,/ } ;;
     envmx|frames)
@@ -44,10 +47,11 @@ for step in "$@"; do
         for cfg in "${ENVS[@]}"; do
           for w in ${a2//,/ }; do
             envs=""; [ "$cfg" != "-" ] && envs="${cfg//,/ }"
+            wl=${w%@*}; sz=""; [ "$wl" != "$w" ] && sz="--size ${w#*@}"
             if [ $kind = envmx ]; then
-              res=$(env $envs timeout -k 10 120 python tools/exp_timing.py --workload "$w" --frames 30 --backends megakernel --layouts pairs --no-mesh-variant 2>&1 | tail -1); rc=$?
+              res=$(env $envs timeout -k 10 120 python tools/exp_timing.py --workload "$wl" --frames 30 --backends megakernel --layouts pairs --no-mesh-variant 2>&1 | tail -1); rc=$?
             else
-              res=$(env $envs timeout -k 10 200 python3 bench.py --workload "$w" --no-pmc --cpu-budget 0 --no-check --no-anchors 2>&1 | tail -1); rc=$?
+              res=$(env $envs timeout -k 10 200 python3 bench.py --workload "$wl" $sz --no-pmc --cpu-budget 0 --no-check --no-anchors 2>&1 | tail -1); rc=$?
             fi
             echo "r$r [$cfg] $w $res" >> "$LOG"
             [ $rc -ne 0 ] && break 3
