@@ -152,8 +152,9 @@ struct TraceArgs {
     const unsigned* order;
     unsigned* cost;
     unsigned prio_tiles;   // the first prio_tiles tiles of `order` (the slowest last frame) run at s_setprio 3
-    unsigned order_zig;    // 1: after the split tiles, slots take `order` from both ends alternately (slowest,
-                           // cheapest, 2nd slowest, ...): the slowest still start first, cheap tiles mix in
+    unsigned order_zig;    // 1: after the split tiles, runs of 8 slots (a tile per XCD) take `order` from both
+                           // ends in turn (8 slowest, 8 cheapest, ...): the slowest still start first, cheap
+                           // tiles mix in
     // *split (written by the previous pt_order_build; a multiple of 8): the first *split tiles of
     // `order` are shaded by 16 waves of 16 lanes (4x4 pixels) instead of 4 waves of 64 (pt_trace);
     // the grid carries padding rows for up to split_cap of them

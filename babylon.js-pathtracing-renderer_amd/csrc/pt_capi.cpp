@@ -1019,10 +1019,6 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
-    // split tiles shorten a launch's critical path; with frames overlapping, the next frame's waves fill
-    // it instead, and the split waves only cost issue (profiles/r05c_frames_ab.txt: helmet +2.6 %,
-    // sky + dragon +1 %, the rest +-0.3 % without them): off unless PT_SPLIT_TILES asks for them
-    if (c->overlap && !std::getenv("PT_SPLIT_TILES")) c->split_tiles = 0;
     if (const char* v = std::getenv("PT_CONT")) c->cont = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_CONT_BOUNCE")) c->cont_bounce = (unsigned)std::max(2, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_LANES")) c->cont_lanes = (unsigned)std::min(64, std::max(1, std::atoi(v)));

@@ -1,6 +1,6 @@
 // pt_kernels.hip — gfx950 kernels behind libpt.so.
 //
-//   pt_trace<PROG,COUNT>  the per-pixel path-tracing program (js/PathTracingCommon.js:1251-1358
+//   pt_trace<PROG,COUNT,CONT> the per-pixel path-tracing program (js/PathTracingCommon.js:1251-1358
 //                         with the Cornell / glTF scene shaders' SetupScene, SceneIntersect and
 //                         CalculateRadiance). One lane = one pixel = one path of <= 6 segments.
 //   pt_copy               screenCopy (js/PathTracingCommon.js:1-16), band-aware.

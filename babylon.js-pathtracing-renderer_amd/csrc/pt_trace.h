@@ -1,5 +1,5 @@
 // pt_trace.h — the per-pixel path-tracing kernels as templates over the program variant (the
-// scene program x PBR code x BVH walk): pt_trace<PROG,COUNT> (the megakernel) and pt_persist<PROG,COUNT>
+// scene program x PBR code x BVH walk): pt_trace<PROG,COUNT,CONT> (the megakernel; CONT: late-bounce compaction, with pt_cont) and pt_persist<PROG,COUNT>
 // (path regeneration). Instantiated per BVH walk in pt_trace_walk*.hip (one translation unit each, so
 // the variants compile in parallel); see pt_kernels.hip for the mapping onto CDNA4.
 #pragma once
@@ -246,7 +246,9 @@ struct GBits {
 // the path ended here, or a helper lane outside the target, whose path no pixel needs - the 2x2
 // derivatives only read its G-buffer, final by then). Slots: one atomic per wave, a lane prefix (mbcnt)
 // over the ballot of the storing lanes.
-template <int PROG, bool COUNT, int LS, class G>
+// CONT is a kernel variant of its own (pt_trace<PROG, false, true>): the check in the bounce loop costs the
+// 8-wave variants at their 64-VGPR budget even where it never fires (dragon stand-in +14 %, r05g)
+template <int PROG, bool COUNT, int LS, bool CONT, class G>
 PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_slot, unsigned deep, Cnt& cnt,
                  bool inside, int& slot)
 {
@@ -255,8 +257,7 @@ PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_s
     f3 accum = mk(0, 0, 0);
 #pragma unroll 1
     while (bounceStep<PROG, COUNT, LS, G>(a, p, s, g, accum, lds, lane_slot, deep, cnt)) {
-        if (!COUNT && kHasMesh<PROG> && a.cont_rec && (unsigned)s.bounce >= a.cont_bounce &&
-            (unsigned)__popcll(__ballot(1)) <= a.cont_lanes) {
+        if (CONT && (unsigned)s.bounce >= a.cont_bounce && (unsigned)__popcll(__ballot(1)) <= a.cont_lanes) {
             const unsigned long long st = __ballot(inside);
             const int lead = __ffsll((long long)__ballot(1)) - 1;
             unsigned base = 0;
@@ -337,9 +338,9 @@ PT_D bool tracePlace(const TraceArgs& a, int lane, TracePlace& pl)
         wave = (int)(r / T);
     }
     unsigned rank = slot;   // the slot's place in the longest-first order
-    if (a.order_zig && slot >= K) {
-        const unsigned j = slot - K, m = ntiles - K;
-        rank = K + ((j & 1u) ? m - 1u - (j >> 1) : (j >> 1));
+    if (a.order_zig && slot >= K) {   // runs of 8 (one tile per XCD): from the top and the bottom in turn
+        const unsigned j = slot - K, m = ntiles - K, g = j >> 3, t = (g >> 1) * 8u + (j & 7u);
+        rank = K + ((g & 1u) ? m - 1u - t : t);
     }
     const unsigned tile = a.order ? a.order[rank] : slot;
     if (rank < a.prio_tiles) __builtin_amdgcn_s_setprio(3);   // the critical path: issue first
@@ -360,9 +361,10 @@ PT_D bool tracePlace(const TraceArgs& a, int lane, TracePlace& pl)
     return true;
 }
 
-template <int PROG, bool COUNT>
+template <int PROG, bool COUNT, bool CONT>
 __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceArgs a)
 {
+    static_assert(!CONT || (kHasMesh<PROG> && !COUNT), "late-bounce compaction: mesh programs, timed kernels");
     // one LDS array: the stack levels (+ the scratch level, kScratchOf) or the trail walk's ring, then
     // the G-buffer's LDS fields (none in some variants: no zero-length array)
     __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock + (kGoutLdsOf<PROG> * kTraceBlock + 1) / 2];
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     if (active) {
         cameraRay(a, px, py, p);
         PT_SEC(cnt, 0);
-        r = radiance<PROG, COUNT, kTraceBlock>(a, p, gl, lds_stack, tid, deep, cnt, px < a.width && py < a.height, slot);
+        r = radiance<PROG, COUNT, kTraceBlock, CONT>(a, p, gl, lds_stack, tid, deep, cnt, px < a.width && py < a.height, slot);
     }
     PT_SEC(cnt, 4);
     const GOut g = gl.load([&](float id) {
@@ -473,7 +475,7 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     if (!active || px >= a.width || py >= a.height) return;   // quad helper outside the target, idle lane
     const bool edge = colorDiff >= 1.0f || normalDiff >= 1.0f || objectDiff >= 1.0f;
     const long long pi = (long long)py * a.width + px;
-    if (slot >= 0) {   // the path continues in pt_cont, which writes the pixel's radiance
+    if (CONT && slot >= 0) {   // the path continues in pt_cont, which writes the pixel's radiance
         a.cont_aux[slot] = (unsigned)pi | (edge ? 0x80000000u : 0u);
         return;
     }

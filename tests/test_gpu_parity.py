@@ -840,7 +840,6 @@ def test_order_build_beyond_register_tiles_is_a_permutation(monkeypatch):
     for lpt in ("1", "0"):
         monkeypatch.setenv("PT_LPT", lpt)
         monkeypatch.setenv("PT_SPLIT_ALWAYS", lpt)
-        monkeypatch.setenv("PT_SPLIT_TILES", "32")   # (off by default while frames overlap)
         e = bp.Engine(0)
         try:
             p = bp.StreamPlayer(e, meta, H.bluenoise(), H.texture_payloads(meta, mesh_arrays), W, Hh)
