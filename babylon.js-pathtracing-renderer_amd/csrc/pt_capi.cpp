@@ -143,13 +143,30 @@ struct Dev {
     bool mark_valid = false;      // mark[(mk_seq - 1) & 1] may gate the next draw (else it waits for a fresh mark)
     float4* rad_mem = nullptr;    // rad[2]: radiance + flag per pixel
     size_t rad_pixels = 0;
-    // late-bounce compaction of the megakernel's mesh draws (pt_trace -> pt_cont; PT_CONT=1 enables):
-    // per parity 64-B path records, their pixels and a counter; the bounce from which, and the live lanes
-    // at or below which, a wave hands its paths on; the refill batch and pt_cont's one-wave workgroups
-    bool cont = false;
+    // late-bounce compaction of the megakernel's mesh draws (pt_trace<P,false,true> -> pt_cont; PT_CONT:
+    // 0 off, 1 on, 2 auto - the default): per parity 64-B path records, their pixels and a counter; the
+    // bounce from which, and the live lanes at or below which, a wave hands its paths on; the refill batch
+    // and pt_cont's one-wave workgroups
+    int cont_mode = 2;
     void* cont_mem = nullptr;
     size_t cont_cap = 0;
-    unsigned cont_bounce = 3, cont_lanes = 16, cont_refill = 16, cont_waves = 2048;
+    unsigned cont_bounce = 2, cont_lanes = 32, cont_refill = 16, cont_waves = 2048;
+    // auto mode: compaction pays on the heavy 4K frames (sky + dragon +19 %, dragon stand-in +10 %) and
+    // costs elsewhere (bunny 4K -22 %, helmet -9 %, rank-sized frames -29 %: profiles/r05i_*), which
+    // the draw's arguments do not tell apart. So the draws of one target / program / partition time it:
+    // after kContSkip draws (one of them compacting, to warm it up), blocks of kContBlock draws with it on,
+    // off, off, on, each block bounded by an event on the main stream; once the last boundary has passed
+    // (a non-blocking query at later draws: no host wait), compaction stays on only if its faster block took
+    // 2 % less time than the faster block without. Same bits either way.
+    struct ContTune {
+        const void* target; int prog, part, parts, w, h;
+        int seen;                 // megakernel draws of this key so far
+        bool decided, choice;
+        float ms_on, ms_off;
+    } tune = {};
+    static constexpr int kContSkip = 4, kContBlock = 4, kContBlocks = 4;
+    size_t cont_auto_pixels = 4u << 20;   // (PT_CONT_AUTO_PIXELS)
+    hipEvent_t tune_ev[kContBlocks + 1] = {};
     pt::WfBufs gb = {};           // persistent backend: per-pixel G-buffer + radiance
     void* gb_mem = nullptr;
     size_t gb_pixels = 0;
@@ -503,6 +520,54 @@ void cont_args(Dev* c, int p, pt::TraceArgs& a)
     a.cont_refill = c->cont_refill;
 }
 
+// auto mode of late-bounce compaction (Dev::ContTune): whether this draw compacts
+int cont_decide(Dev* c, const DevTex* target, int prog, bool eligible, bool* on)
+{
+    *on = false;
+    if (!eligible || c->cont_mode == 0) return PT_OK;
+    // auto mode only tries it on frames of at least kContAutoPixels: it lost on every 1080p and smaller
+    // frame measured (dragon stand-in 1080p -15 %, rank-sized 3840x272 -37 %, helmet -6 %, r05k), and a
+    // trial's compacting blocks would cost those frames
+    if (c->cont_mode == 2 && (size_t)target->w * target->h < c->cont_auto_pixels) return PT_OK;
+    // the records first, so that no trial block pays for their allocation
+    if (int rc = cont_reserve(c, (size_t)target->w * target->h)) return rc;
+    if (c->cont_mode == 1) { *on = true; return PT_OK; }
+    auto& t = c->tune;
+    if (t.target != target || t.prog != prog || t.part != c->part || t.parts != c->num_parts || t.w != target->w ||
+        t.h != target->h)
+        t = Dev::ContTune{ target, prog, c->part, c->num_parts, target->w, target->h, 0, false, false, 0.0f, 0.0f };
+    const int i = t.seen++ - Dev::kContSkip;
+    if (t.decided) { *on = t.choice; return PT_OK; }
+    // one compacting draw before the trial: the first launch of a variant that needs more scratch than
+    // any before it waits for the device to drain while the runtime grows its scratch (r05k: the first
+    // trial block then took 2-8x the others)
+    if (i == -2 || i == -1) *on = true;   // (both side streams)
+    if (i < 0) return PT_OK;
+    constexpr int trial = Dev::kContBlocks * Dev::kContBlock;
+    if (i <= trial && i % Dev::kContBlock == 0) {   // a block boundary: the main stream's work before this draw
+        hipEvent_t& e = c->tune_ev[i / Dev::kContBlock];
+        if (!e) HIPCHK(c, hipEventCreate(&e));
+        HIPCHK(c, hipEventRecord(e, c->stream));
+    }
+    if (i < trial) {
+        const int b = i / Dev::kContBlock;
+        *on = b == 0 || b == Dev::kContBlocks - 1;   // on, off, off, on
+        return PT_OK;
+    }
+    if (hipEventQuery(c->tune_ev[Dev::kContBlocks]) != hipSuccess) return PT_OK;   // not yet: off meanwhile
+    t.ms_on = t.ms_off = 1e30f;   // the faster block of each mode (one stray block cannot decide)
+    for (int b = 0; b < Dev::kContBlocks; b++) {
+        float ms = 0.0f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->tune_ev[b], c->tune_ev[b + 1]));
+        float& m = b == 0 || b == Dev::kContBlocks - 1 ? t.ms_on : t.ms_off;
+        m = std::min(m, ms);
+    }
+    t.decided = true;
+    t.choice = t.ms_on < 0.98f * t.ms_off;
+    *on = t.choice;
+    return PT_OK;
+}
+
 // the side streams and events of frame overlap (created at the first overlapped draw)
 int overlap_init(Dev* c)
 {
@@ -782,7 +847,12 @@ int render_trace(DevFx* fx, DevTex* target)
     const bool lpt = c->lpt && !c->counting;
     const bool same = lpt && key.valid && key.n == n && key.target == target && key.prog == fx->prog &&
                       key.part == c->part && key.parts == c->num_parts && c->lpt_cap >= n;
-    const unsigned split = same ? (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u : 0u;   // the cap
+    // late-bounce compaction (cont_decide): when it is on, no split tiles - their 16-lane waves would hand
+    // their slowest paths to pt_cont at once (r05j: dragon stand-in 4K with both 2222 Mpaths/s, with
+    // compaction alone 2762)
+    bool cont = false;
+    if (int rc = cont_decide(c, target, fx->prog, mesh && !c->counting && !PT_SECPROF_BUILD, &cont)) return rc;
+    const unsigned split = same && !cont ? (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u : 0u;   // the cap
     const unsigned extra = 4u * pt::kSplitParts - 4u;   // more workgroups per split tile
     const int gy_grid = gy + (int)((extra * split + 4u * gx - 1) / (4u * gx));
     if (mesh) {
@@ -796,11 +866,7 @@ int render_trace(DevFx* fx, DevTex* target)
     }
     if (int rc = rad_reserve(c, (size_t)target->w * target->h)) return rc;
     a.rad = c->rad_mem + (size_t)par * c->rad_pixels;
-    const bool cont = c->cont && mesh && !c->counting && !PT_SECPROF_BUILD;
-    if (cont) {
-        if (int rc = cont_reserve(c, (size_t)target->w * target->h)) return rc;
-        cont_args(c, par, a);
-    }
+    if (cont) cont_args(c, par, a);
     if (lpt && c->lpt_cap < n) {
         if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
         HIPCHK(c, hipMalloc(&c->lpt_mem, (10 * n + 2) * sizeof(unsigned)));   // cost[2] | order[2] | split[2]
@@ -1019,11 +1085,12 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
-    if (const char* v = std::getenv("PT_CONT")) c->cont = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PT_CONT")) c->cont_mode = std::min(2, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_BOUNCE")) c->cont_bounce = (unsigned)std::max(2, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_LANES")) c->cont_lanes = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_REFILL")) c->cont_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_WAVES")) c->cont_waves = (unsigned)std::max(1, std::atoi(v));
+    if (const char* v = std::getenv("PT_CONT_AUTO_PIXELS")) c->cont_auto_pixels = (size_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_SPLIT_NEAR")) c->split_near = std::max(1, std::min(128, std::atoi(v)));
     if (const char* v = std::getenv("PT_SPLIT_ALWAYS")) c->split_dominance = std::atoi(v) ? 0u : 8u;
     if (const char* v = std::getenv("PT_BVH_LAYOUT"))   // reference | pairs | trail: the context's initial walk
@@ -1068,6 +1135,7 @@ void dev_ctx_destroy(Dev* c)
     if (c->mk_spill) hipFree(c->mk_spill);
     if (c->rad_mem) hipFree(c->rad_mem);
     if (c->cont_mem) hipFree(c->cont_mem);
+    for (auto& e : c->tune_ev) if (e) hipEventDestroy(e);
     for (int p = 0; p < 2; p++) {   // (every side-stream draw was waited for by a blend on the main stream)
         if (c->ts[p]) { hipStreamSynchronize(c->ts[p]); hipStreamDestroy(c->ts[p]); }
         if (c->ev_mark[p]) hipEventDestroy(c->ev_mark[p]);
@@ -1439,6 +1507,10 @@ int dev_queue_stats(Dev* c, uint32_t out[16])
     const int p = (int)(c->mk_seq & 1u);   // the tiles the next megakernel draw of the same grid splits
     if (c->lpt_mem && c->lpt_key[p].valid)
         HIPCHK(c, hipMemcpy(&out[7], c->lpt_split(p), sizeof(uint32_t), hipMemcpyDeviceToHost));
+    // late-bounce compaction: 0 off / undecided, 1 decided off, 2 decided on (auto), 3 forced on (PT_CONT=1);
+    // out[15]: the auto trial's ms with it on per ms with it off, x 1000
+    out[14] = c->cont_mode == 1 ? 3u : c->tune.decided ? (c->tune.choice ? 2u : 1u) : 0u;
+    out[15] = c->tune.decided && c->tune.ms_off > 0.0f ? (uint32_t)(1000.0f * c->tune.ms_on / c->tune.ms_off) : 0u;
     if (!c->wf_mem) return PT_OK;
     std::vector<unsigned> h(16 * pt::kShards);
     HIPCHK(c, hipMemcpy(h.data(), c->wf.cnt, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));

@@ -358,6 +358,12 @@ def single_gpu_run(engine, workload, W, Hh, warmup, steps, event_every, from_fra
     return player, program, tris, elapsed, km, n
 
 
+def compaction(engine):
+    """What the draws' late-bounce compaction auto mode decided (pt_queue_stats; synchronises)."""
+    q = engine.queue_stats()
+    return {"mode": q["late_bounce_compaction"], "trial_ms_on_per_off": q["compaction_trial_ratio"]}
+
+
 def run_anchors(engine, args):
     """Fields beside the N = 1 headline, measured in the same run on the same engine:
     dragon_4k_1gpu - the dragon stand-in at 3840x2160 (BASELINE configs[3] on one GPU: the anchor of
@@ -372,15 +378,18 @@ def run_anchors(engine, args):
     _, _, tris, el, km, n = single_gpu_run(engine, "dragon", 3840, 2160, 5, steps4k, max(1, steps4k // 10))
     out["dragon_4k_1gpu"] = {"value": round(3840 * 2160 * steps4k / el / 1e6, 2), "unit": "Mpaths/s",
                              "ms_per_step": round(el / steps4k * 1e3, 4), "steps": steps4k, "kernel_ms": km,
-                             "width": 3840, "height": 2160, "triangles": tris}
+                             "width": 3840, "height": 2160, "triangles": tris,
+                             "late_bounce_compaction": compaction(engine)}
     _, _, tris, el, km, n = single_gpu_run(engine, "bunny16", 1920, 1080, 10, args.steps, max(1, args.steps // 10))
     out["bunny16_1080p"] = {"value": round(1920 * 1080 * args.steps / el / 1e6, 2), "unit": "Mpaths/s",
                             "ms_per_step": round(el / args.steps * 1e3, 4), "steps": args.steps, "kernel_ms": km,
-                            "triangles": tris, "bvh_walk": engine.bvh_layout_used()}
+                            "triangles": tris, "bvh_walk": engine.bvh_layout_used(),
+                            "late_bounce_compaction": compaction(engine)}
     _, _, tris, el, km, n = single_gpu_run(engine, "sky_dragon", 3840, 2160, 0, CONVERGED_SPP, CONVERGED_SPP // 10,
                                            from_frame_one=True)
     conv = {"seconds": round(el, 4), "frames": CONVERGED_SPP, "ms_per_frame": round(el / CONVERGED_SPP * 1e3, 4),
             "mpaths_per_s": round(3840 * 2160 * CONVERGED_SPP / el / 1e6, 2), "kernel_ms": km, "measured": True,
+            "late_bounce_compaction": compaction(engine),
             "note": "frames 1..%d of the sky + dragon stand-in stream from a cleared history, 3840x2160, each "
                     "pathTracing + screenCopy + screenOutput; wall clock of the whole run" % CONVERGED_SPP}
     if args.dump_canvas:
@@ -708,6 +717,7 @@ def main():
         elapsed = float(t.item())
         ranks_seen = dist.get_world_size()
 
+    comp = compaction(engine)   # (before the counting replay: counting draws never compact)
     # algorithmic bytes of the measured launches: a counted (untimed) replay of the same frames
     engine.set_counting(True)
     engine.reset_counters()
@@ -794,6 +804,7 @@ def main():
         # time flags sampled kernel times inflated by them
         "kernel_sum_ms": round(ksum, 4),
         "kernel_sum_exceeds_step": bool(ksum > ms_per_step),
+        "late_bounce_compaction": comp,
         "roofline": roofline,
     }
     line.update(anchors)

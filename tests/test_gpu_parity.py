@@ -329,6 +329,65 @@ def test_overlapped_frames_observed_between_draws(engine, size):
 
 
 @pytest.mark.parametrize("layout", ["pairs", "trail"])
+def test_late_bounce_compaction_1080p_bitexact(monkeypatch, layout):
+    """Late-bounce compaction forced on (PT_CONT=1, from bounce 2 for waves with <= 32 live paths: the
+    pt_trace<P,false,true> variant stores them, pt_cont runs them packed on the draw's side stream):
+    the dragon stand-in's four recorded 1920x1080 frames, accumulation and canvas bit-exact."""
+    import babylon_pt as bp
+    monkeypatch.setenv("PT_CONT", "1")
+    e = bp.Engine(0)
+    try:
+        e.set_bvh_layout(layout)
+        meta = H.stream("gltf_bunny_1080p")
+        mesh = H.synthetic_dragon()
+        ref_acc, ref_can, _ = H.oracle_replay(meta, None, with_output=True, mesh=mesh)
+        got_acc, got_can, _ = _replay_gpu(e, meta, None, mesh=mesh)
+        assert e.queue_stats()["late_bounce_compaction"] == "on"
+    finally:
+        e.dispose()
+    for i, (ra, ga, rc, gc) in enumerate(zip(ref_acc, got_acc, ref_can, got_can)):
+        assert _bits_equal(ra, ga), "frame %d: %s" % (i, _diff_report(ra, ga))
+        assert _bits_equal(rc, gc), "frame %d canvas: %s" % (i, _diff_report(rc, gc))
+
+
+def test_late_bounce_compaction_auto_mode_bitexact(monkeypatch):
+    """The default auto mode (PT_CONT=2): after 4 draws of a target (the last two compacting, to warm the
+    variant up on both side streams), blocks of 4 draws with compaction
+    on, off, off, on are timed by events on the main stream and the faster mode is kept from the first
+    draw after the last block has completed (a non-blocking query). 30 frames of the dragon stand-in at
+    480x272 (a sync after frame 24, so the decision is taken by frame 25) accumulate the oracle's bits
+    whatever the draws chose, and the decision is reported. (Auto mode tries frames of >= 4 MP only;
+    PT_CONT_AUTO_PIXELS=0 lets this small frame run the trial.)"""
+    import copy
+    import babylon_pt as bp
+    monkeypatch.delenv("PT_CONT", raising=False)
+    monkeypatch.setenv("PT_CONT_AUTO_PIXELS", "0")
+    W, Hh = 480, 272
+    e = bp.Engine(0)
+    try:
+        meta = copy.deepcopy(H.stream("gltf_bunny_1080p"))
+        mesh = H.synthetic_dragon()
+        player = bp.StreamPlayer(e, meta, H.bluenoise(), H.texture_payloads(meta, mesh), W, Hh)
+        meta["frames"] = meta["frames"] + [player.synth_frame(k) for k in range(26)]
+        e.resize_canvas(W, Hh)
+        for i in range(len(meta["frames"])):
+            player.play_frame(i)
+            if i == 24:
+                e.sync()
+        e.sync()
+        got_acc = player.textures["pathTracingRenderTarget"].read()
+        got_can = e.read_canvas(W, Hh)
+        qs = e.queue_stats()
+    finally:
+        e.dispose()
+    ref_acc, ref_can, _ = H.oracle_replay(meta, None, W, Hh, with_output=True, mesh=mesh)
+    assert _bits_equal(ref_acc[-1], got_acc), _diff_report(ref_acc[-1], got_acc)
+    assert _bits_equal(ref_can[-1], got_can), _diff_report(ref_can[-1], got_can)
+    assert qs["late_bounce_compaction"] in ("auto: on", "auto: off"), qs
+    assert qs["compaction_trial_ratio"] and 0.2 < qs["compaction_trial_ratio"] < 5.0, qs
+
+
+@pytest.mark.parametrize("layout", ["pairs", "trail"])
 @pytest.mark.parametrize("workload", ["bunny", "dragon"])
 def test_timed_kernel_1080p_bitexact(engine, workload, layout):
     """The kernels the bench times, at the configurations it times them on: the production
