@@ -154,19 +154,21 @@ struct Dev {
     // auto mode: compaction pays on the heavy 4K frames (sky + dragon +19 %, dragon stand-in +10 %) and
     // costs elsewhere (bunny 4K -22 %, helmet -9 %, rank-sized frames -29 %: profiles/r05i_*), which
     // the draw's arguments do not tell apart. So the draws of one target / program / partition time it:
-    // after kContSkip draws (one of them compacting, to warm it up), blocks of kContBlock draws with it on,
-    // off, off, on, each block bounded by an event on the main stream; once the last boundary has passed
-    // (a non-blocking query at later draws: no host wait), compaction stays on only if its faster block took
-    // 2 % less time than the faster block without. Same bits either way.
+    // after kContSkip draws (the last two compacting, to warm it up on both side streams), blocks of
+    // kContBlock draws with it on, off, off, on, the last kContBlock - kContSettle draws of each timed by
+    // events on the main stream (the first ones carry the switch: orders from the other mode's costs);
+    // at the trial's end the host waits for it once, and compaction stays on only if its faster block
+    // took 2 % less time than the faster block without. Same bits either way.
     struct ContTune {
         const void* target; int prog, part, parts, w, h;
         int seen;                 // megakernel draws of this key so far
         bool decided, choice;
         float ms_on, ms_off;
     } tune = {};
-    static constexpr int kContSkip = 4, kContBlock = 4, kContBlocks = 4;
+    static constexpr int kContSkip = 4, kContBlock = 6, kContSettle = 2, kContBlocks = 4;
     size_t cont_auto_pixels = 4u << 20;   // (PT_CONT_AUTO_PIXELS)
-    hipEvent_t tune_ev[kContBlocks + 1] = {};
+    hipEvent_t tune_ev[2 * kContBlocks] = {};
+    int cont_last = 0;   // what the last megakernel draw did (cont_decide)
     pt::WfBufs gb = {};           // persistent backend: per-pixel G-buffer + radiance
     void* gb_mem = nullptr;
     size_t gb_pixels = 0;
@@ -521,7 +523,7 @@ void cont_args(Dev* c, int p, pt::TraceArgs& a)
 }
 
 // auto mode of late-bounce compaction (Dev::ContTune): whether this draw compacts
-int cont_decide(Dev* c, const DevTex* target, int prog, bool eligible, bool* on)
+int cont_decide_(Dev* c, const DevTex* target, int prog, bool eligible, bool* on)
 {
     *on = false;
     if (!eligible || c->cont_mode == 0) return PT_OK;
@@ -543,29 +545,47 @@ int cont_decide(Dev* c, const DevTex* target, int prog, bool eligible, bool* on)
     // trial block then took 2-8x the others)
     if (i == -2 || i == -1) *on = true;   // (both side streams)
     if (i < 0) return PT_OK;
-    constexpr int trial = Dev::kContBlocks * Dev::kContBlock;
-    if (i <= trial && i % Dev::kContBlock == 0) {   // a block boundary: the main stream's work before this draw
-        hipEvent_t& e = c->tune_ev[i / Dev::kContBlock];
-        if (!e) HIPCHK(c, hipEventCreate(&e));
-        HIPCHK(c, hipEventRecord(e, c->stream));
+    constexpr int B = Dev::kContBlock, trial = Dev::kContBlocks * B;
+    // each block's last B - kContSettle draws are timed: an event on the main stream (the work before
+    // the draw) at the block's offset kContSettle, and at the next block's start
+    const int b = i / B, o = i % B;
+    if (i <= trial && (o == 0 || o == Dev::kContSettle)) {
+        const int k = o == 0 ? 2 * b - 1 : 2 * b;   // (the first block's start is not timed)
+        if (k >= 0) {
+            hipEvent_t& e = c->tune_ev[k];
+            if (!e) HIPCHK(c, hipEventCreate(&e));
+            HIPCHK(c, hipEventRecord(e, c->stream));
+        }
     }
     if (i < trial) {
-        const int b = i / Dev::kContBlock;
         *on = b == 0 || b == Dev::kContBlocks - 1;   // on, off, off, on
         return PT_OK;
     }
-    if (hipEventQuery(c->tune_ev[Dev::kContBlocks]) != hipSuccess) return PT_OK;   // not yet: off meanwhile
-    t.ms_on = t.ms_off = 1e30f;   // the faster block of each mode (one stray block cannot decide)
-    for (int b = 0; b < Dev::kContBlocks; b++) {
+    // the trial's end: the host waits for it once (the draws it has already queued ran without), so that
+    // every later draw of this target takes the decision; the faster block of each mode decides (one
+    // stray block cannot)
+    HIPCHK(c, hipEventSynchronize(c->tune_ev[2 * Dev::kContBlocks - 1]));
+    t.ms_on = t.ms_off = 1e30f;
+    for (int k = 0; k < Dev::kContBlocks; k++) {
         float ms = 0.0f;
-        HIPCHK(c, hipEventElapsedTime(&ms, c->tune_ev[b], c->tune_ev[b + 1]));
-        float& m = b == 0 || b == Dev::kContBlocks - 1 ? t.ms_on : t.ms_off;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->tune_ev[2 * k], c->tune_ev[2 * k + 1]));
+        float& m = k == 0 || k == Dev::kContBlocks - 1 ? t.ms_on : t.ms_off;
         m = std::min(m, ms);
     }
     t.decided = true;
     t.choice = t.ms_on < 0.98f * t.ms_off;
     *on = t.choice;
     return PT_OK;
+}
+
+int cont_decide(Dev* c, const DevTex* target, int prog, bool eligible, bool* on)
+{
+    int rc = cont_decide_(c, target, prog, eligible, on);
+    // what the draw did, for pt_queue_stats: 0 off, 1 auto decided off, 2 auto decided on, 3 forced on,
+    // 4 auto trial
+    const bool tried = c->cont_mode == 2 && eligible && (size_t)target->w * target->h >= c->cont_auto_pixels;
+    c->cont_last = c->cont_mode == 1 && *on ? 3 : !tried ? 0 : c->tune.decided ? (c->tune.choice ? 2 : 1) : 4;
+    return rc;
 }
 
 // the side streams and events of frame overlap (created at the first overlapped draw)
@@ -1507,10 +1527,11 @@ int dev_queue_stats(Dev* c, uint32_t out[16])
     const int p = (int)(c->mk_seq & 1u);   // the tiles the next megakernel draw of the same grid splits
     if (c->lpt_mem && c->lpt_key[p].valid)
         HIPCHK(c, hipMemcpy(&out[7], c->lpt_split(p), sizeof(uint32_t), hipMemcpyDeviceToHost));
-    // late-bounce compaction: 0 off / undecided, 1 decided off, 2 decided on (auto), 3 forced on (PT_CONT=1);
-    // out[15]: the auto trial's ms with it on per ms with it off, x 1000
-    out[14] = c->cont_mode == 1 ? 3u : c->tune.decided ? (c->tune.choice ? 2u : 1u) : 0u;
-    out[15] = c->tune.decided && c->tune.ms_off > 0.0f ? (uint32_t)(1000.0f * c->tune.ms_on / c->tune.ms_off) : 0u;
+    // late-bounce compaction of the last megakernel draw: 0 off, 1 auto decided off, 2 auto decided on,
+    // 3 forced on (PT_CONT=1), 4 auto trial; out[15]: the auto trial's ms with it on per ms without, x 1000
+    out[14] = (uint32_t)c->cont_last;
+    out[15] = (c->cont_last == 1 || c->cont_last == 2) && c->tune.ms_off > 0.0f
+                  ? (uint32_t)(1000.0f * c->tune.ms_on / c->tune.ms_off) : 0u;
     if (!c->wf_mem) return PT_OK;
     std::vector<unsigned> h(16 * pt::kShards);
     HIPCHK(c, hipMemcpy(h.data(), c->wf.cnt, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));

@@ -352,11 +352,10 @@ def test_late_bounce_compaction_1080p_bitexact(monkeypatch, layout):
 
 def test_late_bounce_compaction_auto_mode_bitexact(monkeypatch):
     """The default auto mode (PT_CONT=2): after 4 draws of a target (the last two compacting, to warm the
-    variant up on both side streams), blocks of 4 draws with compaction
-    on, off, off, on are timed by events on the main stream and the faster mode is kept from the first
-    draw after the last block has completed (a non-blocking query). 30 frames of the dragon stand-in at
-    480x272 (a sync after frame 24, so the decision is taken by frame 25) accumulate the oracle's bits
-    whatever the draws chose, and the decision is reported. (Auto mode tries frames of >= 4 MP only;
+    variant up on both side streams), blocks of 6 draws with compaction on, off, off, on, the last 4 of
+    each timed by events on the main stream; at the 29th draw the host waits for the trial once and keeps
+    the faster mode. 30 frames of the dragon stand-in at 480x272 (a sync after frame 24 as well)
+    accumulate the oracle's bits whatever the draws chose, and the decision is reported. (Auto mode tries frames of >= 4 MP only;
     PT_CONT_AUTO_PIXELS=0 lets this small frame run the trial.)"""
     import copy
     import babylon_pt as bp
