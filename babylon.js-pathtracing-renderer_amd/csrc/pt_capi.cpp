@@ -126,21 +126,26 @@ struct Dev {
     pt::WfBufs wf = {};
     void* wf_mem = nullptr;
     size_t wf_pixels = 0, wf_slots = 0, wf_spill = 0;
-    float2* mk_spill = nullptr;   // megakernel BVH stack spill slabs (two: one per draw parity)
+    float2* mk_spill = nullptr;   // megakernel BVH stack spill slabs (one per buffer set of the overlap depth)
     size_t mk_spill_lanes = 0;
     // Frame overlap (megakernel draws; PT_OVERLAP=0 turns it off). pt_trace never reads the history:
     // it writes radiance + the pre-history flag to rad[parity], and pt_blend folds in the history on
-    // the main stream. So draw k's path tracing runs on side stream ts[k & 1] and waits only for the
+    // the main stream. So draw k's path tracing runs on side stream ts[k % depth] and waits only for the
     // main stream's state when draw k - 1 began (mark[(k - 1) & 1]: draw k - 2's blend, its order build,
     // the output that read rad / the order), never for draw k - 1's kernel: consecutive frames' path
     // tracing overlap, and the next frame's waves fill the launch tail of this one. Per parity: the
     // radiance buffer, the spill slab and the longest-first cost / order / split (each parity is its own
     // longest-first pipeline, draw k ordered by draw k - 2's costs).
     bool overlap = true;
-    hipStream_t ts[2] = {};
-    hipEvent_t ev_mark[2] = {}, ev_traced[2] = {};
-    unsigned mk_seq = 0;          // megakernel draws so far (parity = mk_seq & 1)
-    bool mark_valid = false;      // mark[(mk_seq - 1) & 1] may gate the next draw (else it waits for a fresh mark)
+    // Depth (PT_OVERLAP_DEPTH, 2 or 3): draw k uses buffer set k % depth and waits for the mark draw
+    // k - depth + 1 recorded (2: the previous draw's), so up to `depth` frames' path tracing are in flight.
+    static constexpr int kDepthMax = 3;
+    int depth = 2;
+    hipStream_t ts[kDepthMax] = {};
+    hipEvent_t ev_mark[kDepthMax] = {}, ev_traced[kDepthMax] = {};
+    unsigned mk_seq = 0;          // megakernel draws so far (buffer set = mk_seq % depth)
+    bool need_fresh = true;       // the next megakernel draw must wait for everything before it (a fresh mark)
+    unsigned mark_floor = 0;      // no draw waits for a mark older than draw mark_floor's
     float4* rad_mem = nullptr;    // rad[2]: radiance + flag per pixel
     size_t rad_pixels = 0;
     // late-bounce compaction of the megakernel's mesh draws (pt_trace<P,false,true> -> pt_cont; PT_CONT:
@@ -189,13 +194,13 @@ struct Dev {
     struct { bool on; unsigned n; const unsigned* cost; unsigned* order; unsigned* split; unsigned cap, dominance; int near; }
         pending_order = {};
     bool fuse_order = true;
-    unsigned* lpt_mem = nullptr;            // cost[2][4 * cap] | order[2][cap] | split[2]
+    unsigned* lpt_mem = nullptr;            // cost[kDepthMax][4 * cap] | order[kDepthMax][cap] | split[kDepthMax]
     size_t lpt_cap = 0;
     struct LptKey { bool valid; size_t n; const void* target; int prog, part, parts; };
-    LptKey lpt_key[2] = {};                 // what cost[p] / order[p] were last written for
+    LptKey lpt_key[kDepthMax] = {};         // what cost[p] / order[p] were last written for
     unsigned* lpt_cost(int p) const { return lpt_mem + 4 * lpt_cap * p; }
-    unsigned* lpt_order(int p) const { return lpt_mem + 8 * lpt_cap + lpt_cap * p; }
-    unsigned* lpt_split(int p) const { return lpt_mem + 10 * lpt_cap + p; }
+    unsigned* lpt_order(int p) const { return lpt_mem + 4 * lpt_cap * kDepthMax + lpt_cap * p; }
+    unsigned* lpt_split(int p) const { return lpt_mem + 5 * lpt_cap * kDepthMax + p; }
     // per-draw events for pt_last_render_ms: off until its first call (or PT_DRAW_EVENTS=1). Each
     // hipEventRecord costs ~5 us of stream time between two kernels on MI355X (r02h: two pairs per
     // frame were +19 us per frame, +1.7 % dragon stand-in, +3.8 % bunny)
@@ -474,9 +479,9 @@ int spill_reserve(Dev* c, size_t lanes)
     if (lanes <= c->mk_spill_lanes) return PT_OK;
     if (c->mk_spill) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->mk_spill)); c->mk_spill = nullptr; }
     c->mk_spill_lanes = 0;
-    HIPCHK(c, hipMalloc(&c->mk_spill, 2 * lanes * kSpillPerLane * sizeof(float2)));
+    HIPCHK(c, hipMalloc(&c->mk_spill, (size_t)c->depth * lanes * kSpillPerLane * sizeof(float2)));
     c->mk_spill_lanes = lanes;
-    c->mark_valid = false;   // new memory: the next draw waits for everything before it
+    c->need_fresh = true;   // new memory: the next draw waits for everything before it
     return PT_OK;
 }
 float2* spill_slab(Dev* c, int p) { return c->mk_spill + (size_t)p * c->mk_spill_lanes * kSpillPerLane; }
@@ -487,9 +492,9 @@ int rad_reserve(Dev* c, size_t pixels)
     if (pixels <= c->rad_pixels) return PT_OK;
     if (c->rad_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->rad_mem)); c->rad_mem = nullptr; }
     c->rad_pixels = 0;
-    HIPCHK(c, hipMalloc(&c->rad_mem, 2 * pixels * sizeof(float4)));
+    HIPCHK(c, hipMalloc(&c->rad_mem, (size_t)c->depth * pixels * sizeof(float4)));
     c->rad_pixels = pixels;
-    c->mark_valid = false;
+    c->need_fresh = true;
     return PT_OK;
 }
 
@@ -501,13 +506,13 @@ int cont_reserve(Dev* c, size_t paths)
     if (c->cont_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->cont_mem)); c->cont_mem = nullptr; }
     c->cont_cap = 0;
     const size_t per = paths * 64 + ((paths * 4 + 255) & ~(size_t)255) + 256;
-    HIPCHK(c, hipMalloc(&c->cont_mem, 2 * per));
+    HIPCHK(c, hipMalloc(&c->cont_mem, (size_t)c->depth * per));
     // on the main stream (hipMemset would go to the null stream, which the non-blocking side streams do
     // not wait for: the next draw's atomics raced with it); the next draw's path tracing waits for a mark
     // recorded after it
-    HIPCHK(c, hipMemsetAsync(c->cont_mem, 0, 2 * per, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->cont_mem, 0, (size_t)c->depth * per, c->stream));
     c->cont_cap = paths;
-    c->mark_valid = false;
+    c->need_fresh = true;
     return PT_OK;
 }
 void cont_args(Dev* c, int p, pt::TraceArgs& a)
@@ -592,7 +597,7 @@ int cont_decide(Dev* c, const DevTex* target, int prog, bool eligible, bool* on)
 int overlap_init(Dev* c)
 {
     if (c->ts[0]) return PT_OK;
-    for (int p = 0; p < 2; p++) {
+    for (int p = 0; p < c->depth; p++) {
         HIPCHK(c, hipStreamCreateWithFlags(&c->ts[p], hipStreamNonBlocking));
         HIPCHK(c, hipEventCreateWithFlags(&c->ev_mark[p], hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&c->ev_traced[p], hipEventDisableTiming));
@@ -844,7 +849,7 @@ int render_trace(DevFx* fx, DevTex* target)
     if (c->backend != PT_BACKEND_MEGAKERNEL || gy <= 0) {
         // the wavefront / persistent schedules: on the main stream, their finish pass accumulating;
         // the next megakernel draw waits for all of it (they share the spill slab)
-        if (c->backend != PT_BACKEND_MEGAKERNEL) c->mark_valid = false;
+        if (c->backend != PT_BACKEND_MEGAKERNEL) c->need_fresh = true;
         int rc = begin_draw(c, fx->prog);
         if (rc) return rc;
         if (gy > 0 && c->backend == PT_BACKEND_WAVEFRONT) {
@@ -858,8 +863,8 @@ int render_trace(DevFx* fx, DevTex* target)
         return end_draw(c, fx->prog);
     }
 
-    // ---- the megakernel: draw k = mk_seq uses the buffers of parity k & 1
-    const int par = (int)(c->mk_seq & 1u);
+    // ---- the megakernel: draw k = mk_seq uses buffer set k % depth
+    const int par = (int)(c->mk_seq % (unsigned)c->depth);
     // longest-first: the wave durations of draw k - 2 (same parity) order this draw's workgroups when it
     // drew the same grid, target and program; split tiles take 12 more workgroups each, in padding rows
     const size_t n = (size_t)gx * gy;   // 16x16 tiles
@@ -889,10 +894,10 @@ int render_trace(DevFx* fx, DevTex* target)
     if (cont) cont_args(c, par, a);
     if (lpt && c->lpt_cap < n) {
         if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
-        HIPCHK(c, hipMalloc(&c->lpt_mem, (10 * n + 2) * sizeof(unsigned)));   // cost[2] | order[2] | split[2]
+        HIPCHK(c, hipMalloc(&c->lpt_mem, (5 * n + 1) * Dev::kDepthMax * sizeof(unsigned)));   // cost | order | split
         c->lpt_cap = n;
-        c->mark_valid = false;
-        c->lpt_key[0].valid = c->lpt_key[1].valid = false;
+        c->need_fresh = true;
+        for (auto& k : c->lpt_key) k.valid = false;
     }
     // where the path tracing runs: a side stream gated by the main stream's state when the previous
     // megakernel draw began (or now: the first draw, after another schedule or a stream switch, with
@@ -903,12 +908,16 @@ int render_trace(DevFx* fx, DevTex* target)
     hipStream_t ts = c->stream;
     if (overlap) {
         if (int rc = overlap_init(c)) return rc;
+        const unsigned k = c->mk_seq, D = (unsigned)c->depth;
+        if (c->need_fresh) { c->mark_floor = k; c->need_fresh = false; }
         HIPCHK(c, hipEventRecord(c->ev_mark[par], c->stream));
         ts = c->ts[par];
-        HIPCHK(c, hipStreamWaitEvent(ts, c->mark_valid ? c->ev_mark[par ^ 1] : c->ev_mark[par], 0));
-        c->mark_valid = true;
+        // the mark of draw k - depth + 1 (its state: draw k - depth's blend, order build and output), or
+        // of the oldest draw after everything this draw must wait for
+        const unsigned w = k + 1 >= D ? std::max(k + 1 - D, c->mark_floor) : c->mark_floor;
+        HIPCHK(c, hipStreamWaitEvent(ts, c->ev_mark[w % D], 0));
     } else {
-        c->mark_valid = false;
+        c->need_fresh = true;
     }
     if (lpt) {
         if (!same) HIPCHK(c, hipMemsetAsync(c->lpt_cost(par), 0, 4 * n * sizeof(unsigned), ts));   // costs start afresh
@@ -1105,6 +1114,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PT_OVERLAP_DEPTH")) c->depth = std::min(Dev::kDepthMax, std::max(2, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT")) c->cont_mode = std::min(2, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_BOUNCE")) c->cont_bounce = (unsigned)std::max(2, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_LANES")) c->cont_lanes = (unsigned)std::min(64, std::max(1, std::atoi(v)));
@@ -1156,7 +1166,7 @@ void dev_ctx_destroy(Dev* c)
     if (c->rad_mem) hipFree(c->rad_mem);
     if (c->cont_mem) hipFree(c->cont_mem);
     for (auto& e : c->tune_ev) if (e) hipEventDestroy(e);
-    for (int p = 0; p < 2; p++) {   // (every side-stream draw was waited for by a blend on the main stream)
+    for (int p = 0; p < Dev::kDepthMax; p++) {   // (every side-stream draw was waited for by a blend on the main stream)
         if (c->ts[p]) { hipStreamSynchronize(c->ts[p]); hipStreamDestroy(c->ts[p]); }
         if (c->ev_mark[p]) hipEventDestroy(c->ev_mark[p]);
         if (c->ev_traced[p]) hipEventDestroy(c->ev_traced[p]);
@@ -1181,7 +1191,7 @@ int dev_sync(Dev* c)
     if (flags) {   // (on the main stream, which the next draw's path tracing waits for: not the null stream)
         HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(unsigned), c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        c->mark_valid = false;
+        c->need_fresh = true;
         if (flags & pt::E_STACK) return fail(c, PT_ERR_DATA, "BVH traversal needed more than stackLevels[28]");
     }
     return PT_OK;
@@ -1418,7 +1428,7 @@ int dev_set_stream(Dev* c, void* stream)
     if (int rc = flush_order(c)) return rc;        // on the stream its draw ran on
     HIPCHK(c, hipStreamSynchronize(c->stream));   // work already queued finishes first
     c->stream = stream ? (hipStream_t)stream : c->own_stream;
-    c->mark_valid = false;   // the next megakernel draw waits for the new stream's state
+    c->need_fresh = true;   // the next megakernel draw waits for the new stream's state
     return PT_OK;
 }
 
@@ -1524,7 +1534,7 @@ int dev_queue_stats(Dev* c, uint32_t out[16])
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = flush_order(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    const int p = (int)(c->mk_seq & 1u);   // the tiles the next megakernel draw of the same grid splits
+    const int p = (int)(c->mk_seq % (unsigned)c->depth);   // the tiles the next megakernel draw of the same grid splits
     if (c->lpt_mem && c->lpt_key[p].valid)
         HIPCHK(c, hipMemcpy(&out[7], c->lpt_split(p), sizeof(uint32_t), hipMemcpyDeviceToHost));
     // late-bounce compaction of the last megakernel draw: 0 off, 1 auto decided off, 2 auto decided on,

@@ -97,7 +97,10 @@ def algorithmic_bytes(cnt):
     return sum(cnt[k] * b for k, b in BYTES.items()) + PIXEL_IO * cnt["paths"]
 
 
-def roofline_fracs(bytes_per_launch, counts, kernel_ms, frame_ms, traffic):
+SIMDS, VALU_CYC = 1024, 2   # 4 SIMDs per CU; a wave64 VALU instruction issues over 2 cycles (MI355X_MICROARCH.md)
+
+
+def roofline_fracs(bytes_per_launch, counts, kernel_ms, frame_ms, traffic, valu=None):
     """The bounds the path-tracing kernel can be held against, as fractions:
     frac          SURVEY §8d: reference-priced algorithmic bytes per launch / the launch's average HIP-event
                   span / 8 TB/s (with frames overlapping, a span includes time shared with the neighbouring
@@ -108,7 +111,9 @@ def roofline_fracs(bytes_per_launch, counts, kernel_ms, frame_ms, traffic):
                   (null without the PMC passes);
     pipe_frac     the walk's lane-steps (node fetches / 2 inner steps + leaf tests) x the memory pipe's cost per
                   lane-step at full waves (PIPE_CYC_PER_LANE_STEP) / (256 CUs x ms_per_step x 2.4 GHz): how busy
-                  the vector-memory path would be if every load instruction ran 64 lanes."""
+                  the vector-memory path would be if every load instruction ran 64 lanes;
+    valu_frac     the kernel's VALU wave-instructions per launch (PMC SQ_INSTS_VALU) x 2 issue cycles / (1024 SIMDs
+                  x ms_per_step x 2.4 GHz): how busy the SIMDs' vector issue is (null without the PMC passes)."""
     peak = PEAK_HBM_GBS * 1e9
     inner, leaf = counts["node_fetches"] / 2.0, counts["leaf_tests"]
     pipe_cycles = inner * PIPE_CYC_PER_LANE_STEP["inner"] + leaf * PIPE_CYC_PER_LANE_STEP["leaf"]
@@ -116,6 +121,7 @@ def roofline_fracs(bytes_per_launch, counts, kernel_ms, frame_ms, traffic):
             "frac_frame": round(bytes_per_launch / (frame_ms * 1e-3) / peak, 4),
             "counter_frac": round(traffic / (frame_ms * 1e-3) / peak, 4) if traffic else None,
             "pipe_frac": round(pipe_cycles / (CUS * frame_ms * 1e-3 * CLOCK_GHZ * 1e9), 4),
+            "valu_frac": round(valu * VALU_CYC / (SIMDS * frame_ms * 1e-3 * CLOCK_GHZ * 1e9), 4) if valu else None,
             "pipe_model": {"lane_steps_per_launch": int(inner + leaf),
                            "cycles_per_lane_step": {k: round(v, 3) for k, v in PIPE_CYC_PER_LANE_STEP.items()},
                            "source": "tools/ubench/td_width.hip (profiles/r03_ubench_td_width.txt), 64 active lanes",
@@ -183,24 +189,25 @@ def cpu_baseline(workload, budget):
 
 # ------------------------------------------------------------------------------ live PMC traffic
 def live_traffic(workload, W, Hh, frames=5):
-    """L2-to-fabric bytes per launch of the path-tracing kernel, measured now: two rocprofv3 --pmc
-    passes (FETCH_SIZE and WRITE_SIZE need 3 + 2 of the 4 TCC slots, so one pass each) over
-    tools/prof_frames.py rendering `frames` frames of this workload. gfx950 correction
-    (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 128-B read requests at 64 B -> doubled; KiB -> B."""
+    """L2-to-fabric bytes and vector-ALU instructions per launch of the path-tracing kernel, measured
+    now: three rocprofv3 --pmc passes (FETCH_SIZE and WRITE_SIZE need 3 + 2 of the 4 TCC slots, so one
+    pass each; SQ_INSTS_VALU) over tools/prof_frames.py rendering `frames` frames of this workload.
+    gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 128-B read requests at 64 B ->
+    doubled; KiB -> B. Returns (bytes, VALU wave-instructions, note)."""
     exe = shutil.which("rocprofv3")
     if not exe:
-        return None, "rocprofv3 not found"
+        return None, None, "rocprofv3 not found"
     vals = {}
     tmp = tempfile.mkdtemp(prefix="pt_pmc_", dir="/tmp")
     try:
-        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"):
             out = os.path.join(tmp, ctr)
             cmd = ["timeout", "-s", "KILL", "90", exe, "--kernel-trace", "--pmc", ctr, "--output-format", "csv",
                    "-d", out, "-o", "run", "--", sys.executable, os.path.join(ROOT, "tools", "prof_frames.py"),
                    "--workload", workload, "--frames", str(frames), "--width", str(W), "--height", str(Hh)]
             r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), capture_output=True, text=True)
             if r.returncode != 0:
-                return None, "rocprofv3 --pmc %s exited %d" % (ctr, r.returncode)
+                return None, None, "rocprofv3 --pmc %s exited %d" % (ctr, r.returncode)
             per = []
             for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
                 with open(path) as f:
@@ -208,11 +215,11 @@ def live_traffic(workload, W, Hh, frames=5):
                         if "pt_trace<" in row["Kernel_Name"] and row["Counter_Name"] == ctr:
                             per.append(float(row["Counter_Value"]))
             if not per:
-                return None, "no %s samples for pt_trace" % ctr
+                return None, None, "no %s samples for pt_trace" % ctr
             vals[ctr] = sum(per) / len(per)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
-    return int((2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), None
+    return int((2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), vals["SQ_INSTS_VALU"], None
 
 
 # ------------------------------------------------------------------------------ launch
@@ -754,19 +761,21 @@ def main():
              "bunny16": "bunny_split16"}
     workload = "%s_%s_%dx%d" % (program, wname[args.workload], W, Hh)
     kernel = kernel_name(layout, program, args.workload)
-    traffic, pmc_note = None, "N > 1: not collected"
+    traffic, valu, pmc_note = None, None, "N > 1: not collected"
     if world == 1:
         if args.no_pmc:
             pmc_note = "skipped (--no-pmc)"
         elif any(k.startswith("ROCPROF") for k in os.environ):
             pmc_note = "skipped (running under rocprofv3)"
         else:
-            traffic, pmc_note = live_traffic(args.workload, W, Hh)
+            traffic, valu, pmc_note = live_traffic(args.workload, W, Hh)
     ms_per_step = elapsed / args.steps * 1e3
-    fr = roofline_fracs(bytes_per_launch, {k: v / nc for k, v in cnt.items()}, avg_launch_ms, ms_per_step, traffic)
+    fr = roofline_fracs(bytes_per_launch, {k: v / nc for k, v in cnt.items()}, avg_launch_ms, ms_per_step, traffic,
+                        valu)
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                 "frac": fr["frac"], "traffic": traffic,
                 "frac_frame": fr["frac_frame"], "counter_frac": fr["counter_frac"], "pipe_frac": fr["pipe_frac"],
+                "valu_frac": fr["valu_frac"], "valu_insts_per_launch": int(valu) if valu else None,
                 "pipe_model": fr["pipe_model"],
                 "achieved_counter_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic else None,
                 "traffic_source": ("live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over 5 frames of this workload, "

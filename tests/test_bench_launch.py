@@ -154,3 +154,6 @@ def test_roofline_fracs_formulas():
     assert f["pipe_frac"] == round(cyc / (256 * 1.0273e-3 * 2.4e9), 4)
     assert 0.29 < f["pipe_frac"] < 0.31 and f["pipe_model"]["lane_steps_per_launch"] == int(90965227.8 / 2 + 4669916.4)
     assert bench.roofline_fracs(1.0, counts, 1.0, 1.0, None)["counter_frac"] is None
+    assert bench.roofline_fracs(1.0, counts, 1.0, 1.0, None)["valu_frac"] is None
+    v = bench.roofline_fracs(3285147468, counts, 0.9827, 0.8766, 1.036e9, 7.19e8)["valu_frac"]
+    assert v == round(7.19e8 * 2 / (1024 * 0.8766e-3 * 2.4e9), 4) and 0.6 < v < 0.75
