@@ -131,7 +131,7 @@ struct TraceArgs {
     // packed into full waves (cont_rec NULL: off)
     float4* cont_rec;
     unsigned* cont_aux;     // per record: the pixel (py * width + px) | the 2x2 edge flag << 31
-    unsigned* cont_count;   // records stored by this draw (zeroed by the draw's pt_blend for the next user)
+    unsigned* cont_count;   // [0] records stored by this draw, [1] pt_cont's queue head (both zeroed by the draw's pt_blend)
     unsigned cont_bounce, cont_lanes, cont_refill;
     Tex8 bluenoise;
     const float4* aabb;
@@ -195,7 +195,7 @@ struct WfBufs {
     // packed into full waves (cont_rec NULL: off)
     float4* cont_rec;
     unsigned* cont_aux;     // per record: the pixel (py * width + px) | the 2x2 edge flag << 31
-    unsigned* cont_count;   // records stored by this draw (zeroed by the draw's pt_blend for the next user)
+    unsigned* cont_count;   // [0] records stored by this draw, [1] pt_cont's queue head (both zeroed by the draw's pt_blend)
     unsigned cont_bounce, cont_lanes, cont_refill;            // per pixel: CalculateRadiance() result
     float2* spill;          // BVH stack levels >= kStackLds: [level][persistent lane]
     unsigned* cnt;          // [b * kShards + s]: live paths of shard s entering bounce b (b = 0..6)

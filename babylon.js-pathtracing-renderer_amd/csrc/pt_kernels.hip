@@ -189,7 +189,7 @@ __global__ __launch_bounds__(256) void pt_blend(BlendArgs a)
     const int band = blockIdx.y * a.num_parts + a.part;
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int r0 = band * kTile + (threadIdx.x >> 6);
-    if (a.cont_count && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.cont_count = 0u;   // (pt_cont has read it)
+    if (a.cont_count && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) a.cont_count[threadIdx.x] = 0u;   // counter, queue head (pt_cont is done)
     if (x >= a.width) return;
     typedef float nt4 __attribute__((ext_vector_type(4)));
     nt4 rv[4], pv[4];

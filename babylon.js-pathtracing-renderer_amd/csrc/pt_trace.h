@@ -482,10 +482,10 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_trace(TraceAr
     radianceOut(a, pi, r, g.sharp, edge);
 }
 
-// Late-bounce compaction, the second half: the paths pt_trace stored (*cont_count of them) run their
-// remaining bounces packed into full waves. Each one-wave workgroup owns an equal share of the records
-// and refills its finished lanes from it (at least cont_refill of them at a time, or all when none is
-// left): a lane's path is one of the reference's per-pixel paths, resumed with exactly its state, so every
+// Late-bounce compaction, the second half: the paths pt_trace stored (cont_count[0] of them) run their
+// remaining bounces packed into full waves. The one-wave workgroups take records from one queue (an
+// atomic head, cont_count[1]) whenever at least cont_refill of their lanes are free (or all are), so no
+// wave idles on an exhausted share while others still hold paths: a lane's path is one of the reference's per-pixel paths, resumed with exactly its state, so every
 // pixel's bits are those of the uncompacted kernel. It runs after its draw's pt_trace on the same side
 // stream, beside the next frame's pt_trace (frame overlap), so its own tail - a wave waits for the longest
 // chain of dependent walks among its paths - is filled by that frame's waves.
@@ -494,11 +494,9 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_cont(TraceArg
 {
     __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];
     const unsigned lane = threadIdx.x;
-    const unsigned n = *a.cont_count;
-    const unsigned per = (n + gridDim.x - 1) / gridDim.x;
-    unsigned next = blockIdx.x * per;
-    const unsigned end = min(next + per, n);
-    if (next >= end) return;
+    const unsigned n = a.cont_count[0];
+    unsigned* const head = a.cont_count + 1;   // the queue's next record (zeroed with the counter by pt_blend)
+    bool more = true;                          // the queue may still hold records
     const unsigned deep = blockIdx.x * kTraceBlock + lane;
     const unsigned long long below = (1ull << lane) - 1ull;
     Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
@@ -512,20 +510,23 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_cont(TraceArg
     for (;;) {
         const unsigned long long dead = __ballot(!alive);
         const unsigned ndead = (unsigned)__popcll(dead);
-        if (next < end && (ndead >= a.cont_refill || ndead == 64u)) {
+        if (more && (ndead >= a.cont_refill || ndead == 64u)) {   // (wave-uniform: every lane is here)
+            unsigned base = 0;
+            if (lane == 0) base = atomicAdd(head, ndead);
+            base = __shfl(base, 0, 64);
+            if (base + ndead >= n) more = false;
             if (!alive) {
-                const unsigned q = next + (unsigned)__popcll(dead & below);
-                if (q < end) {
+                const unsigned q = base + (unsigned)__popcll(dead & below);
+                if (q < n) {
                     slot = q;
                     contLoad(a, q, p, s);
                     accum = mk(0, 0, 0);
                     alive = true;
                 }
             }
-            next += ndead;
         }
         if (__ballot(alive) == 0ull) {
-            if (next >= end) break;
+            if (!more) break;
             continue;
         }
         if (alive && !bounceStep<PROG, false, kTraceBlock>(a, p, s, g, accum, lds_stack, lane, deep, cnt)) {
