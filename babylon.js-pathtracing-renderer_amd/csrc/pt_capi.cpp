@@ -140,7 +140,7 @@ struct Dev {
     // Depth (PT_OVERLAP_DEPTH, 2 or 3): draw k uses buffer set k % depth and waits for the mark draw
     // k - depth + 1 recorded (2: the previous draw's), so up to `depth` frames' path tracing are in flight.
     static constexpr int kDepthMax = 3;
-    int depth = 2;
+    int depth = 3;   // (r05q: three frames in flight, with compaction, won on every workload but the bunny)
     hipStream_t ts[kDepthMax] = {};
     hipEvent_t ev_mark[kDepthMax] = {}, ev_traced[kDepthMax] = {};
     unsigned mk_seq = 0;          // megakernel draws so far (buffer set = mk_seq % depth)
@@ -159,19 +159,20 @@ struct Dev {
     // auto mode: compaction pays on the heavy 4K frames (sky + dragon +19 %, dragon stand-in +10 %) and
     // costs elsewhere (bunny 4K -22 %, helmet -9 %, rank-sized frames -29 %: profiles/r05i_*), which
     // the draw's arguments do not tell apart. So the draws of one target / program / partition time it:
-    // after kContSkip draws (the last two compacting, to warm it up on both side streams), blocks of
-    // kContBlock draws with it on, off, off, on, the last kContBlock - kContSettle draws of each timed by
-    // events on the main stream (the first ones carry the switch: orders from the other mode's costs);
-    // at the trial's end the host waits for it once, and compaction stays on only if its faster block
-    // took 2 % less time than the faster block without. Same bits either way.
+    // after kContSkip draws (the last two compacting, to warm it up on the side streams), blocks of
+    // kContBlock draws with it on, off, off, on, kContMeasured draws inside each timed by events on the main
+    // stream; at the trial's end the host waits for it once, and compaction stays on only if its faster
+    // block took 2 % less time than the faster block without. Same bits either way.
     struct ContTune {
         const void* target; int prog, part, parts, w, h;
         int seen;                 // megakernel draws of this key so far
         bool decided, choice;
         float ms_on, ms_off;
     } tune = {};
-    static constexpr int kContSkip = 4, kContBlock = 6, kContSettle = 2, kContBlocks = 4;
-    size_t cont_auto_pixels = 4u << 20;   // (PT_CONT_AUTO_PIXELS)
+    // the trial starts at the 33rd draw of a target: short runs (the driver's 5 + 20 frames) stay in the
+    // default, longer ones settle on the measured best
+    static constexpr int kContSkip = 32, kContBlock = 10, kContSettle = 3, kContMeasured = 5, kContBlocks = 4;
+    size_t cont_auto_pixels = 2000000;   // (PT_CONT_AUTO_PIXELS) the default before the trial: on from 2 MP (1080p)
     hipEvent_t tune_ev[2 * kContBlocks] = {};
     int cont_last = 0;   // what the last megakernel draw did (cont_decide)
     pt::WfBufs gb = {};           // persistent backend: per-pixel G-buffer + radiance
@@ -532,10 +533,6 @@ int cont_decide_(Dev* c, const DevTex* target, int prog, bool eligible, bool* on
 {
     *on = false;
     if (!eligible || c->cont_mode == 0) return PT_OK;
-    // auto mode only tries it on frames of at least kContAutoPixels: it lost on every 1080p and smaller
-    // frame measured (dragon stand-in 1080p -15 %, rank-sized 3840x272 -37 %, helmet -6 %, r05k), and a
-    // trial's compacting blocks would cost those frames
-    if (c->cont_mode == 2 && (size_t)target->w * target->h < c->cont_auto_pixels) return PT_OK;
     // the records first, so that no trial block pays for their allocation
     if (int rc = cont_reserve(c, (size_t)target->w * target->h)) return rc;
     if (c->cont_mode == 1) { *on = true; return PT_OK; }
@@ -545,22 +542,27 @@ int cont_decide_(Dev* c, const DevTex* target, int prog, bool eligible, bool* on
         t = Dev::ContTune{ target, prog, c->part, c->num_parts, target->w, target->h, 0, false, false, 0.0f, 0.0f };
     const int i = t.seen++ - Dev::kContSkip;
     if (t.decided) { *on = t.choice; return PT_OK; }
-    // one compacting draw before the trial: the first launch of a variant that needs more scratch than
-    // any before it waits for the device to drain while the runtime grows its scratch (r05k: the first
-    // trial block then took 2-8x the others)
-    if (i == -2 || i == -1) *on = true;   // (both side streams)
-    if (i < 0) return PT_OK;
-    constexpr int B = Dev::kContBlock, trial = Dev::kContBlocks * B;
-    // each block's last B - kContSettle draws are timed: an event on the main stream (the work before
-    // the draw) at the block's offset kContSettle, and at the next block's start
+    // before the trial, the default: on for frames of at least cont_auto_pixels (with three frames in
+    // flight it won on every frame of 2 MP and more but the light bunny, and lost on the rank-sized one,
+    // profiles/r05q_frames_depth_x_compaction.txt); the two draws before the trial compact, one per side
+    // stream of the last two buffer sets, whatever the default: the first launch of a variant that needs
+    // more scratch than any before it waits for the device to drain while the runtime grows its scratch
+    // (r05k: the first trial block then took 2-8x the others)
+    if (i < 0) {
+        *on = (size_t)target->w * target->h >= c->cont_auto_pixels || i >= -2;
+        return PT_OK;
+    }
+    constexpr int B = Dev::kContBlock, S = Dev::kContSettle, M = Dev::kContMeasured, trial = Dev::kContBlocks * B;
+    // each block times draws S .. S + M - 1 of its own: an event on the main stream (the work before the
+    // draw: the previous draw's blend, which waited for its path tracing) at the block's offsets S and
+    // S + M. With up to `depth` frames in flight, S draws settle the switch (buffer sets whose
+    // longest-first order came from the other mode's costs) and the block's last B - S - M draws keep the
+    // next block's frames out of the timed ones.
     const int b = i / B, o = i % B;
-    if (i <= trial && (o == 0 || o == Dev::kContSettle)) {
-        const int k = o == 0 ? 2 * b - 1 : 2 * b;   // (the first block's start is not timed)
-        if (k >= 0) {
-            hipEvent_t& e = c->tune_ev[k];
-            if (!e) HIPCHK(c, hipEventCreate(&e));
-            HIPCHK(c, hipEventRecord(e, c->stream));
-        }
+    if (i < trial && (o == S || o == S + M)) {
+        hipEvent_t& e = c->tune_ev[2 * b + (o == S ? 0 : 1)];
+        if (!e) HIPCHK(c, hipEventCreate(&e));
+        HIPCHK(c, hipEventRecord(e, c->stream));
     }
     if (i < trial) {
         *on = b == 0 || b == Dev::kContBlocks - 1;   // on, off, off, on
@@ -588,8 +590,9 @@ int cont_decide(Dev* c, const DevTex* target, int prog, bool eligible, bool* on)
     int rc = cont_decide_(c, target, prog, eligible, on);
     // what the draw did, for pt_queue_stats: 0 off, 1 auto decided off, 2 auto decided on, 3 forced on,
     // 4 auto trial
-    const bool tried = c->cont_mode == 2 && eligible && (size_t)target->w * target->h >= c->cont_auto_pixels;
-    c->cont_last = c->cont_mode == 1 && *on ? 3 : !tried ? 0 : c->tune.decided ? (c->tune.choice ? 2 : 1) : 4;
+    const bool tried = c->cont_mode == 2 && eligible;
+    c->cont_last = c->cont_mode == 1 && *on ? 3 : !tried ? 0 : c->tune.decided ? (c->tune.choice ? 2 : 1)
+                 : c->tune.seen > Dev::kContSkip ? 4 : (*on ? 5 : 6);
     return rc;
 }
 

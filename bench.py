@@ -382,13 +382,13 @@ def run_anchors(engine, args):
                      whole (no extrapolation); --dump-canvas PATH also saves frame 1024's canvas."""
     out = {}
     steps4k = max(20, args.steps // 5)
-    # (30 warmup draws: a 4K frame's late-bounce compaction trial takes 28, DESIGN.md §4)
-    _, _, tris, el, km, n = single_gpu_run(engine, "dragon", 3840, 2160, 30, steps4k, max(1, steps4k // 10))
+    # (100 warmup draws: the late-bounce compaction trial ends at the 73rd, DESIGN.md §4)
+    _, _, tris, el, km, n = single_gpu_run(engine, "dragon", 3840, 2160, 100, steps4k, max(1, steps4k // 10))
     out["dragon_4k_1gpu"] = {"value": round(3840 * 2160 * steps4k / el / 1e6, 2), "unit": "Mpaths/s",
                              "ms_per_step": round(el / steps4k * 1e3, 4), "steps": steps4k, "kernel_ms": km,
                              "width": 3840, "height": 2160, "triangles": tris,
                              "late_bounce_compaction": compaction(engine)}
-    _, _, tris, el, km, n = single_gpu_run(engine, "bunny16", 1920, 1080, 10, args.steps, max(1, args.steps // 10))
+    _, _, tris, el, km, n = single_gpu_run(engine, "bunny16", 1920, 1080, 100, args.steps, max(1, args.steps // 10))
     out["bunny16_1080p"] = {"value": round(1920 * 1080 * args.steps / el / 1e6, 2), "unit": "Mpaths/s",
                             "ms_per_step": round(el / args.steps * 1e3, 4), "steps": args.steps, "kernel_ms": km,
                             "triangles": tris, "bvh_walk": engine.bvh_layout_used(),
@@ -574,8 +574,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=30,
-                    help="untimed frames first (>= 28 lets a 4K frame's late-bounce compaction trial finish)")
+    ap.add_argument("--warmup", type=int, default=100,
+                    help="untimed frames first (>= 73 lets the late-bounce compaction trial finish)")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-oracle baseline (0 = skip)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the live rocprofv3 traffic passes")
     ap.add_argument("--no-output", action="store_true", help="time pathTracing+copy only (no screenOutput/gather)")
