@@ -933,9 +933,10 @@ int render_trace(DevFx* fx, DevTex* target)
     a.ntiles = (unsigned)n;
     if (int rc = begin_draw(c, fx->prog, ts)) return rc;
     HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, ts));
+    // (the draw's timing events bracket pt_trace alone, as a kernel trace reports it; pt_cont follows)
+    if (int rc = end_draw(c, fx->prog, ts)) return rc;
     if (cont)   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
         HIPCHK(c, pt_launch_cont(fx->prog, &a, (int)std::min<size_t>(c->cont_waves, (size_t)gx * gy * 4), ts));
-    if (int rc = end_draw(c, fx->prog, ts)) return rc;
     if (overlap) {
         HIPCHK(c, hipEventRecord(c->ev_traced[par], ts));
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_traced[par], 0));

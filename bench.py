@@ -189,8 +189,8 @@ def cpu_baseline(workload, budget):
 
 # ------------------------------------------------------------------------------ live PMC traffic
 def live_traffic(workload, W, Hh, frames=5):
-    """L2-to-fabric bytes and vector-ALU instructions per launch of the path-tracing kernel, measured
-    now: three rocprofv3 --pmc passes (FETCH_SIZE and WRITE_SIZE need 3 + 2 of the 4 TCC slots, so one
+    """L2-to-fabric bytes and vector-ALU instructions per frame of the path tracing (pt_trace, and
+    pt_cont when late-bounce compaction runs), measured now: three rocprofv3 --pmc passes (FETCH_SIZE and WRITE_SIZE need 3 + 2 of the 4 TCC slots, so one
     pass each; SQ_INSTS_VALU) over tools/prof_frames.py rendering `frames` frames of this workload.
     gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 128-B read requests at 64 B ->
     doubled; KiB -> B. Returns (bytes, VALU wave-instructions, note)."""
@@ -208,15 +208,20 @@ def live_traffic(workload, W, Hh, frames=5):
             r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), capture_output=True, text=True)
             if r.returncode != 0:
                 return None, None, "rocprofv3 --pmc %s exited %d" % (ctr, r.returncode)
-            per = []
+            # per frame: pt_trace's launches, and late-bounce compaction's pt_cont with them when it runs
+            # (the path tracing of one frame; a counter is summed over a dispatch's rows)
+            tot, launches = 0.0, set()
             for path in glob.glob(os.path.join(out, "**", "*counter_collection.csv"), recursive=True):
                 with open(path) as f:
                     for row in csv.DictReader(f):
-                        if "pt_trace<" in row["Kernel_Name"] and row["Counter_Name"] == ctr:
-                            per.append(float(row["Counter_Value"]))
-            if not per:
+                        kn = row["Kernel_Name"]
+                        if ("pt_trace<" in kn or "pt_cont<" in kn) and row["Counter_Name"] == ctr:
+                            tot += float(row["Counter_Value"])
+                            if "pt_trace<" in kn:
+                                launches.add(row.get("Dispatch_Id", len(launches)))
+            if not launches:
                 return None, None, "no %s samples for pt_trace" % ctr
-            vals[ctr] = sum(per) / len(per)
+            vals[ctr] = tot / len(launches)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     return int((2.0 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024), vals["SQ_INSTS_VALU"], None
