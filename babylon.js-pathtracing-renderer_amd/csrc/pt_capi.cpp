@@ -141,6 +141,7 @@ struct Dev {
     // k - depth + 1 recorded (2: the previous draw's), so up to `depth` frames' path tracing are in flight.
     static constexpr int kDepthMax = 3;
     int depth = 3;   // (r05q: three frames in flight, with compaction, won on every workload but the bunny)
+    int depth_run = 3;            // the last megakernel draw's depth (<= depth: the auto trial may pick 2)
     hipStream_t ts[kDepthMax] = {};
     hipEvent_t ev_mark[kDepthMax] = {}, ev_traced[kDepthMax] = {};
     unsigned mk_seq = 0;          // megakernel draws so far (buffer set = mk_seq % depth)
@@ -155,7 +156,7 @@ struct Dev {
     int cont_mode = 2;
     void* cont_mem = nullptr;
     size_t cont_cap = 0;
-    unsigned cont_bounce = 2, cont_lanes = 32, cont_refill = 16, cont_waves = 2048;
+    unsigned cont_bounce = 2, cont_lanes = 48, cont_refill = 16, cont_waves = 2048;
     // auto mode: compaction pays on the heavy 4K frames (sky + dragon +19 %, dragon stand-in +10 %) and
     // costs elsewhere (bunny 4K -22 %, helmet -9 %, rank-sized frames -29 %: profiles/r05i_*), which
     // the draw's arguments do not tell apart. So the draws of one target / program / partition time it:
@@ -163,15 +164,19 @@ struct Dev {
     // kContBlock draws with it on, off, off, on, kContMeasured draws inside each timed by events on the main
     // stream; at the trial's end the host waits for it once, and compaction stays on only if its faster
     // block took 2 % less time than the faster block without. Same bits either way.
+    // The blocks without compaction also try two frames in flight instead of three (on, off, off at
+    // depth 2 twice, off, on): the light frames that do not compact lost 2-5 % to the third frame
+    // (r05q: bunny 5365 vs 5228 Mpaths/s, bunny16 -4.5 %), so the faster depth stays with "off".
     struct ContTune {
         const void* target; int prog, part, parts, w, h;
         int seen;                 // megakernel draws of this key so far
         bool decided, choice;
-        float ms_on, ms_off;
+        int depth;                // the frames in flight the decision keeps
+        float ms_on, ms_off, ms_off2;
     } tune = {};
     // the trial starts at the 33rd draw of a target: short runs (the driver's 5 + 20 frames) stay in the
     // default, longer ones settle on the measured best
-    static constexpr int kContSkip = 32, kContBlock = 10, kContSettle = 3, kContMeasured = 5, kContBlocks = 4;
+    static constexpr int kContSkip = 32, kContBlock = 10, kContSettle = 3, kContMeasured = 5, kContBlocks = 6;
     size_t cont_auto_pixels = 2000000;   // (PT_CONT_AUTO_PIXELS) the default before the trial: on from 2 MP (1080p)
     hipEvent_t tune_ev[2 * kContBlocks] = {};
     int cont_last = 0;   // what the last megakernel draw did (cont_decide)
@@ -529,9 +534,10 @@ void cont_args(Dev* c, int p, pt::TraceArgs& a)
 }
 
 // auto mode of late-bounce compaction (Dev::ContTune): whether this draw compacts
-int cont_decide_(Dev* c, const DevTex* target, int prog, bool eligible, bool* on)
+int cont_decide_(Dev* c, const DevTex* target, int prog, bool eligible, bool* on, int* depth)
 {
     *on = false;
+    *depth = c->depth;
     if (!eligible || c->cont_mode == 0) return PT_OK;
     // the records first, so that no trial block pays for their allocation
     if (int rc = cont_reserve(c, (size_t)target->w * target->h)) return rc;
@@ -539,9 +545,10 @@ int cont_decide_(Dev* c, const DevTex* target, int prog, bool eligible, bool* on
     auto& t = c->tune;
     if (t.target != target || t.prog != prog || t.part != c->part || t.parts != c->num_parts || t.w != target->w ||
         t.h != target->h)
-        t = Dev::ContTune{ target, prog, c->part, c->num_parts, target->w, target->h, 0, false, false, 0.0f, 0.0f };
+        t = Dev::ContTune{ target, prog, c->part, c->num_parts, target->w, target->h, 0, false, false, c->depth,
+                           0.0f, 0.0f, 0.0f };
     const int i = t.seen++ - Dev::kContSkip;
-    if (t.decided) { *on = t.choice; return PT_OK; }
+    if (t.decided) { *on = t.choice; *depth = t.depth; return PT_OK; }
     // before the trial, the default: on for frames of at least cont_auto_pixels (with three frames in
     // flight it won on every frame of 2 MP and more but the light bunny, and lost on the rank-sized one,
     // profiles/r05q_frames_depth_x_compaction.txt); the two draws before the trial compact, one per side
@@ -565,29 +572,33 @@ int cont_decide_(Dev* c, const DevTex* target, int prog, bool eligible, bool* on
         HIPCHK(c, hipEventRecord(e, c->stream));
     }
     if (i < trial) {
-        *on = b == 0 || b == Dev::kContBlocks - 1;   // on, off, off, on
+        *on = b == 0 || b == Dev::kContBlocks - 1;   // on, off, off at depth 2 (twice), off, on
+        if (b == 2 || b == 3) *depth = std::min(2, c->depth);
         return PT_OK;
     }
     // the trial's end: the host waits for it once (the draws it has already queued ran without), so that
     // every later draw of this target takes the decision; the faster block of each mode decides (one
     // stray block cannot)
     HIPCHK(c, hipEventSynchronize(c->tune_ev[2 * Dev::kContBlocks - 1]));
-    t.ms_on = t.ms_off = 1e30f;
+    t.ms_on = t.ms_off = t.ms_off2 = 1e30f;
     for (int k = 0; k < Dev::kContBlocks; k++) {
         float ms = 0.0f;
         HIPCHK(c, hipEventElapsedTime(&ms, c->tune_ev[2 * k], c->tune_ev[2 * k + 1]));
-        float& m = k == 0 || k == Dev::kContBlocks - 1 ? t.ms_on : t.ms_off;
+        float& m = k == 0 || k == Dev::kContBlocks - 1 ? t.ms_on : k == 2 || k == 3 ? t.ms_off2 : t.ms_off;
         m = std::min(m, ms);
     }
     t.decided = true;
-    t.choice = t.ms_on < 0.98f * t.ms_off;
+    const bool two = t.ms_off2 < t.ms_off;
+    t.choice = t.ms_on < 0.98f * std::min(t.ms_off, t.ms_off2);
+    t.depth = t.choice || !two ? c->depth : std::min(2, c->depth);
     *on = t.choice;
+    *depth = t.depth;
     return PT_OK;
 }
 
-int cont_decide(Dev* c, const DevTex* target, int prog, bool eligible, bool* on)
+int cont_decide(Dev* c, const DevTex* target, int prog, bool eligible, bool* on, int* depth)
 {
-    int rc = cont_decide_(c, target, prog, eligible, on);
+    int rc = cont_decide_(c, target, prog, eligible, on, depth);
     // what the draw did, for pt_queue_stats: 0 off, 1 auto decided off, 2 auto decided on, 3 forced on,
     // 4 auto trial
     const bool tried = c->cont_mode == 2 && eligible;
@@ -867,7 +878,17 @@ int render_trace(DevFx* fx, DevTex* target)
     }
 
     // ---- the megakernel: draw k = mk_seq uses buffer set k % depth
-    const int par = (int)(c->mk_seq % (unsigned)c->depth);
+    // late-bounce compaction and the frames in flight (cont_decide): when compaction is on, no split
+    // tiles - their 16-lane waves would hand their slowest paths to pt_cont at once (r05j: dragon
+    // stand-in 4K with both 2222 Mpaths/s, with compaction alone 2762)
+    bool cont = false;
+    int depth = c->depth;
+    if (int rc = cont_decide(c, target, fx->prog, mesh && !c->counting && !PT_SECPROF_BUILD, &cont, &depth)) return rc;
+    if (depth != c->depth_run) {   // another buffer-set cycle: the draw waits for everything before it
+        c->depth_run = depth;
+        c->need_fresh = true;
+    }
+    const int par = (int)(c->mk_seq % (unsigned)depth);
     // longest-first: the wave durations of draw k - 2 (same parity) order this draw's workgroups when it
     // drew the same grid, target and program; split tiles take 12 more workgroups each, in padding rows
     const size_t n = (size_t)gx * gy;   // 16x16 tiles
@@ -875,11 +896,6 @@ int render_trace(DevFx* fx, DevTex* target)
     const bool lpt = c->lpt && !c->counting;
     const bool same = lpt && key.valid && key.n == n && key.target == target && key.prog == fx->prog &&
                       key.part == c->part && key.parts == c->num_parts && c->lpt_cap >= n;
-    // late-bounce compaction (cont_decide): when it is on, no split tiles - their 16-lane waves would hand
-    // their slowest paths to pt_cont at once (r05j: dragon stand-in 4K with both 2222 Mpaths/s, with
-    // compaction alone 2762)
-    bool cont = false;
-    if (int rc = cont_decide(c, target, fx->prog, mesh && !c->counting && !PT_SECPROF_BUILD, &cont)) return rc;
     const unsigned split = same && !cont ? (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u : 0u;   // the cap
     const unsigned extra = 4u * pt::kSplitParts - 4u;   // more workgroups per split tile
     const int gy_grid = gy + (int)((extra * split + 4u * gx - 1) / (4u * gx));
@@ -911,7 +927,7 @@ int render_trace(DevFx* fx, DevTex* target)
     hipStream_t ts = c->stream;
     if (overlap) {
         if (int rc = overlap_init(c)) return rc;
-        const unsigned k = c->mk_seq, D = (unsigned)c->depth;
+        const unsigned k = c->mk_seq, D = (unsigned)depth;
         if (c->need_fresh) { c->mark_floor = k; c->need_fresh = false; }
         HIPCHK(c, hipEventRecord(c->ev_mark[par], c->stream));
         ts = c->ts[par];
@@ -1119,6 +1135,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP_DEPTH")) c->depth = std::min(Dev::kDepthMax, std::max(2, std::atoi(v)));
+    c->depth_run = c->depth;
     if (const char* v = std::getenv("PT_CONT")) c->cont_mode = std::min(2, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_BOUNCE")) c->cont_bounce = (unsigned)std::max(2, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_LANES")) c->cont_lanes = (unsigned)std::min(64, std::max(1, std::atoi(v)));
@@ -1538,14 +1555,15 @@ int dev_queue_stats(Dev* c, uint32_t out[16])
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = flush_order(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    const int p = (int)(c->mk_seq % (unsigned)c->depth);   // the tiles the next megakernel draw of the same grid splits
+    const int p = (int)(c->mk_seq % (unsigned)c->depth_run);   // the tiles the next megakernel draw of the same grid splits
     if (c->lpt_mem && c->lpt_key[p].valid)
         HIPCHK(c, hipMemcpy(&out[7], c->lpt_split(p), sizeof(uint32_t), hipMemcpyDeviceToHost));
     // late-bounce compaction of the last megakernel draw: 0 off, 1 auto decided off, 2 auto decided on,
-    // 3 forced on (PT_CONT=1), 4 auto trial; out[15]: the auto trial's ms with it on per ms without, x 1000
-    out[14] = (uint32_t)c->cont_last;
-    out[15] = (c->cont_last == 1 || c->cont_last == 2) && c->tune.ms_off > 0.0f
-                  ? (uint32_t)(1000.0f * c->tune.ms_on / c->tune.ms_off) : 0u;
+    // 3 forced on (PT_CONT=1), 4 auto trial, 5 / 6 default on / off; bits 8-15: its frames in flight;
+    // out[15]: the auto trial's ms with it on per ms without (the faster depth), x 1000
+    out[14] = (uint32_t)c->cont_last | (uint32_t)c->depth_run << 8;
+    const float off = std::min(c->tune.ms_off, c->tune.ms_off2);
+    out[15] = (c->cont_last == 1 || c->cont_last == 2) && off > 0.0f ? (uint32_t)(1000.0f * c->tune.ms_on / off) : 0u;
     if (!c->wf_mem) return PT_OK;
     std::vector<unsigned> h(16 * pt::kShards);
     HIPCHK(c, hipMemcpy(h.data(), c->wf.cnt, h.size() * sizeof(unsigned), hipMemcpyDeviceToHost));

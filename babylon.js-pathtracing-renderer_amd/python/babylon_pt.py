@@ -216,7 +216,8 @@ class Engine:
         self.check(lib().pt_queue_stats(self.ctx, buf), "pt_queue_stats")
         return {"paths": list(buf[0:7]), "bvh": list(buf[8:14]), "split_tiles": int(buf[7]),
                 "late_bounce_compaction": {0: "off", 1: "auto: off", 2: "auto: on", 3: "on", 4: "auto: trial",
-                                           5: "auto: default on", 6: "auto: default off"}[int(buf[14])],
+                                           5: "auto: default on", 6: "auto: default off"}[int(buf[14]) & 0xFF],
+                "frames_in_flight": int(buf[14]) >> 8,
                 "compaction_trial_ratio": buf[15] / 1000.0 if buf[15] else None}
 
     def math_probe(self, op, x, y=None):

@@ -373,7 +373,8 @@ def single_gpu_run(engine, workload, W, Hh, warmup, steps, event_every, from_fra
 def compaction(engine):
     """What the draws' late-bounce compaction auto mode decided (pt_queue_stats; synchronises)."""
     q = engine.queue_stats()
-    return {"mode": q["late_bounce_compaction"], "trial_ms_on_per_off": q["compaction_trial_ratio"]}
+    return {"mode": q["late_bounce_compaction"], "trial_ms_on_per_off": q["compaction_trial_ratio"],
+            "frames_in_flight": q["frames_in_flight"]}
 
 
 def run_anchors(engine, args):

@@ -211,9 +211,10 @@ int pt_reset_counters(pt_ctx* ctx);
  * bounce b (b = 0..6), out[8 + b] = rays handed to the BVH walk at bounce b (b = 0..5); megakernel:
  * out[7] = the slowest tiles the next draw of the same target and program shades as 16-lane waves;
  * out[14] = late-bounce compaction of the last megakernel draw (PT_CONT: 0 off, 1 on, 2 auto = default):
- * 0 off, 1 auto decided off, 2 auto decided on, 3 forced on, 4 auto trial running, 5 / 6 auto before the
- * trial, default on / off; out[15] = the auto trial's time with compaction per time without, x 1000
- * (0 before the decision). */
+ * bits 0-7: 0 off, 1 auto decided off, 2 auto decided on, 3 forced on, 4 auto trial running, 5 / 6 auto
+ * before the trial, default on / off; bits 8-15: the frames that draw kept in flight (PT_OVERLAP_DEPTH, or 2
+ * when the auto trial found two faster without compaction); out[15] = the auto trial's time with
+ * compaction per time without (at the faster depth), x 1000 (0 before the decision). */
 int pt_queue_stats(pt_ctx* ctx, uint32_t out[16]);
 /* Device self-test of the pinned GLSL built-ins (ops as the oracle's pto_math_probe). */
 int pt_math_probe(pt_ctx* ctx, int op, const float* x, const float* y, float* out, int n);

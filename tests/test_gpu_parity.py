@@ -353,10 +353,11 @@ def test_late_bounce_compaction_1080p_bitexact(monkeypatch, layout):
 def test_late_bounce_compaction_auto_mode_bitexact(monkeypatch):
     """The default auto mode (PT_CONT=2): a target's first 32 draws use the default (on from
     PT_CONT_AUTO_PIXELS, here 0, so on; the last two before the trial compact either way, warming the
-    variant up on the side streams), then blocks of 10 draws with compaction on, off, off, on, draws 3-7
-    of each timed by events on the main stream; at the 73rd draw the host waits for the trial once and
-    keeps the faster mode. 76 frames of the dragon stand-in at 480x272 accumulate the oracle's bits
-    whatever the draws chose, and the decision is reported."""
+    variant up on the side streams), then blocks of 10 draws with compaction on, off, off with two frames
+    in flight (twice), off, on, draws 3-7 of each timed by events on the main stream; at the 93rd draw
+    the host waits for the trial once and keeps the faster mode (and, without compaction, the faster
+    depth). 96 frames of the dragon stand-in at 480x272 accumulate the oracle's bits whatever the draws
+    chose - across the switches between buffer-set cycles too - and the decision is reported."""
     import copy
     import babylon_pt as bp
     monkeypatch.delenv("PT_CONT", raising=False)
@@ -367,13 +368,14 @@ def test_late_bounce_compaction_auto_mode_bitexact(monkeypatch):
         meta = copy.deepcopy(H.stream("gltf_bunny_1080p"))
         mesh = H.synthetic_dragon()
         player = bp.StreamPlayer(e, meta, H.bluenoise(), H.texture_payloads(meta, mesh), W, Hh)
-        meta["frames"] = meta["frames"] + [player.synth_frame(k) for k in range(72)]
+        meta["frames"] = meta["frames"] + [player.synth_frame(k) for k in range(92)]
         e.resize_canvas(W, Hh)
         states = []
         for i in range(len(meta["frames"])):
             player.play_frame(i)
-            if i in (10, 40):
-                states.append(e.queue_stats()["late_bounce_compaction"])
+            if i in (10, 40, 55):
+                q = e.queue_stats()
+                states.append((q["late_bounce_compaction"], q["frames_in_flight"]))
         e.sync()
         got_acc = player.textures["pathTracingRenderTarget"].read()
         got_can = e.read_canvas(W, Hh)
@@ -383,8 +385,9 @@ def test_late_bounce_compaction_auto_mode_bitexact(monkeypatch):
     ref_acc, ref_can, _ = H.oracle_replay(meta, None, W, Hh, with_output=True, mesh=mesh)
     assert _bits_equal(ref_acc[-1], got_acc), _diff_report(ref_acc[-1], got_acc)
     assert _bits_equal(ref_can[-1], got_can), _diff_report(ref_can[-1], got_can)
-    assert states == ["auto: default on", "auto: trial"], states
+    assert states == [("auto: default on", 3), ("auto: trial", 3), ("auto: trial", 2)], states
     assert qs["late_bounce_compaction"] in ("auto: on", "auto: off"), qs
+    assert qs["frames_in_flight"] == 3 if qs["late_bounce_compaction"] == "auto: on" else qs["frames_in_flight"] in (2, 3)
     assert qs["compaction_trial_ratio"] and 0.2 < qs["compaction_trial_ratio"] < 5.0, qs
 
 
