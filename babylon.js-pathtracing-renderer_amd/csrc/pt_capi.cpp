@@ -139,11 +139,23 @@ struct Dev {
     bool overlap = true;
     // Depth (PT_OVERLAP_DEPTH, 2 or 3): draw k uses buffer set k % depth and waits for the mark draw
     // k - depth + 1 recorded (2: the previous draw's), so up to `depth` frames' path tracing are in flight.
-    static constexpr int kDepthMax = 3;
+    static constexpr int kDepthMax = 6;
     int depth = 3;   // (r05q: three frames in flight, with compaction, won on every workload but the bunny)
     int depth_run = 3;            // the last megakernel draw's depth (<= depth: the auto trial may pick 2)
+    // Lag (PT_OVERLAP_LAG): buffer sets beyond the streams. Draw k's buffer set is k % (depth + lag)
+    // (radiance, compaction records, longest-first cost / order: what the main stream's blend, output
+    // and order build read) and its stream / spill slab k % depth (what only its own stream touches),
+    // and it waits for the mark of draw k - depth - lag + 1: with lag > 0 a side stream runs its next
+    // draw as soon as its previous one ends, not after that draw's blend and output on the main stream.
+    // By default (lag -1) the lag is kLagSmall for draws that trace fewer than lag_pixels pixels and
+    // 0 above: a small frame (a rank's bands of an N-GPU frame) fills the chip only with more frames
+    // in flight, a 1080p one lost 3-4 % to the extra lag (r05an: 260-520 kpx +4-10 %, 1 Mpx and up -3 %).
+    static constexpr int kLagMax = 6, kSetsMax = kDepthMax + kLagMax, kLagSmall = 2;
+    int lag = -1;
+    int lag_run = 0;              // the last megakernel draw's lag
+    size_t lag_pixels = 800000;   // (PT_OVERLAP_LAG_PIXELS)
     hipStream_t ts[kDepthMax] = {};
-    hipEvent_t ev_mark[kDepthMax] = {}, ev_traced[kDepthMax] = {};
+    hipEvent_t ev_mark[kSetsMax] = {}, ev_traced[kDepthMax] = {};
     unsigned mk_seq = 0;          // megakernel draws so far (buffer set = mk_seq % depth)
     bool need_fresh = true;       // the next megakernel draw must wait for everything before it (a fresh mark)
     unsigned mark_floor = 0;      // no draw waits for a mark older than draw mark_floor's
@@ -200,13 +212,14 @@ struct Dev {
     struct { bool on; unsigned n; const unsigned* cost; unsigned* order; unsigned* split; unsigned cap, dominance; int near; }
         pending_order = {};
     bool fuse_order = true;
-    unsigned* lpt_mem = nullptr;            // cost[kDepthMax][4 * cap] | order[kDepthMax][cap] | split[kDepthMax]
+    unsigned* lpt_mem = nullptr;            // cost[kSetsMax][4 * cap] | order[kSetsMax][cap] | split[kSetsMax]
     size_t lpt_cap = 0;
     struct LptKey { bool valid; size_t n; const void* target; int prog, part, parts; };
-    LptKey lpt_key[kDepthMax] = {};         // what cost[p] / order[p] were last written for
+    LptKey lpt_key[kSetsMax] = {};          // what cost[p] / order[p] were last written for
     unsigned* lpt_cost(int p) const { return lpt_mem + 4 * lpt_cap * p; }
-    unsigned* lpt_order(int p) const { return lpt_mem + 4 * lpt_cap * kDepthMax + lpt_cap * p; }
-    unsigned* lpt_split(int p) const { return lpt_mem + 5 * lpt_cap * kDepthMax + p; }
+    unsigned* lpt_order(int p) const { return lpt_mem + 4 * lpt_cap * kSetsMax + lpt_cap * p; }
+    unsigned* lpt_split(int p) const { return lpt_mem + 5 * lpt_cap * kSetsMax + p; }
+    int sets() const { return depth + (lag >= 0 ? lag : kLagSmall); }   // buffer sets allocated (rad, compaction records)
     // per-draw events for pt_last_render_ms: off until its first call (or PT_DRAW_EVENTS=1). Each
     // hipEventRecord costs ~5 us of stream time between two kernels on MI355X (r02h: two pairs per
     // frame were +19 us per frame, +1.7 % dragon stand-in, +3.8 % bunny)
@@ -498,7 +511,7 @@ int rad_reserve(Dev* c, size_t pixels)
     if (pixels <= c->rad_pixels) return PT_OK;
     if (c->rad_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->rad_mem)); c->rad_mem = nullptr; }
     c->rad_pixels = 0;
-    HIPCHK(c, hipMalloc(&c->rad_mem, (size_t)c->depth * pixels * sizeof(float4)));
+    HIPCHK(c, hipMalloc(&c->rad_mem, (size_t)c->sets() * pixels * sizeof(float4)));
     c->rad_pixels = pixels;
     c->need_fresh = true;
     return PT_OK;
@@ -512,11 +525,11 @@ int cont_reserve(Dev* c, size_t paths)
     if (c->cont_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->cont_mem)); c->cont_mem = nullptr; }
     c->cont_cap = 0;
     const size_t per = paths * 64 + ((paths * 4 + 255) & ~(size_t)255) + 256;
-    HIPCHK(c, hipMalloc(&c->cont_mem, (size_t)c->depth * per));
+    HIPCHK(c, hipMalloc(&c->cont_mem, (size_t)c->sets() * per));
     // on the main stream (hipMemset would go to the null stream, which the non-blocking side streams do
     // not wait for: the next draw's atomics raced with it); the next draw's path tracing waits for a mark
     // recorded after it
-    HIPCHK(c, hipMemsetAsync(c->cont_mem, 0, (size_t)c->depth * per, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->cont_mem, 0, (size_t)c->sets() * per, c->stream));
     c->cont_cap = paths;
     c->need_fresh = true;
     return PT_OK;
@@ -556,7 +569,9 @@ int cont_decide_(Dev* c, const DevTex* target, int prog, bool eligible, bool* on
     // more scratch than any before it waits for the device to drain while the runtime grows its scratch
     // (r05k: the first trial block then took 2-8x the others)
     if (i < 0) {
-        *on = (size_t)target->w * target->h >= c->cont_auto_pixels || i >= -2;
+        // (the pixels this partition traces: a rank's bands of an N-GPU frame are a small frame -
+        // r05ao: 0.5-1 Mpx frames lost 33-41 % to compaction)
+        *on = (size_t)target->w * target->h / (size_t)std::max(1, c->num_parts) >= c->cont_auto_pixels || i >= -2;
         return PT_OK;
     }
     constexpr int B = Dev::kContBlock, S = Dev::kContSettle, M = Dev::kContMeasured, trial = Dev::kContBlocks * B;
@@ -611,9 +626,20 @@ int cont_decide(Dev* c, const DevTex* target, int prog, bool eligible, bool* on,
 int overlap_init(Dev* c)
 {
     if (c->ts[0]) return PT_OK;
+    // (experiment, PT_SIDE_STREAMS=1) CU-masked side streams over every CU, each on a hardware queue of
+    // its own: with PT_OVERLAP_DEPTH=6, rank-sized dragon frames +30 %, the bunny's bimodal, 1080p -6 %
+    // (profiles/r05ad_*, r05an_*); stream priorities and CUs kept free for the main stream lost
+    const char* sk = std::getenv("PT_SIDE_STREAMS");
+    const int kind = sk ? std::atoi(sk) : 0;
+    for (int p = 0; p < c->sets(); p++) HIPCHK(c, hipEventCreateWithFlags(&c->ev_mark[p], hipEventDisableTiming));
     for (int p = 0; p < c->depth; p++) {
-        HIPCHK(c, hipStreamCreateWithFlags(&c->ts[p], hipStreamNonBlocking));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_mark[p], hipEventDisableTiming));
+        if (kind == 1) {
+            uint32_t mask[16];
+            for (auto& m : mask) m = 0xffffffffu;
+            HIPCHK(c, hipExtStreamCreateWithCUMask(&c->ts[p], 16, mask));
+        } else {
+            HIPCHK(c, hipStreamCreateWithFlags(&c->ts[p], hipStreamNonBlocking));
+        }
         HIPCHK(c, hipEventCreateWithFlags(&c->ev_traced[p], hipEventDisableTiming));
     }
     return PT_OK;
@@ -884,13 +910,19 @@ int render_trace(DevFx* fx, DevTex* target)
     bool cont = false;
     int depth = c->depth;
     if (int rc = cont_decide(c, target, fx->prog, mesh && !c->counting && !PT_SECPROF_BUILD, &cont, &depth)) return rc;
-    if (depth != c->depth_run) {   // another buffer-set cycle: the draw waits for everything before it
+    const size_t traced = (size_t)target->w * target->h / (size_t)std::max(1, c->num_parts);   // (about)
+    const int lag = c->lag >= 0 ? c->lag : traced < c->lag_pixels ? Dev::kLagSmall : 0;
+    if (depth != c->depth_run || lag != c->lag_run) {   // another buffer-set cycle: the draw waits for everything before it
         c->depth_run = depth;
+        c->lag_run = lag;
         c->need_fresh = true;
     }
-    const int par = (int)(c->mk_seq % (unsigned)depth);
-    // longest-first: the wave durations of draw k - 2 (same parity) order this draw's workgroups when it
-    // drew the same grid, target and program; split tiles take 12 more workgroups each, in padding rows
+    const unsigned nsets = (unsigned)(depth + lag);
+    const int par = (int)(c->mk_seq % nsets);            // buffer set
+    const int str = (int)(c->mk_seq % (unsigned)depth);  // stream and spill slab
+    // longest-first: the wave durations of draw k - sets (same buffer set) order this draw's workgroups
+    // when it drew the same grid, target and program; split tiles take 12 more workgroups each, in
+    // padding rows
     const size_t n = (size_t)gx * gy;   // 16x16 tiles
     const Dev::LptKey& key = c->lpt_key[par];
     const bool lpt = c->lpt && !c->counting;
@@ -905,7 +937,7 @@ int render_trace(DevFx* fx, DevTex* target)
             return fail(c, PT_ERR_ARG, "render target too large for the BVH stack slab");
         int rc = spill_reserve(c, lanes);
         if (rc) return rc;
-        a.spill = spill_slab(c, par);
+        a.spill = spill_slab(c, str);
         a.spill_stride = lanes;
     }
     if (int rc = rad_reserve(c, (size_t)target->w * target->h)) return rc;
@@ -913,7 +945,7 @@ int render_trace(DevFx* fx, DevTex* target)
     if (cont) cont_args(c, par, a);
     if (lpt && c->lpt_cap < n) {
         if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
-        HIPCHK(c, hipMalloc(&c->lpt_mem, (5 * n + 1) * Dev::kDepthMax * sizeof(unsigned)));   // cost | order | split
+        HIPCHK(c, hipMalloc(&c->lpt_mem, (5 * n + 1) * Dev::kSetsMax * sizeof(unsigned)));   // cost | order | split
         c->lpt_cap = n;
         c->need_fresh = true;
         for (auto& k : c->lpt_key) k.valid = false;
@@ -927,12 +959,13 @@ int render_trace(DevFx* fx, DevTex* target)
     hipStream_t ts = c->stream;
     if (overlap) {
         if (int rc = overlap_init(c)) return rc;
-        const unsigned k = c->mk_seq, D = (unsigned)depth;
+        const unsigned k = c->mk_seq, D = nsets;
         if (c->need_fresh) { c->mark_floor = k; c->need_fresh = false; }
         HIPCHK(c, hipEventRecord(c->ev_mark[par], c->stream));
-        ts = c->ts[par];
-        // the mark of draw k - depth + 1 (its state: draw k - depth's blend, order build and output), or
-        // of the oldest draw after everything this draw must wait for
+        ts = c->ts[str];
+        // the mark of draw k - sets + 1 (its state: draw k - sets' blend, order build and output), or
+        // of the oldest draw after everything this draw must wait for; the draw k - depth before it on
+        // this stream is ordered by the stream
         const unsigned w = k + 1 >= D ? std::max(k + 1 - D, c->mark_floor) : c->mark_floor;
         HIPCHK(c, hipStreamWaitEvent(ts, c->ev_mark[w % D], 0));
     } else {
@@ -954,8 +987,8 @@ int render_trace(DevFx* fx, DevTex* target)
     if (cont)   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
         HIPCHK(c, pt_launch_cont(fx->prog, &a, (int)std::min<size_t>(c->cont_waves, (size_t)gx * gy * 4), ts));
     if (overlap) {
-        HIPCHK(c, hipEventRecord(c->ev_traced[par], ts));
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_traced[par], 0));
+        HIPCHK(c, hipEventRecord(c->ev_traced[str], ts));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_traced[str], 0));
     }
     // the history half of main() on the main stream, where the copy / output draws that read the
     // accumulation follow
@@ -1136,6 +1169,8 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP_DEPTH")) c->depth = std::min(Dev::kDepthMax, std::max(2, std::atoi(v)));
     c->depth_run = c->depth;
+    if (const char* v = std::getenv("PT_OVERLAP_LAG")) c->lag = std::min(Dev::kLagMax, std::max(-1, std::atoi(v)));
+    if (const char* v = std::getenv("PT_OVERLAP_LAG_PIXELS")) c->lag_pixels = (size_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT")) c->cont_mode = std::min(2, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_BOUNCE")) c->cont_bounce = (unsigned)std::max(2, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_LANES")) c->cont_lanes = (unsigned)std::min(64, std::max(1, std::atoi(v)));
@@ -1187,9 +1222,10 @@ void dev_ctx_destroy(Dev* c)
     if (c->rad_mem) hipFree(c->rad_mem);
     if (c->cont_mem) hipFree(c->cont_mem);
     for (auto& e : c->tune_ev) if (e) hipEventDestroy(e);
+    for (int p = 0; p < Dev::kSetsMax; p++)
+        if (c->ev_mark[p]) hipEventDestroy(c->ev_mark[p]);
     for (int p = 0; p < Dev::kDepthMax; p++) {   // (every side-stream draw was waited for by a blend on the main stream)
         if (c->ts[p]) { hipStreamSynchronize(c->ts[p]); hipStreamDestroy(c->ts[p]); }
-        if (c->ev_mark[p]) hipEventDestroy(c->ev_mark[p]);
         if (c->ev_traced[p]) hipEventDestroy(c->ev_traced[p]);
     }
     if (c->gb_mem) hipFree(c->gb_mem);
@@ -1555,7 +1591,7 @@ int dev_queue_stats(Dev* c, uint32_t out[16])
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = flush_order(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    const int p = (int)(c->mk_seq % (unsigned)c->depth_run);   // the tiles the next megakernel draw of the same grid splits
+    const int p = (int)(c->mk_seq % (unsigned)(c->depth_run + c->lag_run));   // the tiles the next megakernel draw of the same grid splits
     if (c->lpt_mem && c->lpt_key[p].valid)
         HIPCHK(c, hipMemcpy(&out[7], c->lpt_split(p), sizeof(uint32_t), hipMemcpyDeviceToHost));
     // late-bounce compaction of the last megakernel draw: 0 off, 1 auto decided off, 2 auto decided on,

@@ -17,6 +17,7 @@ bench.py: the classes mirror
 fallback: if libpt.so or a gfx950 device is missing, construction raises.
 """
 import ctypes
+import struct
 import json
 import os
 
@@ -325,10 +326,21 @@ class Effect:
 
     def __init__(self, engine, handle):
         self.engine, self.handle = engine, handle
+        # the last value each uniform was given, as its float32 / int bits: a set that repeats it is
+        # skipped (Babylon's Effect keeps the same value cache for setFloat*/setInt/setMatrix), so a
+        # still camera's frame crosses the C ABI only for the counters and the random vector
+        self._cache = {}
 
     def _f(self, name, vals):
-        arr = (ctypes.c_float * len(vals))(*vals)
+        try:   # (the C cast ctypes makes; a finite double beyond float range packs as ctypes's inf)
+            bits = struct.pack("%df" % len(vals), *vals)
+        except (OverflowError, struct.error):
+            bits = bytes((ctypes.c_float * len(vals))(*vals))
+        if self._cache.get(name) == bits:
+            return
+        arr = (ctypes.c_float * len(vals)).from_buffer_copy(bits)
         self.engine.check(lib().pt_set_float(self.handle, name.encode(), arr, len(vals)), "setFloat " + name)
+        self._cache[name] = bits
 
     def setFloat(self, name, v):
         self._f(name, [v])
@@ -343,7 +355,11 @@ class Effect:
         self._f(name, list(m))
 
     def setInt(self, name, v):
-        self.engine.check(lib().pt_set_int(self.handle, name.encode(), int(v)), "setInt " + name)
+        v = int(v)
+        if self._cache.get(name) == v:
+            return
+        self.engine.check(lib().pt_set_int(self.handle, name.encode(), v), "setInt " + name)
+        self._cache[name] = v
 
     def setBool(self, name, v):
         self.setInt(name, 1 if v else 0)

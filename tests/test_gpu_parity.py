@@ -801,6 +801,30 @@ def test_sky_mesh_4k_eight_bands_bitexact(engine):
         assert _bits_equal(rc, gc), "frame %d canvas: %s" % (i, _diff_report(rc, gc))
 
 
+@pytest.mark.parametrize("lag", ["0", "2"])
+def test_sky_mesh_bands_compaction_lag_bitexact(monkeypatch, lag):
+    """Band partitions of small frames with late-bounce compaction forced on (PT_CONT=1) and the
+    overlap lag (PT_OVERLAP_LAG: buffer sets beyond the three side streams, so a stream runs its next
+    draw before the main stream blended its previous one): 4 parts of 960x544 sky + dragon stand-in,
+    copied full-frame and output band by band, bit-exact with the oracle's whole-frame render."""
+    import babylon_pt as bp
+    monkeypatch.setenv("PT_CONT", "1")
+    monkeypatch.setenv("PT_OVERLAP_LAG", lag)
+    meta = H.sky_mesh_stream()
+    mesh = _dragon()
+    W, Hh = 960, 544
+    e = bp.Engine(0)
+    try:
+        got_acc, got_can, _ = _replay_gpu(e, meta, None, W, Hh, parts=4, split_output=True, mesh=mesh)
+        assert e.queue_stats()["late_bounce_compaction"] == "on"
+    finally:
+        e.dispose()
+    ref_acc, ref_can, _ = H.oracle_replay(meta, None, width=W, height=Hh, with_output=True, mesh=mesh)
+    for i, (ra, ga, rc, gc) in enumerate(zip(ref_acc, got_acc, ref_can, got_can)):
+        assert _bits_equal(ra, ga), "frame %d accumulation: %s" % (i, _diff_report(ra, ga))
+        assert _bits_equal(rc, gc), "frame %d canvas: %s" % (i, _diff_report(rc, gc))
+
+
 def test_sky_mesh_converges_1024_frames_bitexact(engine):
     """configs[4]'s converged run at a reduced size: 1024 progressive frames (the 3 recorded ones,
     then the render loop's still-camera frames) through pathTracing -> screenCopy -> screenOutput;
