@@ -327,11 +327,27 @@ class Effect:
     def __init__(self, engine, handle):
         self.engine, self.handle = engine, handle
         # the last value each uniform was given, as its float32 / int bits: a set that repeats it is
-        # skipped (Babylon's Effect keeps the same value cache for setFloat*/setInt/setMatrix), so a
-        # still camera's frame crosses the C ABI only for the counters and the random vector
+        # skipped (Babylon's Effect keeps the same value cache for setFloat*/setInt/setMatrix, and
+        # skips rebinding the texture a sampler already has), so a still camera's frame crosses the C
+        # ABI only for the counters and the random vector
         self._cache = {}
+        self._entry = {}   # the recorded-stream entry (StreamPlayer) each uniform was last set from
+        self._tex = {}
+
+    def _set_entry(self, name, ent):
+        """A recorded uniform entry [kind, values]: nothing to do when this very entry object was
+        the last one set (recorded entries are never mutated)."""
+        if self._entry.get(name) is ent:
+            return
+        kind, vals = ent
+        if kind == "i":
+            self.setInt(name, vals[0])
+        else:
+            self._f(name, vals)
+        self._entry[name] = ent
 
     def _f(self, name, vals):
+        self._entry.pop(name, None)
         try:   # (the C cast ctypes makes; a finite double beyond float range packs as ctypes's inf)
             bits = struct.pack("%df" % len(vals), *vals)
         except (OverflowError, struct.error):
@@ -355,6 +371,7 @@ class Effect:
         self._f(name, list(m))
 
     def setInt(self, name, v):
+        self._entry.pop(name, None)
         v = int(v)
         if self._cache.get(name) == v:
             return
@@ -365,7 +382,12 @@ class Effect:
         self.setInt(name, 1 if v else 0)
 
     def setTexture(self, name, tex):
-        self.engine.check(lib().pt_set_texture(self.handle, name.encode(), tex.handle if tex is not None else None), "setTexture")
+        h = tex.handle if tex is not None else None
+        last = self._tex.get(name)
+        if last is not None and last[0] is tex and last[1] == h:
+            return
+        self.engine.check(lib().pt_set_texture(self.handle, name.encode(), h), "setTexture")
+        self._tex[name] = (tex, h)
 
 
 class EffectWrapper:
@@ -523,11 +545,8 @@ class StreamPlayer:
         uniforms.update({k: v for k, v in self.override.items() if k in uniforms})
         if uniform_override:
             uniforms.update({k: v for k, v in uniform_override.items() if k in uniforms})
-        for name, (kind, vals) in uniforms.items():
-            if kind == "i":
-                fx.setInt(name, vals[0])
-            else:
-                fx._f(name, vals)
+        for name, ent in uniforms.items():
+            fx._set_entry(name, ent)
         for name, tex in call["samplers"].items():
             fx.setTexture(name, self.textures.get(tex) if tex else None)
         target = self.textures[call["target"]] if call["target"] else None

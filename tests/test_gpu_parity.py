@@ -881,10 +881,12 @@ def test_helmet_real_maps_1080p_bitexact(engine):
 def test_split_tiles_bitexact(name, monkeypatch):
     """Tile splitting (the slowest tiles of the longest-first order shaded by 16 waves of 16 lanes,
     pt_trace / pt_order_build) forced on every frame after the first: the recorded stream's
-    accumulation and canvas stay bit-exact with the oracle, and the draws did split tiles."""
+    accumulation and canvas stay bit-exact with the oracle, and the draws did split tiles. (No overlap
+    lag: with it a small frame's buffer set comes round again only after the three recorded frames.)"""
     import babylon_pt as bp
     monkeypatch.setenv("PT_SPLIT_ALWAYS", "1")
     monkeypatch.setenv("PT_SPLIT_TILES", "64")
+    monkeypatch.setenv("PT_OVERLAP_LAG", "0")
     e = bp.Engine(0)
     try:
         meta = H.stream(name)

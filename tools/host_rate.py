@@ -60,7 +60,7 @@ def main():
             step(k)
         pr.disable()
         engine.sync()
-        pstats.Stats(pr).sort_stats("tottime").print_stats(14)
+        pstats.Stats(pr).strip_dirs().sort_stats("tottime").print_stats(16)
     print("host us/step %.1f (synth_frame %.1f, %.1f calls/step)  device-bound us/step %.1f  host share %.2f"
           % (1e6 * t_host / n, 1e6 * t_synth / n, calls / n, 1e6 * t_all / n, t_host / t_all))
     print("  host us/step per call: " + ", ".join("%s %.1f" % (k, 1e6 * v / n) for k, v in per_call.items()))
