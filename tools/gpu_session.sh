@@ -14,7 +14,7 @@
 #   frames:ROUNDS:WLS:ENVS     the same for whole frames (bench.py --no-pmc --cpu-budget 0 per setting);
 #                              a workload W@WxH runs at that frame size
 #   wavetime:LIB:WLS           wave timeline + CU occupancy of a -DPT_SECPROF build (tools/wavetime.py)
-#   prof                       rocprofv3 --kernel-trace --stats of the default bench
+#   prof                       rocprofv3 --kernel-trace --stats of the exact command's workload (20 steps + 5 warmup)
 #   pmc[:W]                    the five PMC passes over tools/prof_frames.py (default workload dragon)
 cd "$GRAFT_REPO_ROOT" || exit 1
 R=$GRAFT_REPO_ROOT
@@ -62,7 +62,7 @@ for step in "$@"; do
     wavetime) mkdir -p "gpurun_out/wt_$TAG"; PT_LIBPT=$a1 run 300 "$LOG" python3 tools/wavetime.py "gpurun_out/wt_$TAG" ${a2//,/ } ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$R/gpurun_out/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 50 --warmup 5 --cpu-budget 0 --no-pmc --no-anchors) > "$LOG" 2>&1 ;;
+        -d "$R/gpurun_out/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 --cpu-budget 0 --no-pmc --no-anchors) > "$LOG" 2>&1 ;;
     pmc)
       W=${a1:-dragon}; OUT="$R/gpurun_out/pmc_$TAG"; mkdir -p "$OUT"; i=0; rc=0
       for C in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES" \
