@@ -1,0 +1,63 @@
+"""One rank's share of an N-GPU frame, on one GPU (tools/README.md): rank R's 16-row bands of the
+N-way round-robin partition (pt_set_row_partition), pathTracing + screenCopy of those bands and
+screenOutput of those bands (pt_set_output_partition), as bench.py's ranks draw them - without the
+RCCL halo exchange and gather, which the one-GPU box cannot run. Prints the rank's paths per second
+(the pixels its bands hold) and ms per frame, the per-rank half of a strong-scaling point.
+
+usage: python tools/rank_proxy.py [--workload dragon] [--size 3840x2160] [--world 8] [--rank 0]
+                                  [--steps 200] [--warmup 100]"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="dragon")
+    ap.add_argument("--size", default="3840x2160")
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=100)
+    args = ap.parse_args()
+    import babylon_pt as bp
+    W, Hh = (int(v) for v in args.size.lower().split("x"))
+    engine = bp.Engine(0)
+    try:
+        player, _, _ = bench.make_player(engine, args.workload, W, Hh)
+        engine.resize_canvas(W, Hh)
+        engine.set_row_partition(args.world, args.rank)
+        engine.set_output_partition(True)
+
+        def step(k):
+            for call in player.synth_frame(k):
+                player.play_call(call)
+
+        for k in range(args.warmup):
+            step(k)
+        engine.sync()
+        t0 = time.perf_counter()
+        for k in range(args.warmup, args.warmup + args.steps):
+            step(k)
+        engine.sync()
+        dt = time.perf_counter() - t0
+        rows = len(bp.owned_rows(Hh, args.world, args.rank))
+        q = engine.queue_stats()
+        print(json.dumps({"workload": args.workload, "size": [W, Hh], "world": args.world, "rank": args.rank,
+                          "rows": rows, "mpaths_per_s": round(rows * W * args.steps / dt / 1e6, 2),
+                          "ms_per_frame": round(1e3 * dt / args.steps, 4),
+                          "late_bounce_compaction": q["late_bounce_compaction"],
+                          "frames_in_flight": q["frames_in_flight"], "env": {k: v for k, v in os.environ.items()
+                                                                             if k.startswith("PT_")}}))
+    finally:
+        engine.dispose()
+
+
+if __name__ == "__main__":
+    main()
