@@ -142,6 +142,7 @@ struct Dev {
     static constexpr int kDepthMax = 6;
     int depth = 3;   // (r05q: three frames in flight, with compaction, won on every workload but the bunny)
     int depth_run = 3;            // the last megakernel draw's depth (<= depth: the auto trial may pick 2)
+    bool depth_env = false;       // PT_OVERLAP_DEPTH given: the auto mode's default keeps it
     // Lag (PT_OVERLAP_LAG): buffer sets beyond the streams. Draw k's buffer set is k % (depth + lag)
     // (radiance, compaction records, longest-first cost / order: what the main stream's blend, output
     // and order build read) and its stream / spill slab k % depth (what only its own stream touches),
@@ -571,7 +572,12 @@ int cont_decide_(Dev* c, const DevTex* target, int prog, bool eligible, bool* on
     if (i < 0) {
         // (the pixels this partition traces: a rank's bands of an N-GPU frame are a small frame -
         // r05ao: 0.5-1 Mpx frames lost 33-41 % to compaction)
-        *on = (size_t)target->w * target->h / (size_t)std::max(1, c->num_parts) >= c->cont_auto_pixels || i >= -2;
+        const size_t traced = (size_t)target->w * target->h / (size_t)std::max(1, c->num_parts);
+        *on = traced >= c->cont_auto_pixels || i >= -2;
+        // without compaction, frames of lag_pixels and more keep two frames in flight (r05aw: the
+        // 4K frame's eighth at N = 8 +5.6 %; r05y: StanfordBunny 1080p +3.5 %), smaller ones three
+        // and the lag (a 1920x136 frame: two lost a third, r05aa)
+        if (!*on && !c->depth_env && traced >= c->lag_pixels) *depth = std::min(2, c->depth);
         return PT_OK;
     }
     constexpr int B = Dev::kContBlock, S = Dev::kContSettle, M = Dev::kContMeasured, trial = Dev::kContBlocks * B;
@@ -1167,7 +1173,10 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
-    if (const char* v = std::getenv("PT_OVERLAP_DEPTH")) c->depth = std::min(Dev::kDepthMax, std::max(2, std::atoi(v)));
+    if (const char* v = std::getenv("PT_OVERLAP_DEPTH")) {
+        c->depth = std::min(Dev::kDepthMax, std::max(2, std::atoi(v)));
+        c->depth_env = true;
+    }
     c->depth_run = c->depth;
     if (const char* v = std::getenv("PT_OVERLAP_LAG")) c->lag = std::min(Dev::kLagMax, std::max(-1, std::atoi(v)));
     if (const char* v = std::getenv("PT_OVERLAP_LAG_PIXELS")) c->lag_pixels = (size_t)std::max(0, std::atoi(v));
