@@ -126,19 +126,20 @@ struct Dev {
     pt::WfBufs wf = {};
     void* wf_mem = nullptr;
     size_t wf_pixels = 0, wf_slots = 0, wf_spill = 0;
-    float2* mk_spill = nullptr;   // megakernel BVH stack spill slabs (one per buffer set of the overlap depth)
+    float2* mk_spill = nullptr;   // megakernel BVH stack spill slabs (one per side stream of the overlap depth)
     size_t mk_spill_lanes = 0;
     // Frame overlap (megakernel draws; PT_OVERLAP=0 turns it off). pt_trace never reads the history:
-    // it writes radiance + the pre-history flag to rad[parity], and pt_blend folds in the history on
-    // the main stream. So draw k's path tracing runs on side stream ts[k % depth] and waits only for the
-    // main stream's state when draw k - 1 began (mark[(k - 1) & 1]: draw k - 2's blend, its order build,
-    // the output that read rad / the order), never for draw k - 1's kernel: consecutive frames' path
-    // tracing overlap, and the next frame's waves fill the launch tail of this one. Per parity: the
-    // radiance buffer, the spill slab and the longest-first cost / order / split (each parity is its own
-    // longest-first pipeline, draw k ordered by draw k - 2's costs).
+    // it writes radiance + the pre-history flag to its buffer set's rad, and pt_blend folds in the
+    // history on the main stream. So draw k's path tracing runs on side stream ts[k % depth] and waits
+    // only for the main stream's state when an earlier draw began (with depth 2: draw k - 1's mark, i.e.
+    // draw k - 2's blend, its order build, the output that read rad / the order), never for draw k - 1's
+    // kernel: consecutive frames' path tracing overlap, and the next frame's waves fill the launch tail
+    // of this one. Per buffer set: the radiance buffer, the compaction records and the longest-first
+    // cost / order / split (each set is its own longest-first pipeline, draw k ordered by the costs of
+    // the set's previous draw); per side stream: the spill slab.
     bool overlap = true;
-    // Depth (PT_OVERLAP_DEPTH, 2 or 3): draw k uses buffer set k % depth and waits for the mark draw
-    // k - depth + 1 recorded (2: the previous draw's), so up to `depth` frames' path tracing are in flight.
+    // Depth (PT_OVERLAP_DEPTH, 2-6): side streams; draw k waits for the mark draw k - depth - lag + 1
+    // recorded (depth 2, lag 0: the previous draw's), so up to `depth` frames' path tracing are in flight.
     static constexpr int kDepthMax = 6;
     int depth = 3;   // (r05q: three frames in flight, with compaction, won on every workload but the bunny)
     int depth_run = 3;            // the last megakernel draw's depth (<= depth: the auto trial may pick 2)
@@ -157,13 +158,13 @@ struct Dev {
     size_t lag_pixels = 800000;   // (PT_OVERLAP_LAG_PIXELS)
     hipStream_t ts[kDepthMax] = {};
     hipEvent_t ev_mark[kSetsMax] = {}, ev_traced[kDepthMax] = {};
-    unsigned mk_seq = 0;          // megakernel draws so far (buffer set = mk_seq % depth)
+    unsigned mk_seq = 0;          // megakernel draws so far (buffer set mk_seq % (depth + lag), stream mk_seq % depth)
     bool need_fresh = true;       // the next megakernel draw must wait for everything before it (a fresh mark)
     unsigned mark_floor = 0;      // no draw waits for a mark older than draw mark_floor's
-    float4* rad_mem = nullptr;    // rad[2]: radiance + flag per pixel
+    float4* rad_mem = nullptr;    // rad[sets()]: radiance + flag per pixel
     size_t rad_pixels = 0;
     // late-bounce compaction of the megakernel's mesh draws (pt_trace<P,false,true> -> pt_cont; PT_CONT:
-    // 0 off, 1 on, 2 auto - the default): per parity 64-B path records, their pixels and a counter; the
+    // 0 off, 1 on, 2 auto - the default): per buffer set 64-B path records, their pixels and a counter; the
     // bounce from which, and the live lanes at or below which, a wave hands its paths on; the refill batch
     // and pt_cont's one-wave workgroups
     int cont_mode = 2;
@@ -174,7 +175,7 @@ struct Dev {
     // costs elsewhere (bunny 4K -22 %, helmet -9 %, rank-sized frames -29 %: profiles/r05i_*), which
     // the draw's arguments do not tell apart. So the draws of one target / program / partition time it:
     // after kContSkip draws (the last two compacting, to warm it up on the side streams), blocks of
-    // kContBlock draws with it on, off, off, on, kContMeasured draws inside each timed by events on the main
+    // kContBlock draws with it on and off, kContMeasured draws inside each timed by events on the main
     // stream; at the trial's end the host waits for it once, and compaction stays on only if its faster
     // block took 2 % less time than the faster block without. Same bits either way.
     // The blocks without compaction also try two frames in flight instead of three (on, off, off at
@@ -190,7 +191,7 @@ struct Dev {
     // the trial starts at the 33rd draw of a target: short runs (the driver's 5 + 20 frames) stay in the
     // default, longer ones settle on the measured best
     static constexpr int kContSkip = 32, kContBlock = 10, kContSettle = 3, kContMeasured = 5, kContBlocks = 6;
-    size_t cont_auto_pixels = 2000000;   // (PT_CONT_AUTO_PIXELS) the default before the trial: on from 2 MP (1080p)
+    size_t cont_auto_pixels = 2000000;   // (PT_CONT_AUTO_PIXELS) the default before the trial: on from 2 MP traced (1080p)
     hipEvent_t tune_ev[2 * kContBlocks] = {};
     int cont_last = 0;   // what the last megakernel draw did (cont_decide)
     pt::WfBufs gb = {};           // persistent backend: per-pixel G-buffer + radiance
@@ -491,7 +492,7 @@ int wf_reserve(Dev* c, int wq, int hq, int tiles, int blocks)
 
 constexpr size_t kSpillPerLane = pt::kStackLevels - pt::kStackLdsMin + 4;   // float2 per lane of one slab
 
-// the megakernel's spill slabs, one per draw parity (overlapping draws must not share one): stack
+// the megakernel's spill slabs, one per side stream (overlapping draws must not share one): stack
 // levels kStackLdsMin..27, then up to 8 floats per lane for the G-buffer fields kept out of LDS
 // (pt_trace.h); slab p starts at spill_slab(c, p)
 int spill_reserve(Dev* c, size_t lanes)
@@ -506,7 +507,7 @@ int spill_reserve(Dev* c, size_t lanes)
 }
 float2* spill_slab(Dev* c, int p) { return c->mk_spill + (size_t)p * c->mk_spill_lanes * kSpillPerLane; }
 
-// rad[2] (pt_trace -> pt_blend) for a frame of `pixels`
+// rad[sets()] (pt_trace -> pt_blend) for a frame of `pixels`
 int rad_reserve(Dev* c, size_t pixels)
 {
     if (pixels <= c->rad_pixels) return PT_OK;
@@ -518,7 +519,7 @@ int rad_reserve(Dev* c, size_t pixels)
     return PT_OK;
 }
 
-// pt_cont's records for frames of up to `paths` pixels, per parity: records [cap x 64 B] | pixels [cap x 4 B]
+// pt_cont's records for frames of up to `paths` pixels, per buffer set: records [cap x 64 B] | pixels [cap x 4 B]
 // | counter; the counters start at zero here, afterwards each draw's pt_blend zeroes its own
 int cont_reserve(Dev* c, size_t paths)
 {
