@@ -370,6 +370,36 @@ def single_gpu_run(engine, workload, W, Hh, warmup, steps, event_every, from_fra
     return player, program, tris, elapsed, km, n
 
 
+def rank_share_run(engine, workload, W, Hh, world, rank, warmup, steps):
+    """One rank's share of an N-GPU frame on this GPU: the rank's 16-row bands of the N-way partition,
+    pathTracing + screenCopy of them and screenOutput of them, as the ranks draw them, without the RCCL
+    halo exchange and gather (the per-rank half of a strong-scaling point; tools/rank_proxy.py).
+    Returns (Mpaths/s of the rank's own pixels, ms per frame, rows)."""
+    import babylon_pt as bp
+    player, _, _ = make_player(engine, workload, W, Hh)
+    engine.resize_canvas(W, Hh)
+    engine.set_row_partition(world, rank)
+    engine.set_output_partition(True)
+    try:
+        def step(k):
+            for call in player.synth_frame(k):
+                player.play_call(call)
+
+        for k in range(warmup):
+            step(k)
+        engine.sync()
+        t0 = time.perf_counter()
+        for k in range(warmup, warmup + steps):
+            step(k)
+        engine.sync()
+        dt = time.perf_counter() - t0
+    finally:
+        engine.set_output_partition(False)
+        engine.set_row_partition(1, 0)
+    rows = len(bp.owned_rows(Hh, world, rank))
+    return rows * W * steps / dt / 1e6, 1e3 * dt / steps, rows
+
+
 def compaction(engine):
     """What the draws' late-bounce compaction auto mode decided (pt_queue_stats; synchronises)."""
     q = engine.queue_stats()
@@ -383,12 +413,15 @@ def run_anchors(engine, args):
                      the driver's 1 -> N strong-scaling curve, which renders that frame);
     bunny16_1080p  - the StanfordBunny split x16 (485,408 triangles: scanned geometry at the dragon's
                      size) at the metric's config, beside the procedural torus;
+    rank_share_4k  - rank 0's share of that 4K frame split over N = 2, 4, 8 GPUs, rendered on this GPU
+                     (its bands' draws as the ranks make them, no RCCL): per-rank Mpaths/s against
+                     dragon_4k_1gpu's, the strong-scaling curve's per-rank half;
     converge_1024spp - BASELINE configs[4] as a run: sky + dragon stand-in at 3840x2160, frames 1..1024
                      from a cleared history, pathTracing + screenCopy + 5x5 screenOutput each, timed
                      whole (no extrapolation); --dump-canvas PATH also saves frame 1024's canvas."""
     out = {}
     steps4k = max(20, args.steps // 5)
-    # (100 warmup draws: the late-bounce compaction trial ends at the 73rd, DESIGN.md §4)
+    # (100 warmup draws: the late-bounce compaction trial ends at the 93rd, DESIGN.md §4)
     _, _, tris, el, km, n = single_gpu_run(engine, "dragon", 3840, 2160, 100, steps4k, max(1, steps4k // 10))
     out["dragon_4k_1gpu"] = {"value": round(3840 * 2160 * steps4k / el / 1e6, 2), "unit": "Mpaths/s",
                              "ms_per_step": round(el / steps4k * 1e3, 4), "steps": steps4k, "kernel_ms": km,
@@ -399,6 +432,14 @@ def run_anchors(engine, args):
                             "ms_per_step": round(el / args.steps * 1e3, 4), "steps": args.steps, "kernel_ms": km,
                             "triangles": tris, "bvh_walk": engine.bvh_layout_used(),
                             "late_bounce_compaction": compaction(engine)}
+    shares = {}
+    for world in (2, 4, 8):
+        v, ms, rows = rank_share_run(engine, "dragon", 3840, 2160, world, 0, 100, 100)
+        shares["n%d" % world] = {"value": round(v, 2), "ms_per_step": round(ms, 4), "rows": rows,
+                                 "per_rank_efficiency": round(v / out["dragon_4k_1gpu"]["value"], 3),
+                                 "late_bounce_compaction": compaction(engine)}
+    out["rank_share_4k"] = dict(shares, unit="Mpaths/s", note="rank 0's bands of the 3840x2160 dragon stand-in "
+                                "frame split N ways, on this GPU, 100 frames after 100; no halo exchange or gather")
     _, _, tris, el, km, n = single_gpu_run(engine, "sky_dragon", 3840, 2160, 0, CONVERGED_SPP, CONVERGED_SPP // 10,
                                            from_frame_one=True)
     conv = {"seconds": round(el, 4), "frames": CONVERGED_SPP, "ms_per_frame": round(el / CONVERGED_SPP * 1e3, 4),

@@ -10,7 +10,6 @@ import argparse
 import json
 import os
 import sys
-import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -30,28 +29,10 @@ def main():
     W, Hh = (int(v) for v in args.size.lower().split("x"))
     engine = bp.Engine(0)
     try:
-        player, _, _ = bench.make_player(engine, args.workload, W, Hh)
-        engine.resize_canvas(W, Hh)
-        engine.set_row_partition(args.world, args.rank)
-        engine.set_output_partition(True)
-
-        def step(k):
-            for call in player.synth_frame(k):
-                player.play_call(call)
-
-        for k in range(args.warmup):
-            step(k)
-        engine.sync()
-        t0 = time.perf_counter()
-        for k in range(args.warmup, args.warmup + args.steps):
-            step(k)
-        engine.sync()
-        dt = time.perf_counter() - t0
-        rows = len(bp.owned_rows(Hh, args.world, args.rank))
+        v, ms, rows = bench.rank_share_run(engine, args.workload, W, Hh, args.world, args.rank, args.warmup, args.steps)
         q = engine.queue_stats()
         print(json.dumps({"workload": args.workload, "size": [W, Hh], "world": args.world, "rank": args.rank,
-                          "rows": rows, "mpaths_per_s": round(rows * W * args.steps / dt / 1e6, 2),
-                          "ms_per_frame": round(1e3 * dt / args.steps, 4),
+                          "rows": rows, "mpaths_per_s": round(v, 2), "ms_per_frame": round(ms, 4),
                           "late_bounce_compaction": q["late_bounce_compaction"],
                           "frames_in_flight": q["frames_in_flight"], "env": {k: v for k, v in os.environ.items()
                                                                              if k.startswith("PT_")}}))
