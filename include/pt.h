@@ -10,9 +10,10 @@
  * and never throws. Device memory is owned by the context. Host arrays are copied at the call.
  * All work of a context is ordered on one HIP stream (the context's own, or the caller's: pt_set_stream);
  * pt_render is asynchronous and pt_read_pixels / pt_sync synchronise. The megakernel's path tracing of a
- * frame runs on an internal side stream beside the previous frame's (frame overlap: it never reads the
- * history) and the history blend that follows it runs on that one stream, so every observable result
- * is in call order. Not re-entrant (single JS thread, like the reference).
+ * frame runs on one of the context's internal side streams (two or three, PT_OVERLAP_DEPTH) beside the
+ * previous frames' (frame overlap: it never reads the history), gated by events recorded on the
+ * context's stream, and the history blend that follows it runs on that one stream, so every observable
+ * result is in call order. Not re-entrant (single JS thread, like the reference).
  * Image rows are stored bottom-up (row 0 = gl_FragCoord.y 0.5), as GL render targets are.
  */
 #ifndef PT_H
