@@ -31,11 +31,11 @@ extern "C" {
 hipError_t pt_launch_exhaustive(int op, unsigned long long* bad, hipStream_t s);
 hipError_t pt_launch_trace(int prog, int count, const pt::TraceArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,
-                                 unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s);
+                                 unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s, int threads);
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
-hipError_t pt_launch_blend(const pt::BlendArgs* a, int bands, hipStream_t s);
+hipError_t pt_launch_blend(const pt::BlendArgs* a, int bands, hipStream_t s, int waves);
 hipError_t pt_launch_cont(int prog, const pt::TraceArgs* a, int waves, hipStream_t s);
-hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s);
+hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s, int waves);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
 hipError_t pt_launch_persist(int prog, int count, const pt::TraceArgs* a, const pt::WfBufs* w, int tiles_x,
                              unsigned n_wave_tiles, unsigned per_wave, unsigned refill, hipStream_t s);
@@ -214,6 +214,11 @@ struct Dev {
     struct { bool on; unsigned n; const unsigned* cost; unsigned* order; unsigned* split; unsigned cap, dominance; int near; }
         pending_order = {};
     bool fuse_order = true;
+    // (PT_MAIN_WAVES) pt_blend / pt_output as up to this many one-wave workgroups (0: 4-wave blocks):
+    // beside overlapping path tracing a free wave slot comes one at a time, and a 4-wave workgroup waits
+    // for four on one CU (r05bi: dragon stand-in 1080p +2 %, helmet +3 %; at 4K -4 %, so only up to 8192
+    // tiles)
+    int main_waves = 16384;
     unsigned* lpt_mem = nullptr;            // cost[kSetsMax][4 * cap] | order[kSetsMax][cap] | split[kSetsMax]
     size_t lpt_cap = 0;
     struct LptKey { bool valid; size_t n; const void* target; int prog, part, parts; };
@@ -790,7 +795,8 @@ int flush_order(Dev* c)
     if (!c->pending_order.on) return PT_OK;
     c->pending_order.on = false;
     const auto& po = c->pending_order;
-    HIPCHK(c, pt_launch_order_build(po.n, po.cost, po.order, po.split, po.cap, po.dominance, po.near, c->stream));
+    HIPCHK(c, pt_launch_order_build(po.n, po.cost, po.order, po.split, po.cap, po.dominance, po.near, c->stream,
+                                    1024));
     return PT_OK;
 }
 
@@ -1000,7 +1006,8 @@ int render_trace(DevFx* fx, DevTex* target)
     // the history half of main() on the main stream, where the copy / output draws that read the
     // accumulation follow
     pt::BlendArgs b{ a.width, a.height, a.num_parts, a.part, a.frame, a.moving, a.rad, a.prev, a.out, a.cont_count };
-    HIPCHK(c, pt_launch_blend(&b, gy, c->stream));
+    // (one-wave workgroups up to 8192 tiles, as the output pass below)
+    HIPCHK(c, pt_launch_blend(&b, gy, c->stream, n <= pt::kOrderHeld * 64u ? c->main_waves : 0));
     if (a.cost) {   // this draw's costs order draw k + 2: the build rides along with the next screenOutput
         c->pending_order = { true, (unsigned)n, a.cost, c->lpt_order(par), c->lpt_split(par),
                              (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance, c->split_near };
@@ -1096,7 +1103,12 @@ int render_output(DevFx* fx, DevTex* target)
             a.ob_ntiles = po.n; a.ob_cap = po.cap; a.ob_dominance = po.dominance; a.ob_near = po.near;
             c->pending_order.on = false;
         }
-        HIPCHK(c, pt_launch_output(&a, c->stream));
+        // one-wave workgroups while a fused order build fits one wave's registers (<= 8192 tiles: up to
+        // ~2 MP, and a rank's share of 4K), else the 4-wave blocks with a 256-thread order build
+        const int nb = (a.height + 15) / 16, ob = a.part < nb ? (nb - a.part + a.num_parts - 1) / a.num_parts : 0;
+        const unsigned tiles = (unsigned)((a.width + 15) / 16) * (unsigned)ob;   // (as pt_launch_output's grid)
+        const bool one = tiles <= pt::kOrderHeld * 64u && (!a.ob_cost || a.ob_ntiles <= pt::kOrderHeld * 64u);
+        HIPCHK(c, pt_launch_output(&a, c->stream, one ? c->main_waves : 0));
     }
     return end_draw(c, fx->prog);
 }
@@ -1173,6 +1185,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_PRIO_TILES")) c->prio_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PT_MAIN_WAVES")) c->main_waves = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP_DEPTH")) {
         c->depth = std::min(Dev::kDepthMax, std::max(2, std::atoi(v)));

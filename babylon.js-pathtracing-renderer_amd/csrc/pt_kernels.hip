@@ -184,13 +184,8 @@ __global__ __launch_bounds__(256) void pt_copy(CopyArgs a)
 // moves, plus the radiance pt_trace left in `rad`; alpha = the radiance's pre-history flag unless the
 // history's says 1.01 (stays sharp) or -1 (0). Each pixel reads only its own texels, so `prev` may be
 // `out` (in-place history). A block covers 64 columns x one 16-row band, each thread 4 rows, loads first.
-__global__ __launch_bounds__(256) void pt_blend(BlendArgs a)
+PT_D void blendRows(const BlendArgs& a, int x, int r0)
 {
-    const int band = blockIdx.y * a.num_parts + a.part;
-    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int r0 = band * kTile + (threadIdx.x >> 6);
-    if (a.cont_count && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) a.cont_count[threadIdx.x] = 0u;   // counter, queue head (pt_cont is done)
-    if (x >= a.width) return;
     typedef float nt4 __attribute__((ext_vector_type(4)));
     nt4 rv[4], pv[4];
 #pragma unroll
@@ -217,6 +212,28 @@ __global__ __launch_bounds__(256) void pt_blend(BlendArgs a)
         if (prev.w == 1.01f) ca = 1.01f;
         if (prev.w == -1.0f) ca = 0.0f;
         a.out[(long long)y * a.width + x] = make_float4(prev.x + cr, prev.y + cg, prev.z + cb, ca);
+    }
+}
+__global__ __launch_bounds__(256) void pt_blend(BlendArgs a)
+{
+    const int band = blockIdx.y * a.num_parts + a.part;
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int r0 = band * kTile + (threadIdx.x >> 6);
+    if (a.cont_count && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) a.cont_count[threadIdx.x] = 0u;   // counter, queue head (pt_cont is done)
+    if (x >= a.width) return;
+    blendRows(a, x, r0);
+}
+// The same as one-wave workgroups that stride over (64 columns x 4 rows of a band) units: beside the
+// overlapped frames' path tracing a free wave slot comes one at a time, and a 4-wave workgroup waits
+// for four on one CU (the main stream's small kernels then took 100-600 us)
+__global__ __launch_bounds__(64) void pt_blend_w(BlendArgs a, int units_x, int units)
+{
+    if (a.cont_count && blockIdx.x == 0 && threadIdx.x < 2) a.cont_count[threadIdx.x] = 0u;
+    for (int u = blockIdx.x; u < units; u += gridDim.x) {
+        const int cx = u % units_x, rest = u / units_x;
+        const int band = (rest >> 2) * a.num_parts + a.part;
+        const int x = cx * 64 + threadIdx.x;
+        if (x < a.width) blendRows(a, x, band * kTile + (rest & 3));
     }
 }
 
@@ -331,6 +348,61 @@ __global__ __launch_bounds__(256) void pt_output(OutputArgs a, int tiles_x, int 
             tile[cur ^ 1][tid] = f0;
             if (tid + 256 < 400) tile[cur ^ 1][tid + 256] = f1;
         }
+        __syncthreads();
+        t = tn; x0 = nx0; y0 = ny0;
+    }
+}
+
+// The same as one-wave workgroups (see pt_blend_w): 64 threads stage a tile's 20x20 neighbourhood (7
+// texels each, the next tile's loaded into registers while this one is shaded) and shade 4 pixels each
+__global__ __launch_bounds__(64) void pt_output_w(OutputArgs a, int tiles_x, int ntiles)
+{
+    __shared__ float4 tile[2][20 * 20];
+    const int tid = threadIdx.x;
+    const int lx = tid & 15, ly = tid >> 4;
+    auto origin = [&](int t, int& x0, int& y0) {
+        x0 = (t % tiles_x) * 16;
+        y0 = ((t / tiles_x) * a.num_parts + a.part) * 16;
+    };
+    float4 f[7];
+    auto load = [&](int x0, int y0) {
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            const int k = tid + 64 * i;
+            if (k < 400) f[i] = accAt(a, x0 + k % 20 - 2, y0 + k / 20 - 2);
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            const int k = tid + 64 * i;
+            if (k < 400) tile[buf][k] = f[i];
+        }
+    };
+    int bid = (int)blockIdx.x, nblk = (int)gridDim.x;
+    if (a.ob_cost) {   // block 0: the next megakernel draw's order (pt_order_build), beside the tiles
+        if (bid == 0) {
+            orderBuild(a.ob_ntiles, a.ob_cost, a.ob_order, a.ob_split, a.ob_cap, a.ob_dominance, a.ob_near);
+            return;
+        }
+        bid--; nblk--;
+    }
+    int t = bid, x0, y0;
+    if (t >= ntiles) return;
+    origin(t, x0, y0);
+    load(x0, y0);
+    store(0);
+    __syncthreads();
+    for (int cur = 0; t < ntiles; cur ^= 1) {
+        const int tn = t + nblk;
+        int nx0 = 0, ny0 = 0;
+        if (tn < ntiles) { origin(tn, nx0, ny0); load(nx0, ny0); }
+#pragma unroll 1
+        for (int j = 0; j < 4; j++) {
+            const int x = x0 + lx, y = y0 + ly + 4 * j;
+            if (x < a.width && y < a.height) outputPixel(a, tile[cur], lx, ly + 4 * j, x, y);
+        }
+        if (tn < ntiles) store(cur ^ 1);
         __syncthreads();
         t = tn; x0 = nx0; y0 = ny0;
     }
@@ -593,9 +665,9 @@ hipError_t pt_launch_cont(int prog, const pt::TraceArgs* a, int waves, hipStream
 }
 
 hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,
-                                 unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s)
+                                 unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s, int threads)
 {
-    hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(1024), 0, s, ntiles, cost, order, split, split_cap, dominance,
+    hipLaunchKernelGGL(pt::pt_order_build, dim3(1), dim3(threads), 0, s, ntiles, cost, order, split, split_cap, dominance,
                        near_buckets);
     return hipGetLastError();
 }
@@ -649,9 +721,14 @@ hipError_t pt_launch_trail_pass(int pass, const float4* aabb, long long texels, 
     return hipGetLastError();
 }
 
-hipError_t pt_launch_blend(const pt::BlendArgs* a, int bands, hipStream_t s)
+hipError_t pt_launch_blend(const pt::BlendArgs* a, int bands, hipStream_t s, int waves)
 {
     if (bands <= 0) return hipSuccess;
+    if (waves > 0) {
+        const int ux = (a->width + 63) / 64, units = ux * bands * 4;
+        hipLaunchKernelGGL(pt::pt_blend_w, dim3(units < waves ? units : waves), dim3(64), 0, s, *a, ux, units);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(pt::pt_blend, dim3((a->width + 63) / 64, bands), dim3(256), 0, s, *a);
     return hipGetLastError();
 }
@@ -662,7 +739,7 @@ hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStre
     return hipGetLastError();
 }
 
-hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s)
+hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s, int waves)
 {
     const int nb = (a->height + 15) / 16;
     dim3 grid((a->width + 15) / 16, a->part < nb ? (nb - a->part + a->num_parts - 1) / a->num_parts : 0);
@@ -675,6 +752,11 @@ hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s)
     // persistent screenOutput blocks: about four 16x16 tiles each, 4096..8192 (1080p 4096: 37.2 ->
     // 36.1 us; 4K 8192: 122 -> 109 us; profiles/r02i_ab_out_blocks.txt); PT_OUT_BLOCKS fixes the count
     const int ntiles = (int)(grid.x * grid.y);
+    if (waves > 0) {
+        hipLaunchKernelGGL(pt::pt_output_w, dim3((ntiles < waves ? ntiles : waves) + (a->ob_cost ? 1 : 0)), dim3(64), 0, s,
+                           *a, (int)grid.x, ntiles);
+        return hipGetLastError();
+    }
 #ifdef PT_OUT_BLOCKS
     const int blocks = PT_OUT_BLOCKS;
 #else
