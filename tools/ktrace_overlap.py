@@ -18,7 +18,10 @@ def main():
     ap.add_argument("--rows", action="store_true", help="print every launch")
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.csv)))
-    tr = [r for r in rows if "pt_trace<" in r["Kernel_Name"] and ", true" not in r["Kernel_Name"].split(">")[0]]
+    def counting(name):   # pt_trace<PROG, COUNT, CONT>: the counting variant is not a frame's launch
+        args = name.split("<", 1)[1].split(">", 1)[0].split(",")
+        return len(args) > 1 and args[1].strip() == "true"
+    tr = [r for r in rows if "pt_trace<" in r["Kernel_Name"] and not counting(r["Kernel_Name"])]
     other = [r for r in rows if r not in tr]
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
     tr = tr[-args.last:]
