@@ -138,6 +138,9 @@ struct Dev {
     // cost / order / split (each set is its own longest-first pipeline, draw k ordered by the costs of
     // the set's previous draw); per side stream: the spill slab.
     bool overlap = true;
+    // (PT_MOVING_SERIAL) frames drawn with uCameraIsMoving set run alone, one frame in flight: while the
+    // camera moves, the user sees each frame as soon as it is done instead of two frames later
+    bool moving_serial = true;
     // Depth (PT_OVERLAP_DEPTH, 2-6): side streams; draw k waits for the mark draw k - depth - lag + 1
     // recorded (depth 2, lag 0: the previous draw's), so up to `depth` frames' path tracing are in flight.
     static constexpr int kDepthMax = 6;
@@ -194,6 +197,7 @@ struct Dev {
     size_t cont_auto_pixels = 2000000;   // (PT_CONT_AUTO_PIXELS) the default before the trial: on from 2 MP traced (1080p)
     hipEvent_t tune_ev[2 * kContBlocks] = {};
     int cont_last = 0;   // what the last megakernel draw did (cont_decide)
+    unsigned cont_draws = 0;   // megakernel draws that launched pt_cont, since the context was created
     pt::WfBufs gb = {};           // persistent backend: per-pixel G-buffer + radiance
     void* gb_mem = nullptr;
     size_t gb_pixels = 0;
@@ -967,6 +971,7 @@ int render_trace(DevFx* fx, DevTex* target)
     // megakernel draw began (or now: the first draw, after another schedule or a stream switch, with
     // counting kernels, or when a sampler is a render target, which draws on the main stream may write)
     bool overlap = c->overlap && !c->counting && !PT_SECPROF_BUILD;   // (experiment builds: one wave log)
+    if (a.moving && c->moving_serial) overlap = false;
     for (const auto& kv : fx->samplers)
         if (kv.second && kv.second->kind == TEX_RT && kv.first != "previousBuffer") overlap = false;
     hipStream_t ts = c->stream;
@@ -995,10 +1000,13 @@ int render_trace(DevFx* fx, DevTex* target)
     a.ntiles = (unsigned)n;
     if (int rc = begin_draw(c, fx->prog, ts)) return rc;
     HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, ts));
-    // (the draw's timing events bracket pt_trace alone, as a kernel trace reports it; pt_cont follows)
-    if (int rc = end_draw(c, fx->prog, ts)) return rc;
-    if (cont)   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
+    if (cont) {   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
         HIPCHK(c, pt_launch_cont(fx->prog, &a, (int)std::min<size_t>(c->cont_waves, (size_t)gx * gy * 4), ts));
+        c->cont_draws++;
+    }
+    // the draw's timing events bracket all of its path tracing on the side stream: pt_trace and, when the
+    // draw compacts, pt_cont (the blend below is the main stream's)
+    if (int rc = end_draw(c, fx->prog, ts)) return rc;
     if (overlap) {
         HIPCHK(c, hipEventRecord(c->ev_traced[str], ts));
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_traced[str], 0));
@@ -1187,6 +1195,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_MAIN_WAVES")) c->main_waves = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PT_MOVING_SERIAL")) c->moving_serial = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP_DEPTH")) {
         c->depth = std::min(Dev::kDepthMax, std::max(2, std::atoi(v)));
         c->depth_env = true;
@@ -1583,6 +1592,30 @@ int dev_timing_end(Dev* c, int prog, double* total_ms, int* launches)
     return PT_OK;
 }
 
+int dev_timing_latency(Dev* c, int prog, float* ms, int cap, int* n)
+{
+    if (!c || !n || cap < 0 || (cap && !ms)) return PT_ERR_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = flush_copy(c)) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->window = false;
+    // each bracketed draw of `prog` with the next bracketed screenOutput draw: the same frame's, as long as
+    // every frame draws one of each (the window brackets every timing_every-th draw of each kind)
+    int k = 0, open = -1;
+    for (auto& d : c->window_draws) {
+        if (d.first == prog) open = d.second;
+        else if (d.first == PT_PROG_SCREEN_OUTPUT && open >= 0) {
+            float t = 0.0f;
+            HIPCHK(c, hipEventElapsedTime(&t, c->pool[open].first, c->pool[d.second].second));
+            if (k < cap) ms[k] = t;
+            k++;
+            open = -1;
+        }
+    }
+    *n = std::min(k, cap);
+    return PT_OK;
+}
+
 int dev_set_counting(Dev* c, int enable)
 {
     if (!c) return PT_ERR_ARG;
@@ -1619,8 +1652,9 @@ int dev_queue_stats(Dev* c, uint32_t out[16])
         HIPCHK(c, hipMemcpy(&out[7], c->lpt_split(p), sizeof(uint32_t), hipMemcpyDeviceToHost));
     // late-bounce compaction of the last megakernel draw: 0 off, 1 auto decided off, 2 auto decided on,
     // 3 forced on (PT_CONT=1), 4 auto trial, 5 / 6 default on / off; bits 8-15: its frames in flight;
+    // bits 16-31: the draws that launched pt_cont so far (mod 2^16);
     // out[15]: the auto trial's ms with it on per ms without (the faster depth), x 1000
-    out[14] = (uint32_t)c->cont_last | (uint32_t)c->depth_run << 8;
+    out[14] = (uint32_t)c->cont_last | (uint32_t)c->depth_run << 8 | (c->cont_draws & 0xffffu) << 16;
     const float off = std::min(c->tune.ms_off, c->tune.ms_off2);
     out[15] = (c->cont_last == 1 || c->cont_last == 2) && off > 0.0f ? (uint32_t)(1000.0f * c->tune.ms_on / off) : 0u;
     if (!c->wf_mem) return PT_OK;

@@ -49,6 +49,7 @@ int dev_timing_end(Dev* c, int prog, double* total_ms, int* launches);
 int dev_set_counting(Dev* c, int enable);
 int dev_read_counters(Dev* c, uint64_t out[PT_NUM_COUNTERS]);
 int dev_reset_counters(Dev* c);
+int dev_timing_latency(Dev* c, int prog, float* ms, int cap, int* n);
 int dev_queue_stats(Dev* c, uint32_t out[16]);
 int dev_math_exhaustive(Dev* c, int op, uint64_t* mismatches);
 int dev_math_probe(Dev* c, int op, const float* x, const float* y, float* out, int n);

@@ -621,6 +621,21 @@ int pt_timing_end(pt_ctx* c, int prog, double* total_ms, int* launches)
     return PT_OK;
 }
 
+int pt_timing_latency(pt_ctx* c, int prog, float* ms, int cap, int* n)
+{
+    if (!c || !n || cap < 0 || (cap && !ms)) return PT_ERR_ARG;
+    std::vector<float> part((size_t)cap);
+    int n0 = 0;
+    for (int k = 0; k < c->n(); k++) {
+        int m = 0;
+        if (int rc = take(c, k, dev_timing_latency(c->parts[k], prog, part.data(), cap, &m))) return rc;
+        if (k == 0) { n0 = m; for (int i = 0; i < m; i++) ms[i] = part[i]; }
+        else for (int i = 0; i < std::min(m, n0); i++) ms[i] = std::max(ms[i], part[i]);   // the slowest part's canvas
+    }
+    *n = n0;
+    return PT_OK;
+}
+
 int pt_set_counting(pt_ctx* c, int enable)
 {
     if (!c) return PT_ERR_ARG;

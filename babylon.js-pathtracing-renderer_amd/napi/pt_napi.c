@@ -328,6 +328,17 @@ static napi_value TimingEnd(napi_env env, napi_callback_info info)
     napi_set_element(env, r, 2, num(env, n));
     return r;
 }
+static napi_value TimingLatency(napi_env env, napi_callback_info info)
+{
+    napi_value a[MAXARGS], r; if (args(env, info, a, 2) < 0) return NULL;
+    float ms[1024]; int n = 0;
+    int rc = pt_timing_latency((pt_ctx*)handle(env, a[0]), i32(env, a[1]), ms, 1024, &n);
+    if (rc != PT_OK) n = 0;
+    CHECK(napi_create_array_with_length(env, (size_t)n + 1, &r));
+    napi_set_element(env, r, 0, num(env, rc));
+    for (int i = 0; i < n; i++) napi_set_element(env, r, (uint32_t)i + 1, num(env, ms[i]));
+    return r;
+}
 static napi_value SetCounting(napi_env env, napi_callback_info info)
 { napi_value a[MAXARGS]; if (args(env, info, a, 2) < 0) return NULL; return num(env, pt_set_counting((pt_ctx*)handle(env, a[0]), i32(env, a[1]))); }
 static napi_value ReadCounters(napi_env env, napi_callback_info info)
@@ -424,6 +435,7 @@ static napi_value Init(napi_env env, napi_value exports)
         { "pt_set_row_partition", RowPartition }, { "pt_set_backend", SetBackend }, { "pt_set_output_partition", SetOutputPartition }, { "pt_canvas_wrap", CanvasWrap }, { "pt_set_bvh_layout", SetBvhLayout },
         { "pt_bvh_layout_used", BvhLayoutUsed }, { "pt_set_stream", SetStream }, { "pt_texture_device_ptr", TexDevicePtr },
         { "pt_last_render_ms", LastRenderMs }, { "pt_timing_begin", TimingBegin }, { "pt_timing_end", TimingEnd },
+        { "pt_timing_latency", TimingLatency },
         { "pt_set_counting", SetCounting }, { "pt_read_counters", ReadCounters }, { "pt_reset_counters", ResetCounters }, { "pt_queue_stats", QueueStats },
         { "pt_bvh_build", BvhBuild }, { "pt_bvh_build_gpu", BvhBuildGpu },
         { "pt_jpeg_size", JpegSize }, { "pt_jpeg_decode_rgba8", JpegDecode }, { "pt_version", Version },

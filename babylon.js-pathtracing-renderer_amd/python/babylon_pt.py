@@ -39,7 +39,7 @@ SYMBOLS = [
     "pt_texture_create_rgba32f", "pt_texture_create_rgba8", "pt_render_target_create", "pt_render_target_wrap",
     "pt_render_target_resize", "pt_texture_size", "pt_texture_destroy",
     "pt_render", "pt_read_pixels", "pt_write_pixels",
-    "pt_set_row_partition", "pt_set_output_partition", "pt_canvas_wrap", "pt_set_backend", "pt_set_bvh_layout", "pt_bvh_layout_used", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end",
+    "pt_set_row_partition", "pt_set_output_partition", "pt_canvas_wrap", "pt_set_backend", "pt_set_bvh_layout", "pt_bvh_layout_used", "pt_set_stream", "pt_texture_device_ptr", "pt_last_render_ms", "pt_timing_begin", "pt_timing_end", "pt_timing_latency",
     "pt_set_counting", "pt_read_counters", "pt_reset_counters", "pt_queue_stats", "pt_math_probe", "pt_math_exhaustive", "pt_bvh_build", "pt_bvh_build_gpu", "pt_jpeg_size", "pt_jpeg_decode_rgba8", "pt_version",
 ]
 
@@ -85,6 +85,7 @@ def lib():
         "pt_last_render_ms": ([vp, i32, f32p], i32), "pt_set_counting": ([vp, i32], i32),
         "pt_timing_begin": ([vp], i32),
         "pt_timing_end": ([vp, i32, ctypes.POINTER(ctypes.c_double), ip], i32),
+        "pt_timing_latency": ([vp, i32, ctypes.POINTER(ctypes.c_float), i32, ip], i32),
         "pt_read_counters": ([vp, ctypes.POINTER(ctypes.c_uint64)], i32), "pt_reset_counters": ([vp], i32),
         "pt_math_probe": ([vp, i32, vp, vp, vp, i32], i32),
         "pt_math_exhaustive": ([vp, i32, vp], i32),
@@ -197,6 +198,15 @@ class Engine:
         self.check(lib().pt_timing_end(self.ctx, PROG.get(program, program), ctypes.byref(t), ctypes.byref(n)), "pt_timing_end")
         return t.value, n.value
 
+    def timing_latency(self, program, cap=4096):
+        """Per-frame ms from each bracketed `program` draw's begin (its path tracing may start) to the
+        next bracketed screenOutput's end (its canvas complete), since timing_begin (synchronises)."""
+        buf = (ctypes.c_float * cap)()
+        n = ctypes.c_int(0)
+        self.check(lib().pt_timing_latency(self.ctx, PROG.get(program, program), buf, cap, ctypes.byref(n)),
+                   "pt_timing_latency")
+        return list(buf[:n.value])
+
     def set_counting(self, on):
         self.check(lib().pt_set_counting(self.ctx, 1 if on else 0))
 
@@ -218,7 +228,8 @@ class Engine:
         return {"paths": list(buf[0:7]), "bvh": list(buf[8:14]), "split_tiles": int(buf[7]),
                 "late_bounce_compaction": {0: "off", 1: "auto: off", 2: "auto: on", 3: "on", 4: "auto: trial",
                                            5: "auto: default on", 6: "auto: default off"}[int(buf[14]) & 0xFF],
-                "frames_in_flight": int(buf[14]) >> 8,
+                "frames_in_flight": (int(buf[14]) >> 8) & 0xFF,
+                "compacting_draws": int(buf[14]) >> 16,
                 "compaction_trial_ratio": buf[15] / 1000.0 if buf[15] else None}
 
     def math_probe(self, op, x, y=None):

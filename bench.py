@@ -25,14 +25,16 @@ torch stream (not the legacy default stream). Rank 0 then measures the same fram
 through one multi-part context (`--engine multipart`: libpt's own fan-out, peer copies, no RCCL) in a
 child process and adds it to the line as `multipart`.
 
-At N = 1 the line also carries the roofline of the path-tracing kernel: algorithmic bytes per launch
-(counted exactly by a counting replay of the same frames) over the average launch
-time (HIP events in the timed region) against 8 TB/s, and the L2-to-fabric traffic of the same
-kernel measured live by two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) over 5 frames of the
-same workload, and the CPU baseline (the oracle on the host's cores available to this job, pinned
-with taskset, in a child process); and, for the default dragon workload, fields measured in the same
-run: the 4K frame on one GPU (`dragon_4k_1gpu`), the scan-like stand-in (`bunny16_1080p`) and
-configs[4]'s 1024-frame converging run timed whole (`converge_1024spp`). Prints ONE JSON line (rank 0).
+At N = 1 the line also carries the roofline of the path tracing: algorithmic bytes per frame (SURVEY.md
+§8d, counted exactly by a counting replay of the same frames) over ms_per_step against 8 TB/s, the
+L2-to-fabric traffic and VALU instructions of pt_trace + pt_cont measured live by rocprofv3 --pmc passes
+(FETCH_SIZE, WRITE_SIZE, SQ_INSTS_VALU) over 5 frames of the same workload, the bound those fractions
+name, and the frame latency (a frame's path tracing ready -> its canvas complete); the CPU baseline (the
+oracle on the host's cores available to this job, pinned with taskset, in a child process); and, for the
+default dragon workload, fields measured in the same run: the 4K frame on one GPU (`dragon_4k_1gpu`), the
+scan-like stand-in (`bunny16_1080p`), one rank's share of the 4K frame at N = 2/4/8 (`rank_share_4k`) and
+configs[4]'s 1024-frame converging run timed whole (`converge_1024spp`), the 4K ones with the same roofline
+object. Prints ONE JSON line (rank 0).
 """
 import argparse
 import csv
@@ -101,31 +103,59 @@ SIMDS, VALU_CYC = 1024, 2   # 4 SIMDs per CU; a wave64 VALU instruction issues o
 
 
 def roofline_fracs(bytes_per_launch, counts, kernel_ms, frame_ms, traffic, valu=None):
-    """The bounds the path-tracing kernel can be held against, as fractions:
-    frac          SURVEY §8d: reference-priced algorithmic bytes per launch / the launch's average HIP-event
-                  span / 8 TB/s (with frames overlapping, a span includes time shared with the neighbouring
-                  frames' launches);
-    frac_frame    the same bytes per displayed frame / ms_per_step (one launch per frame): the rate the
-                  job sustains;
-    counter_frac  the measured L2-to-fabric bytes (2 x FETCH_SIZE + WRITE_SIZE) per launch / ms_per_step / 8 TB/s
-                  (null without the PMC passes);
+    """The bounds the path tracing can be held against, as fractions of one displayed
+    frame's time (ms_per_step: with frames in flight that is the time the job spends per frame):
+    frac          SURVEY §8d: reference-priced algorithmic bytes per frame / ms_per_step / 8 TB/s;
+    frac_span     the same bytes over the average HIP-event span of a frame's path tracing on its side
+                  stream (pt_trace, and pt_cont when the draw compacts; with frames overlapping a span
+                  includes time shared with the neighbouring frames' kernels, so it is no kernel time);
+    counter_frac  the measured L2-to-fabric bytes of pt_trace + pt_cont (2 x FETCH_SIZE + WRITE_SIZE) per
+                  frame / ms_per_step / 8 TB/s (null without the PMC passes);
     pipe_frac     the walk's lane-steps (node fetches / 2 inner steps + leaf tests) x the memory pipe's cost per
                   lane-step at full waves (PIPE_CYC_PER_LANE_STEP) / (256 CUs x ms_per_step x 2.4 GHz): how busy
                   the vector-memory path would be if every load instruction ran 64 lanes;
-    valu_frac     the kernel's VALU wave-instructions per launch (PMC SQ_INSTS_VALU) x 2 issue cycles / (1024 SIMDs
-                  x ms_per_step x 2.4 GHz): how busy the SIMDs' vector issue is (null without the PMC passes)."""
+    valu_frac     the VALU wave-instructions of pt_trace + pt_cont per frame (PMC SQ_INSTS_VALU) x 2 issue cycles /
+                  (1024 SIMDs x ms_per_step x 2.4 GHz): how busy the SIMDs' vector issue is (null without PMC).
+    bound         the resource with the largest of these fractions: "hbm" (frac or counter_frac), "vmem"
+                  (pipe_frac) or "valu" (valu_frac)."""
     peak = PEAK_HBM_GBS * 1e9
     inner, leaf = counts["node_fetches"] / 2.0, counts["leaf_tests"]
     pipe_cycles = inner * PIPE_CYC_PER_LANE_STEP["inner"] + leaf * PIPE_CYC_PER_LANE_STEP["leaf"]
-    return {"frac": round(bytes_per_launch / (kernel_ms * 1e-3) / peak, 4),
-            "frac_frame": round(bytes_per_launch / (frame_ms * 1e-3) / peak, 4),
-            "counter_frac": round(traffic / (frame_ms * 1e-3) / peak, 4) if traffic else None,
-            "pipe_frac": round(pipe_cycles / (CUS * frame_ms * 1e-3 * CLOCK_GHZ * 1e9), 4),
-            "valu_frac": round(valu * VALU_CYC / (SIMDS * frame_ms * 1e-3 * CLOCK_GHZ * 1e9), 4) if valu else None,
-            "pipe_model": {"lane_steps_per_launch": int(inner + leaf),
-                           "cycles_per_lane_step": {k: round(v, 3) for k, v in PIPE_CYC_PER_LANE_STEP.items()},
-                           "source": "tools/ubench/td_width.hip (profiles/r03_ubench_td_width.txt), 64 active lanes",
-                           "cus": CUS, "clock_ghz": CLOCK_GHZ}}
+    f = {"frac": round(bytes_per_launch / (frame_ms * 1e-3) / peak, 4),
+         "frac_span": round(bytes_per_launch / (kernel_ms * 1e-3) / peak, 4) if kernel_ms else None,
+         "counter_frac": round(traffic / (frame_ms * 1e-3) / peak, 4) if traffic else None,
+         "pipe_frac": round(pipe_cycles / (CUS * frame_ms * 1e-3 * CLOCK_GHZ * 1e9), 4),
+         "valu_frac": round(valu * VALU_CYC / (SIMDS * frame_ms * 1e-3 * CLOCK_GHZ * 1e9), 4) if valu else None,
+         "pipe_model": {"lane_steps_per_launch": int(inner + leaf),
+                        "cycles_per_lane_step": {k: round(v, 3) for k, v in PIPE_CYC_PER_LANE_STEP.items()},
+                        "source": "tools/ubench/td_width.hip (profiles/r03_ubench_td_width.txt), 64 active lanes",
+                        "cus": CUS, "clock_ghz": CLOCK_GHZ}}
+    cand = {"frac": "hbm", "counter_frac": "hbm", "pipe_frac": "vmem", "valu_frac": "valu"}
+    key = max((k for k in cand if f[k] is not None), key=lambda k: f[k])
+    f["bound"], f["bound_by"] = cand[key], key
+    return f
+
+
+def roofline_object(bytes_per_frame, counts, span_ms, frame_ms, traffic, valu, kernels, note):
+    """The line's roofline object for one workload: every rate over ms_per_step (roofline_fracs), the
+    kernels its traffic and VALU count cover named."""
+    fr = roofline_fracs(bytes_per_frame, counts, span_ms, frame_ms, traffic, valu)
+    return {"bound": fr["bound"], "bound_by": fr["bound_by"],
+            "achieved": round(bytes_per_frame / (frame_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": fr["frac"], "traffic": traffic,
+            "frac_span": fr["frac_span"], "counter_frac": fr["counter_frac"], "pipe_frac": fr["pipe_frac"],
+            "valu_frac": fr["valu_frac"], "valu_insts_per_launch": int(valu) if valu else None,
+            "pipe_model": fr["pipe_model"],
+            "achieved_counter_gbs": round(traffic / (frame_ms * 1e-3) / 1e9, 1) if traffic else None,
+            "traffic_source": ("live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU passes over 5 frames of this "
+                               "workload, (2 x FETCH_SIZE + WRITE_SIZE) x 1024 B per frame (gfx950 correction)")
+            if traffic else note,
+            "kernels": kernels, "algorithmic_bytes_per_launch": int(bytes_per_frame),
+            "counts_per_launch": counts,
+            "rates_over": "ms_per_step (one displayed frame; frames overlap, DESIGN.md §4)",
+            "pricing": ("the reference's work (counting variant: full closest-hit walks and hit lookups); the "
+                        "timed kernel ends shadow rays and eligible last segments at their first occluder "
+                        "(same image bits, DESIGN.md §6), so 'achieved' is reference work per second")}
 
 
 def baseline_metric():
@@ -188,7 +218,7 @@ def cpu_baseline(workload, budget):
 
 
 # ------------------------------------------------------------------------------ live PMC traffic
-def live_traffic(workload, W, Hh, frames=5):
+def live_traffic(workload, W, Hh, frames=5, parts=1, part=0):
     """L2-to-fabric bytes and vector-ALU instructions per frame of the path tracing (pt_trace, and
     pt_cont when late-bounce compaction runs), measured now: three rocprofv3 --pmc passes (FETCH_SIZE and WRITE_SIZE need 3 + 2 of the 4 TCC slots, so one
     pass each; SQ_INSTS_VALU) over tools/prof_frames.py rendering `frames` frames of this workload.
@@ -204,7 +234,8 @@ def live_traffic(workload, W, Hh, frames=5):
             out = os.path.join(tmp, ctr)
             cmd = ["timeout", "-s", "KILL", "90", exe, "--kernel-trace", "--pmc", ctr, "--output-format", "csv",
                    "-d", out, "-o", "run", "--", sys.executable, os.path.join(ROOT, "tools", "prof_frames.py"),
-                   "--workload", workload, "--frames", str(frames), "--width", str(W), "--height", str(Hh)]
+                   "--workload", workload, "--frames", str(frames), "--width", str(W), "--height", str(Hh),
+                   "--parts", str(parts), "--part", str(part)]
             r = subprocess.run(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"), capture_output=True, text=True)
             if r.returncode != 0:
                 return None, None, "rocprofv3 --pmc %s exited %d" % (ctr, r.returncode)
@@ -323,9 +354,24 @@ def compare_frames(canvas, acc, ref_canvas, ref_acc):
             "pixels": int(canvas.shape[0] * canvas.shape[1])}
 
 
+def latency_summary(lat, ms_per_step):
+    """frame_latency_ms of a line: p50 / max over the bracketed frames (pt_timing_latency) of the device
+    time from a frame's path tracing becoming ready on its stream to its canvas being complete."""
+    if not lat:
+        return None
+    v = sorted(lat)
+    p50 = v[len(v) // 2] if len(v) % 2 else 0.5 * (v[len(v) // 2 - 1] + v[len(v) // 2])
+    return {"p50": round(p50, 4), "max": round(v[-1], 4), "frames": len(v),
+            "p50_per_step": round(p50 / ms_per_step, 3) if ms_per_step else None,
+            "definition": "device time from a frame's path-tracing draw being ready to start (event on its side "
+                          "stream after the waits that order it) to the end of its screenOutput (canvas "
+                          "complete, main stream); every event_every-th frame of the timed region"}
+
+
 def timed_region(engine, step, first, count, event_every, barrier_sync, program):
     """`count` steps from frame index `first`, bracketed by barrier_sync, with HIP-event windows around
-    every event_every-th draw of each kind. Returns (elapsed s, kernel_ms dict, bracketed launches)."""
+    every event_every-th draw of each kind. Returns (elapsed s, kernel_ms dict, bracketed launches,
+    per-frame latencies in ms)."""
     os.environ["PT_TIMING_EVERY"] = str(event_every)
     engine.timing_begin()
     t0 = time.perf_counter()
@@ -336,9 +382,10 @@ def timed_region(engine, step, first, count, event_every, barrier_sync, program)
     pt_ms, pt_n = engine.timing_end(program)
     cp_ms, _ = engine.timing_end("screenCopy")
     out_ms, _ = engine.timing_end("screenOutput")
+    lat = engine.timing_latency(program)
     n = max(1, pt_n)
     return elapsed, {"pathtrace": round(pt_ms / n, 4), "screen_copy": round(cp_ms / n, 4),
-                     "screen_output": round(out_ms / n, 4)}, pt_n
+                     "screen_output": round(out_ms / n, 4)}, pt_n, lat
 
 
 def kernel_name(layout, program, workload):
@@ -351,7 +398,7 @@ def single_gpu_run(engine, workload, W, Hh, warmup, steps, event_every, from_fra
     from_frame_one the run starts at the stream's frame 1 (history cleared, the recorded frames
     first), so the last timed frame is frame warmup + steps of a progressive run from scratch
     (configs[4]); else it continues after the recording. Returns (player, program, triangles,
-    elapsed s, kernel_ms, bracketed launches)."""
+    elapsed s, kernel_ms, bracketed launches, per-frame latencies)."""
     player, program, tris = make_player(engine, workload, W, Hh)
     engine.resize_canvas(W, Hh)
     nrec = len(player.meta["frames"])
@@ -366,38 +413,37 @@ def single_gpu_run(engine, workload, W, Hh, warmup, steps, event_every, from_fra
     for k in range(warmup):
         step(k)
     engine.sync()
-    elapsed, km, n = timed_region(engine, step, warmup, steps, event_every, engine.sync, program)
-    return player, program, tris, elapsed, km, n
+    elapsed, km, n, lat = timed_region(engine, step, warmup, steps, event_every, engine.sync, program)
+    return player, program, tris, elapsed, km, n, lat
 
 
 def rank_share_run(engine, workload, W, Hh, world, rank, warmup, steps):
     """One rank's share of an N-GPU frame on this GPU: the rank's 16-row bands of the N-way partition,
     pathTracing + screenCopy of them and screenOutput of them, as the ranks draw them, without the RCCL
     halo exchange and gather (the per-rank half of a strong-scaling point; tools/rank_proxy.py).
-    Returns (Mpaths/s of the rank's own pixels, ms per frame, rows)."""
+    Returns (Mpaths/s of the rank's own pixels, ms per frame, rows, player, frame latencies). The
+    partition stays set (the caller's counting replay prices the same bands); end_partition resets it."""
     import babylon_pt as bp
-    player, _, _ = make_player(engine, workload, W, Hh)
+    player, program, _ = make_player(engine, workload, W, Hh)
     engine.resize_canvas(W, Hh)
     engine.set_row_partition(world, rank)
     engine.set_output_partition(True)
-    try:
-        def step(k):
-            for call in player.synth_frame(k):
-                player.play_call(call)
 
-        for k in range(warmup):
-            step(k)
-        engine.sync()
-        t0 = time.perf_counter()
-        for k in range(warmup, warmup + steps):
-            step(k)
-        engine.sync()
-        dt = time.perf_counter() - t0
-    finally:
-        engine.set_output_partition(False)
-        engine.set_row_partition(1, 0)
+    def step(k):
+        for call in player.synth_frame(k):
+            player.play_call(call)
+
+    for k in range(warmup):
+        step(k)
+    engine.sync()
+    dt, km, _, lat = timed_region(engine, step, warmup, steps, max(1, steps // 10), engine.sync, program)
     rows = len(bp.owned_rows(Hh, world, rank))
-    return rows * W * steps / dt / 1e6, 1e3 * dt / steps, rows
+    return rows * W * steps / dt / 1e6, 1e3 * dt / steps, rows, player, km, lat
+
+
+def end_partition(engine):
+    engine.set_output_partition(False)
+    engine.set_row_partition(1, 0)
 
 
 def compaction(engine):
@@ -405,6 +451,64 @@ def compaction(engine):
     q = engine.queue_stats()
     return {"mode": q["late_bounce_compaction"], "trial_ms_on_per_off": q["compaction_trial_ratio"],
             "frames_in_flight": q["frames_in_flight"]}
+
+
+def counted_frame(engine, player, first, n=5):
+    """Algorithmic-byte counts per frame of the frames just measured: a counting (untimed) replay of the
+    path-tracing draws of synthetic frames first.. first + n - 1 on the same engine, target and partition
+    (counting draws neither overlap nor compact: the counts are the reference's work). Returns
+    (bytes per frame, counts per frame)."""
+    engine.set_counting(True)
+    engine.reset_counters()
+    for k in range(first, first + n):
+        player.play_call(player.synth_frame(k)[0])
+    cnt = engine.counters()
+    engine.set_counting(False)
+    return algorithmic_bytes(cnt) / n, {k: v / n for k, v in cnt.items()}
+
+
+def pmc_note(args):
+    if args.no_pmc:
+        return "skipped (--no-pmc)"
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        return "skipped (running under rocprofv3)"
+    return None
+
+
+def measure_roofline(engine, player, args, workload, W, Hh, first, frame_ms, span_ms, parts=1, part=0):
+    """The roofline object of a workload just timed at W x H (rank `part` of `parts` when partitioned):
+    counts from the counting replay, PMC bytes and VALU instructions from live rocprofv3 passes at the same
+    size and partition, all over ms_per_step (roofline_object)."""
+    bpf, counts = counted_frame(engine, player, first)
+    note = pmc_note(args)
+    traffic = valu = None
+    if note is None:
+        traffic, valu, note = live_traffic(workload, W, Hh, parts=parts, part=part)
+    kernels = "pt_trace (+ pt_cont when the draws compact) of one frame" + (", rank %d of %d" % (part, parts)
+                                                                              if parts > 1 else "")
+    return roofline_object(bpf, counts, span_ms, frame_ms, traffic, valu, kernels, note)
+
+
+def moving_camera_run(engine, args):
+    """The headline frame while the camera moves: the dragon stand-in at 1920x1080 with uCameraIsMoving
+    set on every path-tracing draw (the reference's 0.5 blend, js/PathTracingCommon.js:1331-1337). Such
+    draws run one frame in flight (PT_MOVING_SERIAL): throughput and frame latency."""
+    player, program, _ = make_player(engine, "dragon", 1920, 1080)
+    engine.resize_canvas(1920, 1080)
+    moving = {"uCameraIsMoving": ["i", [1]]}
+
+    def step(k):
+        for call in player.synth_frame(k):
+            player.play_call(call, uniform_override=moving)
+
+    for k in range(20):
+        step(k)
+    engine.sync()
+    el, km, _, lat = timed_region(engine, step, 20, args.steps, max(1, args.steps // 10), engine.sync, program)
+    ms = el / args.steps * 1e3
+    return {"value": round(1920 * 1080 * args.steps / el / 1e6, 2), "unit": "Mpaths/s", "ms_per_step": round(ms, 4),
+            "steps": args.steps, "kernel_ms": km, "frame_latency_ms": latency_summary(lat, ms),
+            "one_frame_in_flight": os.environ.get("PT_MOVING_SERIAL", "1") != "0"}
 
 
 def run_anchors(engine, args):
@@ -418,33 +522,50 @@ def run_anchors(engine, args):
                      dragon_4k_1gpu's, the strong-scaling curve's per-rank half;
     converge_1024spp - BASELINE configs[4] as a run: sky + dragon stand-in at 3840x2160, frames 1..1024
                      from a cleared history, pathTracing + screenCopy + 5x5 screenOutput each, timed
-                     whole (no extrapolation); --dump-canvas PATH also saves frame 1024's canvas."""
+                     whole (no extrapolation); --dump-canvas PATH also saves frame 1024's canvas.
+    The 4K fields (north_star's target frame) carry the same roofline object as the headline, and
+    every field its frame latency."""
     out = {}
     steps4k = max(20, args.steps // 5)
     # (100 warmup draws: the late-bounce compaction trial ends at the 93rd, DESIGN.md §4)
-    _, _, tris, el, km, n = single_gpu_run(engine, "dragon", 3840, 2160, 100, steps4k, max(1, steps4k // 10))
+    player, _, tris, el, km, n, lat = single_gpu_run(engine, "dragon", 3840, 2160, 100, steps4k, max(1, steps4k // 10))
+    ms = el / steps4k * 1e3
     out["dragon_4k_1gpu"] = {"value": round(3840 * 2160 * steps4k / el / 1e6, 2), "unit": "Mpaths/s",
-                             "ms_per_step": round(el / steps4k * 1e3, 4), "steps": steps4k, "kernel_ms": km,
+                             "ms_per_step": round(ms, 4), "steps": steps4k, "kernel_ms": km,
                              "width": 3840, "height": 2160, "triangles": tris,
-                             "late_bounce_compaction": compaction(engine)}
-    _, _, tris, el, km, n = single_gpu_run(engine, "bunny16", 1920, 1080, 100, args.steps, max(1, args.steps // 10))
+                             "late_bounce_compaction": compaction(engine),
+                             "frame_latency_ms": latency_summary(lat, ms)}
+    out["dragon_4k_1gpu"]["roofline"] = measure_roofline(engine, player, args, "dragon", 3840, 2160, 100 + steps4k,
+                                                         ms, km["pathtrace"])
+    player, _, tris, el, km, n, lat = single_gpu_run(engine, "bunny16", 1920, 1080, 100, args.steps,
+                                                     max(1, args.steps // 10))
+    ms = el / args.steps * 1e3
     out["bunny16_1080p"] = {"value": round(1920 * 1080 * args.steps / el / 1e6, 2), "unit": "Mpaths/s",
-                            "ms_per_step": round(el / args.steps * 1e3, 4), "steps": args.steps, "kernel_ms": km,
+                            "ms_per_step": round(ms, 4), "steps": args.steps, "kernel_ms": km,
                             "triangles": tris, "bvh_walk": engine.bvh_layout_used(),
-                            "late_bounce_compaction": compaction(engine)}
+                            "late_bounce_compaction": compaction(engine), "frame_latency_ms": latency_summary(lat, ms)}
+    out["moving_camera_1080p"] = moving_camera_run(engine, args)
     shares = {}
     for world in (2, 4, 8):
-        v, ms, rows = rank_share_run(engine, "dragon", 3840, 2160, world, 0, 100, 100)
-        shares["n%d" % world] = {"value": round(v, 2), "ms_per_step": round(ms, 4), "rows": rows,
-                                 "per_rank_efficiency": round(v / out["dragon_4k_1gpu"]["value"], 3),
-                                 "late_bounce_compaction": compaction(engine)}
+        v, ms, rows, player, km, lat = rank_share_run(engine, "dragon", 3840, 2160, world, 0, 100, 100)
+        try:
+            shares["n%d" % world] = {"value": round(v, 2), "ms_per_step": round(ms, 4), "rows": rows,
+                                     "per_rank_efficiency": round(v / out["dragon_4k_1gpu"]["value"], 3),
+                                     "kernel_ms": km, "late_bounce_compaction": compaction(engine),
+                                     "frame_latency_ms": latency_summary(lat, ms)}
+            if world == 8:
+                shares["n8"]["roofline"] = measure_roofline(engine, player, args, "dragon", 3840, 2160, 200, ms,
+                                                            km["pathtrace"], parts=8, part=0)
+        finally:
+            end_partition(engine)
     out["rank_share_4k"] = dict(shares, unit="Mpaths/s", note="rank 0's bands of the 3840x2160 dragon stand-in "
                                 "frame split N ways, on this GPU, 100 frames after 100; no halo exchange or gather")
-    _, _, tris, el, km, n = single_gpu_run(engine, "sky_dragon", 3840, 2160, 0, CONVERGED_SPP, CONVERGED_SPP // 10,
-                                           from_frame_one=True)
-    conv = {"seconds": round(el, 4), "frames": CONVERGED_SPP, "ms_per_frame": round(el / CONVERGED_SPP * 1e3, 4),
+    player, _, tris, el, km, n, lat = single_gpu_run(engine, "sky_dragon", 3840, 2160, 0, CONVERGED_SPP,
+                                                     CONVERGED_SPP // 10, from_frame_one=True)
+    ms = el / CONVERGED_SPP * 1e3
+    conv = {"seconds": round(el, 4), "frames": CONVERGED_SPP, "ms_per_frame": round(ms, 4),
             "mpaths_per_s": round(3840 * 2160 * CONVERGED_SPP / el / 1e6, 2), "kernel_ms": km, "measured": True,
-            "late_bounce_compaction": compaction(engine),
+            "late_bounce_compaction": compaction(engine), "frame_latency_ms": latency_summary(lat, ms),
             "note": "frames 1..%d of the sky + dragon stand-in stream from a cleared history, 3840x2160, each "
                     "pathTracing + screenCopy + screenOutput; wall clock of the whole run" % CONVERGED_SPP}
     if args.dump_canvas:
@@ -452,6 +573,8 @@ def run_anchors(engine, args):
         path = os.path.splitext(args.dump_canvas)[0] + "_sky_dragon_%dspp.npy" % CONVERGED_SPP
         np.save(path, engine.read_canvas(3840, 2160))
         conv["canvas"] = os.path.basename(path)
+    conv["roofline"] = measure_roofline(engine, player, args, "sky_dragon", 3840, 2160, CONVERGED_SPP, ms,
+                                        km["pathtrace"])
     out["converge_%dspp" % CONVERGED_SPP] = conv
     return out
 
@@ -486,7 +609,7 @@ def multipart_main(args, event_every):
     for k in range(args.warmup):
         step(k)
     engine.sync()
-    elapsed, km, n = timed_region(engine, step, args.warmup, args.steps, event_every, engine.sync, program)
+    elapsed, km, n, lat = timed_region(engine, step, args.warmup, args.steps, event_every, engine.sync, program)
     if args.dump_canvas:
         import numpy as np
         np.save(args.dump_canvas, engine.read_canvas(W, Hh))
@@ -512,7 +635,7 @@ def multipart_main(args, event_every):
                        "gather": "per frame: 2-row halo pulls from band neighbours and the RGBA8 gather to part 0 "
                                  "as peer copies inside pt_render (hipMemcpy2DAsync, event-ordered)"},
             "kernel_timing": "HIP events around every %d-th timed frame's draws, slowest part (%d launches)" % (event_every, n),
-            "kernel_ms": km}
+            "kernel_ms": km, "frame_latency_ms": latency_summary(lat, elapsed / args.steps * 1e3)}
     if check is not None:
         line["n_gpu_bitexact"] = check["n_gpu_bitexact"]
         line["n_gpu_check"] = check
@@ -745,7 +868,8 @@ def main():
     # kernel durations from HIP event pairs around every event_every-th frame's draws (an event
     # record costs ~5 us of stream time between kernels: bracketing every draw slowed the dragon
     # stand-in's frame by 1.7 %, the bunny's by 3.8 %)
-    elapsed, kernel_ms, pt_n = timed_region(engine, step, args.warmup, args.steps, event_every, barrier_sync, program)
+    elapsed, kernel_ms, pt_n, lat = timed_region(engine, step, args.warmup, args.steps, event_every, barrier_sync,
+                                                 program)
     if args.dump_canvas:
         import numpy as np
         if dist is None:
@@ -774,16 +898,9 @@ def main():
         ranks_seen = dist.get_world_size()
 
     comp = compaction(engine)   # (before the counting replay: counting draws never compact)
-    # algorithmic bytes of the measured launches: a counted (untimed) replay of the same frames
-    engine.set_counting(True)
-    engine.reset_counters()
-    nc = min(args.steps, 5)
-    for k in range(args.warmup, args.warmup + nc):
-        player.play_call(player.synth_frame(k)[0])
-    cnt = engine.counters()
-    engine.set_counting(False)
+    # algorithmic bytes of the measured frames: a counted (untimed) replay of the same frames
+    bytes_per_launch, counts = counted_frame(engine, player, args.warmup, min(args.steps, 5))
     layout = engine.bvh_layout_used()
-    bytes_per_launch = algorithmic_bytes(cnt) / nc
 
     anchors = {}
     if world == 1 and not args.no_anchors and args.workload == "dragon" and args.size is None:
@@ -802,40 +919,21 @@ def main():
 
     paths = W * Hh * args.steps
     value = paths / elapsed / 1e6
-    avg_launch_ms = max(kernel_ms["pathtrace"], 1e-9)
-    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9
+    avg_span_ms = max(kernel_ms["pathtrace"], 1e-9)
     wname = {"bunny": "bunny", "helmet": "helmet_pbr", "dragon": "dragon_standin", "sky_dragon": "dragon_standin",
              "bunny16": "bunny_split16"}
     workload = "%s_%s_%dx%d" % (program, wname[args.workload], W, Hh)
     kernel = kernel_name(layout, program, args.workload)
-    traffic, valu, pmc_note = None, None, "N > 1: not collected"
+    traffic, valu, note = None, None, "N > 1: not collected"
     if world == 1:
-        if args.no_pmc:
-            pmc_note = "skipped (--no-pmc)"
-        elif any(k.startswith("ROCPROF") for k in os.environ):
-            pmc_note = "skipped (running under rocprofv3)"
-        else:
-            traffic, valu, pmc_note = live_traffic(args.workload, W, Hh)
+        note = pmc_note(args)
+        if note is None:
+            traffic, valu, note = live_traffic(args.workload, W, Hh)
     ms_per_step = elapsed / args.steps * 1e3
-    fr = roofline_fracs(bytes_per_launch, {k: v / nc for k, v in cnt.items()}, avg_launch_ms, ms_per_step, traffic,
-                        valu)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                "frac": fr["frac"], "traffic": traffic,
-                "frac_frame": fr["frac_frame"], "counter_frac": fr["counter_frac"], "pipe_frac": fr["pipe_frac"],
-                "valu_frac": fr["valu_frac"], "valu_insts_per_launch": int(valu) if valu else None,
-                "pipe_model": fr["pipe_model"],
-                "achieved_counter_gbs": round(traffic / (avg_launch_ms * 1e-3) / 1e9, 1) if traffic else None,
-                "traffic_source": ("live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over 5 frames of this workload, "
-                                   "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 B per launch (gfx950 correction)")
-                if traffic else pmc_note,
-                "kernel": kernel, "bvh_walk": layout, "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                "counts_per_launch": {k: v / nc for k, v in cnt.items()},
-                "pricing": ("the reference's work (counting variant: full closest-hit walks and hit lookups); the "
-                            "timed kernel ends shadow rays and eligible last segments at their first occluder "
-                            "(same image bits, DESIGN.md §6), so 'achieved' is reference work per second"),
-                "spans": ("frames overlap (pt_trace of frame k+1 runs beside frame k's, DESIGN.md §4): the HIP-event "
-                          "span of a launch includes time shared with its neighbours, so frac (per span) is below "
-                          "frac_frame (per displayed frame)")}
+    roofline = roofline_object(bytes_per_launch, counts, avg_span_ms, ms_per_step, traffic, valu,
+                               "%s (+ pt_cont<...> when the draws compact) of one frame" % kernel, note)
+    roofline["kernel"] = kernel
+    roofline["bvh_walk"] = layout
     ksum = sum(kernel_ms.values())
     line = {
         "metric": baseline_metric() if args.workload == "dragon" else METRICS[args.workload],
@@ -855,9 +953,12 @@ def main():
                    "gather": ("per frame: 2-row halo exchange with band neighbours (RCCL P2P), screenOutput "
                               "of own bands, async RCCL gather of RGBA8 bands to rank 0 overlapping the next "
                               "frame") if world > 1 else None},
-        "pathtrace_mpaths_per_s": round(W * Hh / (avg_launch_ms * 1e-3) / 1e6 * world, 2),
-        "kernel_timing": "HIP events around the draws of every %d-th timed frame (%d launches)" % (event_every, pt_n),
+        "pathtrace_span_mpaths_per_s": round(W * Hh / (avg_span_ms * 1e-3) / 1e6 * world, 2),
+        "kernel_timing": ("HIP events around the draws of every %d-th timed frame (%d launches); pathtrace = the "
+                          "span of a frame's path tracing on its side stream (pt_trace, then pt_cont when the draw "
+                          "compacts), which overlaps the neighbouring frames' spans" % (event_every, pt_n)),
         "kernel_ms": kernel_ms,
+        "frame_latency_ms": latency_summary(lat, ms_per_step),
         # event windows add their own stream time around the bracketed draws: a sum above the step
         # time flags sampled kernel times inflated by them
         "kernel_sum_ms": round(ksum, 4),

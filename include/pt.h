@@ -202,6 +202,14 @@ int pt_last_render_ms(pt_ctx* ctx, int program, float* ms);
  * stream; the launch count returned is then the bracketed draws'. */
 int pt_timing_begin(pt_ctx* ctx);
 int pt_timing_end(pt_ctx* ctx, int program, double* total_ms, int* launches);
+/* Frame latency from the same timing window (closes it and synchronises, like pt_timing_end): for each
+ * bracketed path-tracing draw of `program`, the device time from its begin event (recorded on the stream
+ * its path tracing runs on, after the waits that order it: the moment its frame's path tracing may start)
+ * to the end event of the next bracketed screenOutput draw (its canvas complete, main stream). Writes up
+ * to `cap` values in window order and their count; with several parts, the slowest part's per frame. The
+ * reference displays every frame it draws (js/GLTF_Model_Path_Tracing.js:1228-1237): with frames in
+ * flight this is the draw-to-display delay the overlap adds. */
+int pt_timing_latency(pt_ctx* ctx, int program, float* ms, int cap, int* n);
 /* Algorithmic-byte counters: when enabled, path-tracing passes also accumulate
  * {paths, segments, node_fetches, leaf_tests, hit_lookups, rgba8_taps, stack_overflow, hdr_taps}. */
 #define PT_NUM_COUNTERS 8
@@ -214,7 +222,9 @@ int pt_reset_counters(pt_ctx* ctx);
  * out[14] = late-bounce compaction of the last megakernel draw (PT_CONT: 0 off, 1 on, 2 auto = default):
  * bits 0-7: 0 off, 1 auto decided off, 2 auto decided on, 3 forced on, 4 auto trial running, 5 / 6 auto
  * before the trial, default on / off; bits 8-15: the frames that draw kept in flight (PT_OVERLAP_DEPTH, or 2
- * when the auto trial found two faster without compaction); out[15] = the auto trial's time with
+ * when the auto trial found two faster without compaction); bits 16-31: the path-tracing draws that
+ * launched the late-bounce continuation (pt_cont) since the context was created, mod 2^16;
+ * out[15] = the auto trial's time with
  * compaction per time without (at the faster depth), x 1000 (0 before the decision). */
 int pt_queue_stats(pt_ctx* ctx, uint32_t out[16]);
 /* Device self-test of the pinned GLSL built-ins (ops as the oracle's pto_math_probe). */

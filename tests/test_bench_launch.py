@@ -140,20 +140,43 @@ def test_multipart_devices_fall_back_to_device_zero(monkeypatch):
 
 
 def test_roofline_fracs_formulas():
-    """The roofline's bounds (bench.roofline_fracs) on round 4's dragon stand-in numbers:
-    frac per HIP-event span, frac_frame per displayed frame, counter_frac from the PMC bytes, pipe_frac
-    from the walk's lane-steps priced by the td_width microbenchmark."""
+    """The roofline's bounds (bench.roofline_fracs) on round 5's dragon stand-in numbers: every
+    rate over ms_per_step (frac = reference-priced bytes per displayed frame, counter_frac from the PMC
+    bytes of pt_trace + pt_cont, pipe_frac from the walk's lane-steps priced by the td_width microbenchmark,
+    valu_frac from SQ_INSTS_VALU), the per-span figure under its own name, and the bound the largest
+    fraction names."""
     sys.path.insert(0, ROOT)
     import bench
     counts = {"node_fetches": 90965227.8, "leaf_tests": 4669916.4}
-    f = bench.roofline_fracs(3285147468, counts, 0.9827, 1.0273, 1088e6)
-    assert f["frac"] == round(3285147468 / 0.9827e-3 / 8e12, 4) == 0.4179
-    assert f["frac_frame"] == round(3285147468 / 1.0273e-3 / 8e12, 4)
-    assert f["counter_frac"] == round(1088e6 / 1.0273e-3 / 8e12, 4)
+    f = bench.roofline_fracs(3285147468, counts, 1.0896, 0.8089, 1289260064)
+    assert f["frac"] == round(3285147468 / 0.8089e-3 / 8e12, 4) == 0.5077
+    assert f["frac_span"] == round(3285147468 / 1.0896e-3 / 8e12, 4)
+    assert f["counter_frac"] == round(1289260064 / 0.8089e-3 / 8e12, 4) == 0.1992
     cyc = 90965227.8 / 2 * 243.8 / 64 + 4669916.4 * 189.2 / 64
-    assert f["pipe_frac"] == round(cyc / (256 * 1.0273e-3 * 2.4e9), 4)
-    assert 0.29 < f["pipe_frac"] < 0.31 and f["pipe_model"]["lane_steps_per_launch"] == int(90965227.8 / 2 + 4669916.4)
+    assert f["pipe_frac"] == round(cyc / (256 * 0.8089e-3 * 2.4e9), 4)
+    assert 0.37 < f["pipe_frac"] < 0.38 and f["pipe_model"]["lane_steps_per_launch"] == int(90965227.8 / 2 + 4669916.4)
+    assert (f["bound"], f["bound_by"]) == ("hbm", "frac")          # without the VALU count, the bytes lead
     assert bench.roofline_fracs(1.0, counts, 1.0, 1.0, None)["counter_frac"] is None
     assert bench.roofline_fracs(1.0, counts, 1.0, 1.0, None)["valu_frac"] is None
-    v = bench.roofline_fracs(3285147468, counts, 0.9827, 0.8766, 1.036e9, 7.19e8)["valu_frac"]
-    assert v == round(7.19e8 * 2 / (1024 * 0.8766e-3 * 2.4e9), 4) and 0.6 < v < 0.75
+    v = bench.roofline_fracs(3285147468, counts, 1.0896, 0.8089, 1289260064, 509562504)
+    assert v["valu_frac"] == round(509562504 * 2 / (1024 * 0.8089e-3 * 2.4e9), 4) == 0.5127
+    assert (v["bound"], v["bound_by"]) == ("valu", "valu_frac")   # round 5's line: VALU issue, not HBM
+    # a walk-bound frame (pipe_frac largest)
+    w = bench.roofline_fracs(1e6, {"node_fetches": 4e8, "leaf_tests": 1e7}, 1.0, 1.0, 1e6, 1e6)
+    assert w["bound"] == "vmem"
+    o = bench.roofline_object(3285147468, counts, 1.0896, 0.8089, 1289260064, 509562504, "pt_trace + pt_cont", None)
+    assert o["achieved"] == round(3285147468 / 0.8089e-3 / 1e9, 1) and o["frac"] == 0.5077
+    assert o["achieved_counter_gbs"] == round(1289260064 / 0.8089e-3 / 1e9, 1)
+    assert o["bound"] == "valu" and o["peak"] == 8000.0 and o["unit"] == "GB/s"
+    assert "ms_per_step" in o["rates_over"]
+
+
+def test_frame_latency_summary():
+    """frame_latency_ms: p50 / max of the per-frame latencies the timing window pairs up
+    (pt_timing_latency), and the p50 in frame times."""
+    sys.path.insert(0, ROOT)
+    import bench
+    s = bench.latency_summary([2.0, 3.0, 2.5, 9.0], 1.0)
+    assert (s["p50"], s["max"], s["frames"], s["p50_per_step"]) == (2.75, 9.0, 4, 2.75)
+    assert bench.latency_summary([1.5, 0.5, 1.0], 0.5)["p50"] == 1.0
+    assert bench.latency_summary([], 1.0) is None

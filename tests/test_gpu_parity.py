@@ -330,7 +330,8 @@ def test_overlapped_frames_observed_between_draws(engine, size):
 
 @pytest.mark.parametrize("layout", ["pairs", "trail"])
 def test_late_bounce_compaction_1080p_bitexact(monkeypatch, layout):
-    """Late-bounce compaction forced on (PT_CONT=1, from bounce 2 for waves with <= 32 live paths: the
+    """Late-bounce compaction forced on (PT_CONT=1, from bounce 2 for waves with <= 48 live paths, the
+    default PT_CONT_LANES: the
     pt_trace<P,false,true> variant stores them, pt_cont runs them packed on the draw's side stream):
     the dragon stand-in's four recorded 1920x1080 frames, accumulation and canvas bit-exact."""
     import babylon_pt as bp
@@ -389,6 +390,83 @@ def test_late_bounce_compaction_auto_mode_bitexact(monkeypatch):
     assert qs["late_bounce_compaction"] in ("auto: on", "auto: off"), qs
     assert qs["frames_in_flight"] == 3 if qs["late_bounce_compaction"] == "auto: on" else qs["frames_in_flight"] in (2, 3)
     assert qs["compaction_trial_ratio"] and 0.2 < qs["compaction_trial_ratio"] < 5.0, qs
+
+
+def _oracle_at(meta, frames, W, Hh, mesh, keep_acc, keep_can):
+    """The oracle over `frames` (lists of calls) at W x H, keeping the accumulation after the frames in
+    keep_acc and the canvas after those in keep_can (a 4K run keeps a few frames, not all of them)."""
+    import ptoracle as po
+    sc = H.oracle_scene(meta, W, Hh, mesh)
+    acc = np.zeros((Hh, W, 4), np.float32)
+    accs, cans = {}, {}
+    for i, f in enumerate(frames):
+        acc, _ = sc.path_trace(H.with_resolution(H.path_call(f)["uniforms"], W, Hh), acc)
+        if i in keep_acc:
+            accs[i] = acc.copy()
+        if i in keep_can:
+            ou = H.output_call(f)["uniforms"]
+            cans[i] = po.screen_output(acc, ou["uOneOverSampleCounter"][1][0],
+                                       ou.get("uToneMappingExposure", ["f", [0.0]])[1][0])
+    return accs, cans
+
+
+@pytest.mark.parametrize("case", ["dragon_1080p", "dragon_4k_whole", "sky_dragon_4k_from_frame1"])
+def test_bench_schedule_bitexact(monkeypatch, case):
+    """The draws exactly as bench.py's step loop issues them, at the bench's sizes and default knobs (no
+    PT_* environment: three frames in flight, no overlap lag, late-bounce compaction in the auto mode's
+    default, which is on from 2 MP traced), with no sync or read between frames except one mid-stream read:
+      dragon_1080p              - the headline: the dragon stand-in's 4 recorded 1920x1080 frames + 12 of
+                                  the render loop's still-camera frames;
+      dragon_4k_whole           - dragon_4k_1gpu: the same at 3840x2160 as ONE partition (the compacting
+                                  whole-frame 4K path), 4 recorded + 4 frames;
+      sky_dragon_4k_from_frame1 - converge_1024spp: sky + dragon stand-in at 3840x2160 from frame 1 (history
+                                  cleared), 3 recorded + 5 frames.
+    The accumulation read right after one mid-stream path-tracing draw (before its copy / output), the
+    canvas after one mid-stream output, and the last frame's accumulation and canvas equal the oracle's
+    bits; queue_stats shows that every draw launched pt_cont with three frames in flight, so the test
+    cannot pass on a serial fallback (js/PathTracingCommon.js:1304-1357,
+    js/GLTFModelPathTracing_FragmentShader.js:387-609)."""
+    import copy
+    import os
+    import babylon_pt as bp
+    for k in list(os.environ):
+        if k.startswith("PT_"):
+            monkeypatch.delenv(k)
+    if case == "sky_dragon_4k_from_frame1":
+        meta, W, Hh, extra, read_acc, read_can = H.sky_mesh_stream(), 3840, 2160, 5, 3, 5
+    else:
+        meta = copy.deepcopy(H.stream("gltf_bunny_1080p"))
+        W, Hh = (1920, 1080) if case == "dragon_1080p" else (3840, 2160)
+        extra, read_acc, read_can = (12, 9, 7) if case == "dragon_1080p" else (4, 4, 5)
+    mesh = _dragon()
+    e = bp.Engine(0)
+    try:
+        player = bp.StreamPlayer(e, meta, H.bluenoise(), H.texture_payloads(meta, mesh), W, Hh)
+        frames = meta["frames"] + [player.synth_frame(k) for k in range(extra)]
+        e.resize_canvas(W, Hh)
+        seen = []
+        for i, calls in enumerate(frames):
+            for call in calls:
+                player.play_call(call)
+                if call["shader"] == "pathTracingFragmentShader" and i == read_acc:
+                    seen.append(("acc after path tracing", i, player.textures["pathTracingRenderTarget"].read()))
+                if call["shader"] == "screenOutputFragmentShader" and i == read_can:
+                    seen.append(("canvas", i, e.read_canvas(W, Hh)))
+        e.sync()
+        last = len(frames) - 1
+        seen.append(("final acc", last, player.textures["pathTracingRenderTarget"].read()))
+        seen.append(("final canvas", last, e.read_canvas(W, Hh)))
+        qs = e.queue_stats()
+    finally:
+        e.dispose()
+    assert qs["late_bounce_compaction"] == "auto: default on", qs
+    assert qs["frames_in_flight"] == 3, qs
+    assert qs["compacting_draws"] == len(frames), qs
+    accs, cans = _oracle_at(meta, frames, W, Hh, mesh, {read_acc, last}, {read_can, last})
+    for what, i, got in seen:
+        want = cans[i] if "canvas" in what else accs[i]
+        assert got.shape == want.shape
+        assert _bits_equal(want, got), "%s %s, frame %d: %s" % (case, what, i, _diff_report(want, got))
 
 
 @pytest.mark.parametrize("layout", ["pairs", "trail"])

@@ -48,26 +48,25 @@ def test_stated_tolerance_holds(report):
 
 @pytest.mark.parametrize("name", ["cornell_256", "gltf_teapot", "hdri_helmet"])
 def test_first_frame_reproduces(name, report):
-    """The study's generator reproduces its committed first-frame numbers. Exactly with the toolchain
-    that generated them (tolerance.json "toolchain"): the fma / libm / gpu builds' bits depend on how
+    """The study's generator reproduces its committed first-frame numbers exactly, with the toolchain
+    that generated them (tolerance.json "toolchain"). The fma / libm / gpu builds' bits depend on how
     gcc fuses under -ffp-contract=fast and on the C library's transcendentals, so under another gcc or
-    libc they are compared within a tolerance, and without x86 FMA (-mfma) the case is skipped."""
+    libc (or without x86 FMA, -mfma) the committed numbers are not a prediction and the case is skipped
+    with the reason, rather than compared within a bound loose enough to pass a regression."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import tolerance
     tc = tolerance.toolchain()
     if tc["machine"] not in ("x86_64", "AMD64"):
         pytest.skip("the fma / libm / gpu oracle builds use x86 FMA (-mfma)")
-    same = tc == report.get("toolchain")
+    if tc != report.get("toolchain"):
+        pytest.skip("toolchain %r differs from the study's %r: its fma / libm / gpu builds round differently"
+                    % (tc, report.get("toolchain")))
     got = tolerance.run_case(name, 1, report["variants"])
     want = report["cases"][name]
     for v in report["variants"]:
         g, w = got["variants"][v], want["variants"][v]
-        if same:
-            assert g["bit_divergent_frac_frame1"] == w["bit_divergent_frac_frame1"], (name, v)
-            assert g["estimate"]["1"]["rmse"] == pytest.approx(w["estimate"]["1"]["rmse"], rel=1e-12), (name, v)
-        else:   # same built-in classes, another toolchain's rounding: same magnitudes
-            assert g["bit_divergent_frac_frame1"] == pytest.approx(w["bit_divergent_frac_frame1"], abs=0.1), (name, v, tc)
-            assert g["estimate"]["1"]["rmse"] <= 10.0 * max(w["estimate"]["1"]["rmse"], 1e-6), (name, v, tc)
+        assert g["bit_divergent_frac_frame1"] == w["bit_divergent_frac_frame1"], (name, v)
+        assert g["estimate"]["1"]["rmse"] == pytest.approx(w["estimate"]["1"]["rmse"], rel=1e-12), (name, v)
 
 
 def test_toolchain_recorded(report):

@@ -16,6 +16,8 @@
 #   wavetime:LIB:WLS           wave timeline + CU occupancy of a -DPT_SECPROF build (tools/wavetime.py)
 #   prof                       rocprofv3 --kernel-trace --stats of the exact command's workload (20 steps + 5 warmup)
 #   pmc[:W]                    the five PMC passes over tools/prof_frames.py (default workload dragon)
+#   ktrace:K                   rocprofv3 --kernel-trace --stats over the GPU tests matching -k K
+set -o pipefail   # a step's status is its GPU command's, not that of a `| tail` after it
 cd "$GRAFT_REPO_ROOT" || exit 1
 R=$GRAFT_REPO_ROOT
 TAG=$1; shift
@@ -49,9 +51,9 @@ for step in "$@"; do
             envs=""; [ "$cfg" != "-" ] && envs="${cfg//,/ }"
             wl=${w%@*}; sz=""; [ "$wl" != "$w" ] && sz="--size ${w#*@}"
             if [ $kind = envmx ]; then
-              res=$(env $envs timeout -k 10 120 python tools/exp_timing.py --workload "$wl" --frames 30 --backends megakernel --layouts pairs --no-mesh-variant 2>&1 | tail -1); rc=$?
+              res=$(set -o pipefail; env $envs timeout -k 10 120 python tools/exp_timing.py --workload "$wl" --frames 30 --backends megakernel --layouts pairs --no-mesh-variant 2>&1 | tail -1); rc=$?
             else
-              res=$(env $envs timeout -k 10 200 python3 bench.py --workload "$wl" $sz --no-pmc --cpu-budget 0 --no-check --no-anchors 2>&1 | tail -1); rc=$?
+              res=$(set -o pipefail; env $envs timeout -k 10 200 python3 bench.py --workload "$wl" $sz --no-pmc --cpu-budget 0 --no-check --no-anchors 2>&1 | tail -1); rc=$?
             fi
             echo "r$r [$cfg] $w $res" >> "$LOG"
             [ $rc -ne 0 ] && break 3
@@ -63,6 +65,10 @@ for step in "$@"; do
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$R/gpurun_out/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 --cpu-budget 0 --no-pmc --no-anchors) > "$LOG" 2>&1 ;;
+    ktrace)   # rocprofv3 --kernel-trace --stats over the GPU tests matching -k a1
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$R/gpurun_out/ktrace_$TAG" -o run -- python3 -m pytest "$R/tests" -m gpu -q -x -p no:cacheprovider \
+        --timeout 300 --timeout-method thread -k "$a1") > "$LOG" 2>&1 ;;
     pmc)
       W=${a1:-dragon}; OUT="$R/gpurun_out/pmc_$TAG"; mkdir -p "$OUT"; i=0; rc=0
       for C in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES" \

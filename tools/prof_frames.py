@@ -20,6 +20,8 @@ ap.add_argument("--frames", type=int, default=10)
 ap.add_argument("--width", type=int, default=0)
 ap.add_argument("--height", type=int, default=0)
 ap.add_argument("--dragon", action="store_true", help="the StanfordDragon stand-in mesh instead of the stream's")
+ap.add_argument("--parts", type=int, default=1, help="draw only rank --part's bands of a --parts-way row partition")
+ap.add_argument("--part", type=int, default=0)
 a = ap.parse_args()
 maps = None
 if a.workload:
@@ -35,6 +37,9 @@ if maps:
     for kind, sampler in H.PBR_SAMPLERS.items():
         p.textures[sampler] = bp.Texture(e, maps[kind], name=kind)
 e.resize_canvas(p.width, p.height)
+if a.parts > 1:   # one rank's share of an N-GPU frame, as bench.py's rank_share_4k draws it
+    e.set_row_partition(a.parts, a.part)
+    e.set_output_partition(True)
 for k in range(a.frames):
     for call in p.synth_frame(k):
         p.play_call(call)
