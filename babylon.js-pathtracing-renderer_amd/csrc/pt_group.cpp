@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <set>
 #include <string>
@@ -43,6 +44,11 @@ struct pt_ctx {
     std::vector<bool> has_draw, has_out;
     hipEvent_t ev_gather = nullptr;            // part 0: after the last canvas gather
     bool has_gather = false;
+    // peer access between every two distinct devices of the context: the halo pulls and the gather are
+    // strided 2D copies over xGMI. Without it (hipDeviceCanAccessPeer false, hipDeviceEnablePeerAccess
+    // failing, or PT_PEER=0) they go band by band through hipMemcpyPeerAsync, which the runtime stages
+    std::vector<int> devs;
+    bool peer = true;
     int cw = 0, ch = 0;
     std::string err;
     std::set<pt_texture*> textures;
@@ -99,11 +105,23 @@ bool is_trace(int prog)
 // Rows [b*16 + off, b*16 + off + nrows) of the bands b = b0, b0 + N, b0 + 2N, ... (count of them),
 // clipped to [0, H), from src to dst (same row layout, `rowbytes` per row): one strided 2D copy for
 // the bands whose rows all lie inside the image, single copies for the (at most two) clipped ones.
+//
+// Peer fallback (dst_dev >= 0): one hipMemcpyPeerAsync per band (its rows are contiguous), from src_dev.
 hipError_t copy_band_rows(char* dst, const char* src, size_t rowbytes, int N, int b0, int count, int off, int nrows,
-                          int H, hipMemcpyKind kind, hipStream_t s)
+                          int H, hipMemcpyKind kind, hipStream_t s, int dst_dev = -1, int src_dev = -1)
 {
     if (count <= 0) return hipSuccess;
     auto row0 = [&](int m) { return (long)(b0 + (long)m * N) * kBand + off; };
+    if (dst_dev >= 0) {
+        hipError_t e = hipSuccess;
+        for (int m = 0; m < count && e == hipSuccess; m++) {
+            const long r0 = std::max(0L, row0(m)), r1 = std::min((long)H, row0(m) + nrows);
+            if (r1 > r0)
+                e = hipMemcpyPeerAsync(dst + r0 * rowbytes, dst_dev, src + r0 * rowbytes, src_dev,
+                                       (size_t)(r1 - r0) * rowbytes, s);
+        }
+        return e;
+    }
     int lo = 0, hi = count - 1;
     while (lo <= hi && row0(lo) < 0) lo++;
     while (hi >= lo && row0(hi) + nrows > H) hi--;
@@ -158,10 +176,11 @@ int render_output_parts(pt_effect* fx, pt_texture* target)
             const size_t rb = (size_t)acc->w * 16;
             char* dst = (char*)dev_texture_device_ptr(acc->sub[j]);
             const int cnt = bands_of(nb, N, j);
+            const int dd = c->peer ? -1 : c->devs[j];
             GHIP(c, copy_band_rows(dst, (const char*)dev_texture_device_ptr(acc->sub[lo]), rb, N, j, cnt, -2, 2, acc->h,
-                                   hipMemcpyDefault, dev_stream(d)));
+                                   hipMemcpyDefault, dev_stream(d), dd, c->devs[lo]));
             GHIP(c, copy_band_rows(dst, (const char*)dev_texture_device_ptr(acc->sub[hi]), rb, N, j, cnt, kBand, 2, acc->h,
-                                   hipMemcpyDefault, dev_stream(d)));
+                                   hipMemcpyDefault, dev_stream(d), dd, c->devs[hi]));
         }
         if (int rc = take(c, j, dev_render(fx->sub[j], target ? target->sub[j] : nullptr))) return rc;
         if (int rc = record(c, j, c->ev_out[j])) return rc;
@@ -178,7 +197,7 @@ int render_output_parts(pt_effect* fx, pt_texture* target)
     for (int k = 1; k < N; k++) {
         if (int rc = wait(c, 0, c->ev_out[k], true)) return rc;
         GHIP(c, copy_band_rows(dst, (const char*)dev_canvas_ptr(c->parts[k]), (size_t)cw * 4, N, k, bands_of(nb, N, k), 0,
-                               kBand, ch, hipMemcpyDefault, dev_stream(d0)));
+                               kBand, ch, hipMemcpyDefault, dev_stream(d0), c->peer ? -1 : c->devs[0], c->devs[k]));
     }
     if (int rc = record(c, 0, c->ev_gather)) return rc;
     c->has_gather = true;
@@ -228,18 +247,21 @@ pt_ctx* pt_ctx_create_devices(const int* devices, int n, int* err)
             if (rc == PT_OK) rc = dev_set_output_partition(d, 1);
         }
     }
-    // peer access between the distinct devices of the context (halo pulls, the gather)
+    // peer access between the distinct devices of the context (halo pulls, the gather); where a pair has
+    // none, every copy of the context takes the per-band hipMemcpyPeerAsync path instead (pt_ctx::peer)
+    c->devs.assign(devices, devices + n);
+    if (const char* v = std::getenv("PT_PEER")) c->peer = std::atoi(v) != 0;
     std::vector<int> uniq(devices, devices + n);
     std::sort(uniq.begin(), uniq.end());
     uniq.erase(std::unique(uniq.begin(), uniq.end()), uniq.end());
-    for (size_t a = 0; a < uniq.size() && rc == PT_OK; a++)
-        for (size_t b = 0; b < uniq.size() && rc == PT_OK; b++) {
+    for (size_t a = 0; a < uniq.size() && rc == PT_OK && c->peer; a++)
+        for (size_t b = 0; b < uniq.size() && c->peer; b++) {
             if (a == b) continue;
             int can = 0;
-            if (hipDeviceCanAccessPeer(&can, uniq[a], uniq[b]) != hipSuccess || !can) { rc = PT_ERR_DEVICE; break; }
+            if (hipDeviceCanAccessPeer(&can, uniq[a], uniq[b]) != hipSuccess || !can) { c->peer = false; break; }
             hipSetDevice(uniq[a]);
             hipError_t e = hipDeviceEnablePeerAccess(uniq[b], 0);
-            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) rc = PT_ERR_DEVICE;
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) c->peer = false;
             (void)hipGetLastError();
         }
     for (int k = 0; k < (int)c->parts.size() && rc == PT_OK && n > 1; k++) {
@@ -271,6 +293,8 @@ pt_ctx* pt_ctx_create_mask(uint32_t device_mask, int* err)
 }
 
 int pt_ctx_parts(const pt_ctx* c) { return c ? c->n() : PT_ERR_ARG; }
+
+int pt_ctx_peer_copies(const pt_ctx* c) { return c ? (c->peer ? 1 : 0) : PT_ERR_ARG; }
 
 void pt_ctx_destroy(pt_ctx* c)
 {

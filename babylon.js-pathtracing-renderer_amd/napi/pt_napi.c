@@ -123,6 +123,8 @@ static napi_value CtxCreateMask(napi_env env, napi_callback_info info)
 }
 static napi_value CtxParts(napi_env env, napi_callback_info info)
 { napi_value a[MAXARGS]; if (args(env, info, a, 1) < 0) return NULL; return num(env, pt_ctx_parts((pt_ctx*)handle(env, a[0]))); }
+static napi_value CtxPeerCopies(napi_env env, napi_callback_info info)
+{ napi_value a[MAXARGS]; if (args(env, info, a, 1) < 0) return NULL; return num(env, pt_ctx_peer_copies((pt_ctx*)handle(env, a[0]))); }
 static napi_value CtxDestroy(napi_env env, napi_callback_info info)
 { napi_value a[MAXARGS]; if (args(env, info, a, 1) < 0) return NULL; pt_ctx_destroy((pt_ctx*)handle(env, a[0])); return nul(env); }
 static napi_value LastError(napi_env env, napi_callback_info info)
@@ -423,7 +425,7 @@ static napi_value Init(napi_env env, napi_value exports)
 {
     static const struct { const char* name; napi_callback fn; } F[] = {
         { "pt_ctx_create", CtxCreate }, { "pt_ctx_create_devices", CtxCreateDevices }, { "pt_ctx_create_mask", CtxCreateMask },
-        { "pt_ctx_parts", CtxParts }, { "pt_ctx_destroy", CtxDestroy }, { "pt_last_error", LastError },
+        { "pt_ctx_peer_copies", CtxPeerCopies }, { "pt_ctx_parts", CtxParts }, { "pt_ctx_destroy", CtxDestroy }, { "pt_last_error", LastError },
         { "pt_sync", Sync }, { "pt_canvas_resize", CanvasResize },
         { "pt_effect_create", EffectCreate }, { "pt_effect_create_program", EffectCreateProgram },
         { "pt_effect_destroy", EffectDestroy }, { "pt_effect_program", EffectProgram },

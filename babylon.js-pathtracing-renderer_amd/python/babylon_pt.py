@@ -33,7 +33,7 @@ NEAREST, BILINEAR, TRILINEAR = 1, 2, 3
 
 # every symbol include/pt.h declares (checked by tests/test_capi_symbols.py)
 SYMBOLS = [
-    "pt_ctx_create", "pt_ctx_create_mask", "pt_ctx_create_devices", "pt_ctx_parts", "pt_ctx_destroy", "pt_last_error", "pt_sync", "pt_canvas_resize",
+    "pt_ctx_create", "pt_ctx_create_mask", "pt_ctx_create_devices", "pt_ctx_parts", "pt_ctx_peer_copies", "pt_ctx_destroy", "pt_last_error", "pt_sync", "pt_canvas_resize",
     "pt_effect_create", "pt_effect_create_program", "pt_effect_destroy", "pt_effect_program",
     "pt_set_float", "pt_set_int", "pt_set_texture",
     "pt_texture_create_rgba32f", "pt_texture_create_rgba8", "pt_render_target_create", "pt_render_target_wrap",
@@ -58,7 +58,7 @@ def lib():
     cpp = ctypes.POINTER(ctypes.c_char_p)
     sig = {
         "pt_ctx_create": ([i32, ip], vp), "pt_ctx_create_mask": ([ctypes.c_uint32, ip], vp),
-        "pt_ctx_create_devices": ([ctypes.POINTER(ctypes.c_int), i32, ip], vp), "pt_ctx_parts": ([vp], i32),
+        "pt_ctx_create_devices": ([ctypes.POINTER(ctypes.c_int), i32, ip], vp), "pt_ctx_parts": ([vp], i32), "pt_ctx_peer_copies": ([vp], i32),
         "pt_ctx_destroy": ([vp], None), "pt_last_error": ([vp], ctypes.c_char_p),
         "pt_sync": ([vp], i32), "pt_canvas_resize": ([vp, i32, i32], i32),
         "pt_effect_create": ([vp, ctypes.c_char_p, cpp, i32, cpp, i32, ip], vp),
@@ -127,6 +127,7 @@ class Engine:
                                                              ERRORS.get(err.value, err.value)))
         self.device = device if devices is None else devices[0]
         self.parts = lib().pt_ctx_parts(self.ctx)
+        self.peer_copies = lib().pt_ctx_peer_copies(self.ctx) == 1
         self._objs = []
 
     def check(self, rc, what=""):

@@ -75,6 +75,11 @@ pt_ctx* pt_ctx_create_mask(uint32_t device_mask, int* err);
  * split, halo and gather path on a one-GPU host) */
 pt_ctx* pt_ctx_create_devices(const int* devices, int n, int* err);
 int pt_ctx_parts(const pt_ctx* ctx);
+/* 1 when the halo pulls and the canvas gather between the context's distinct devices run as strided 2D
+ * copies over peer access (xGMI), 0 when some pair has no peer access (hipDeviceCanAccessPeer false or
+ * hipDeviceEnablePeerAccess failing; PT_PEER=0 forces it): they then run band by band through
+ * hipMemcpyPeerAsync, same results. One-device contexts report 1. */
+int pt_ctx_peer_copies(const pt_ctx* ctx);
 void pt_ctx_destroy(pt_ctx* ctx);
 const char* pt_last_error(pt_ctx* ctx);
 int pt_sync(pt_ctx* ctx);

@@ -53,6 +53,27 @@ def test_multipart_context_bitexact(parts):
     _check(ref_acc, ref_can, *got)
 
 
+@pytest.mark.parametrize("parts,size", [(2, (320, 180)), (3, (203, 117))])
+def test_multipart_without_peer_access_bitexact(monkeypatch, parts, size):
+    """The route a node without peer access between its GPUs takes (hipDeviceCanAccessPeer false or
+    hipDeviceEnablePeerAccess failing: the context still opens, pt_group.cpp): halo pulls and the canvas
+    gather band by band through hipMemcpyPeerAsync, forced here by PT_PEER=0 - the reference's unchanged
+    render loop over it (js/GLTF_Model_Path_Tracing.js:1228-1235), accumulation and canvas bit-exact,
+    a partial last band and clipped halo rows included at 203x117."""
+    import babylon_pt as bp
+    monkeypatch.setenv("PT_PEER", "0")
+    meta = H.stream("gltf_teapot_320x180")
+    W, Hh = size
+    e = bp.Engine(devices=[0] * parts)
+    try:
+        assert e.parts == parts and e.peer_copies is False
+        got = _replay(e, meta, width=W, height=Hh)
+    finally:
+        e.dispose()
+    ref_acc, ref_can, _ = H.oracle_replay(meta, width=W, height=Hh, with_output=True)
+    _check(ref_acc, ref_can, *got)
+
+
 @pytest.mark.parametrize("parts", [2, 5])
 def test_multipart_odd_size_bitexact(parts):
     """203x117: a partial last band (5 rows), a halo row pair clipped at the top edge."""
