@@ -172,7 +172,8 @@ struct Dev {
     // and pt_cont's one-wave workgroups
     int cont_mode = 2;
     void* cont_mem = nullptr;
-    size_t cont_cap = 0;
+    size_t cont_cap = 0;          // records per buffer set ...
+    int cont_sets = 0;            // ... and buffer sets allocated
     unsigned cont_bounce = 2, cont_lanes = 48, cont_refill = 16, cont_waves = 2048;
     unsigned cont_walk = 0;   // (PT_CONT_WALK) pt_cont's schedule: 0 per wave-bounce, T > 0 per lane (TraceArgs::cont_walk)
     // auto mode: compaction pays on the heavy 4K frames (sky + dragon +19 %, dragon stand-in +10 %) and
@@ -529,20 +530,37 @@ int rad_reserve(Dev* c, size_t pixels)
     return PT_OK;
 }
 
-// pt_cont's records for frames of up to `paths` pixels, per buffer set: records [cap x 64 B] | pixels [cap x 4 B]
-// | counter; the counters start at zero here, afterwards each draw's pt_blend zeroes its own
-int cont_reserve(Dev* c, size_t paths)
+// the overlap lag of a draw that traces `traced` pixels (Dev::lag)
+int draw_lag(const Dev* c, size_t traced) { return c->lag >= 0 ? c->lag : traced < c->lag_pixels ? Dev::kLagSmall : 0; }
+
+// the pixels a draw of `target` traces: the owned 16-row bands of the partition (a bound on its records)
+size_t traced_pixels(const Dev* c, const DevTex* target)
 {
-    if (paths <= c->cont_cap) return PT_OK;
+    const int nb = (target->h + pt::kTile - 1) / pt::kTile;
+    const int own = c->part < nb ? (nb - c->part + c->num_parts - 1) / c->num_parts : 0;
+    return std::min((size_t)target->w * target->h, (size_t)own * pt::kTile * target->w);
+}
+
+// pt_cont's records for draws that trace up to `paths` pixels (a record per traced pixel at most), in `sets`
+// buffer sets: per set records [cap x 64 B] | pixels [cap x 4 B] | counter; the counters start at zero here,
+// afterwards each draw's pt_blend zeroes its own. (Sized by the partition's pixels and the sets its draws
+// cycle through, not the whole target times every set: a 4K frame's records are 0.53 GB per set.)
+int cont_reserve(Dev* c, size_t paths, int sets)
+{
+    if (paths <= c->cont_cap && sets <= c->cont_sets) return PT_OK;
+    paths = std::max(paths, c->cont_cap);
+    sets = std::max(sets, c->cont_sets);
     if (c->cont_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->cont_mem)); c->cont_mem = nullptr; }
     c->cont_cap = 0;
+    c->cont_sets = 0;
     const size_t per = paths * 64 + ((paths * 4 + 255) & ~(size_t)255) + 256;
-    HIPCHK(c, hipMalloc(&c->cont_mem, (size_t)c->sets() * per));
+    HIPCHK(c, hipMalloc(&c->cont_mem, (size_t)sets * per));
     // on the main stream (hipMemset would go to the null stream, which the non-blocking side streams do
     // not wait for: the next draw's atomics raced with it); the next draw's path tracing waits for a mark
     // recorded after it
-    HIPCHK(c, hipMemsetAsync(c->cont_mem, 0, (size_t)c->sets() * per, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->cont_mem, 0, (size_t)sets * per, c->stream));
     c->cont_cap = paths;
+    c->cont_sets = sets;
     c->need_fresh = true;
     return PT_OK;
 }
@@ -565,8 +583,10 @@ int cont_decide_(Dev* c, const DevTex* target, int prog, bool eligible, bool* on
     *on = false;
     *depth = c->depth;
     if (!eligible || c->cont_mode == 0) return PT_OK;
-    // the records first, so that no trial block pays for their allocation
-    if (int rc = cont_reserve(c, (size_t)target->w * target->h)) return rc;
+    // the records first, so that no trial block pays for their allocation (for every set the draws of this
+    // target cycle through: the depth, at most c->depth, plus the lag)
+    const size_t traced_approx = (size_t)target->w * target->h / (size_t)std::max(1, c->num_parts);   // (as render_trace's)
+    if (int rc = cont_reserve(c, traced_pixels(c, target), c->depth + draw_lag(c, traced_approx))) return rc;
     if (c->cont_mode == 1) { *on = true; return PT_OK; }
     auto& t = c->tune;
     if (t.target != target || t.prog != prog || t.part != c->part || t.parts != c->num_parts || t.w != target->w ||
@@ -930,7 +950,7 @@ int render_trace(DevFx* fx, DevTex* target)
     int depth = c->depth;
     if (int rc = cont_decide(c, target, fx->prog, mesh && !c->counting && !PT_SECPROF_BUILD, &cont, &depth)) return rc;
     const size_t traced = (size_t)target->w * target->h / (size_t)std::max(1, c->num_parts);   // (about)
-    const int lag = c->lag >= 0 ? c->lag : traced < c->lag_pixels ? Dev::kLagSmall : 0;
+    const int lag = draw_lag(c, traced);
     if (depth != c->depth_run || lag != c->lag_run) {   // another buffer-set cycle: the draw waits for everything before it
         c->depth_run = depth;
         c->lag_run = lag;
@@ -961,7 +981,10 @@ int render_trace(DevFx* fx, DevTex* target)
     }
     if (int rc = rad_reserve(c, (size_t)target->w * target->h)) return rc;
     a.rad = c->rad_mem + (size_t)par * c->rad_pixels;
-    if (cont) cont_args(c, par, a);
+    if (cont) {   // (records for this draw's set: allocated by cont_decide already, unless the lag changed)
+        if (int rc = cont_reserve(c, traced_pixels(c, target), (int)nsets)) return rc;
+        cont_args(c, par, a);
+    }
     if (lpt && c->lpt_cap < n) {
         if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
         HIPCHK(c, hipMalloc(&c->lpt_mem, (5 * n + 1) * Dev::kSetsMax * sizeof(unsigned)));   // cost | order | split
