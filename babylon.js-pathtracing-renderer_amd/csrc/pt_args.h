@@ -133,9 +133,6 @@ struct TraceArgs {
     unsigned* cont_aux;     // per record: the pixel (py * width + px) | the 2x2 edge flag << 31
     unsigned* cont_count;   // [0] records stored by this draw, [1] pt_cont's queue head (both zeroed by the draw's pt_blend)
     unsigned cont_bounce, cont_lanes, cont_refill;
-    // pt_cont's schedule: 0 = a wave steps its paths a whole bounce at a time (pt_cont); T > 0 = per lane at walk
-    // granularity (pt_cont_walk, child-pair walk only): the walk loop yields once at most T lanes still walk
-    unsigned cont_walk;
     Tex8 bluenoise;
     const float4* aabb;
     long long aabb_texels;

@@ -175,7 +175,6 @@ struct Dev {
     size_t cont_cap = 0;          // records per buffer set ...
     int cont_sets = 0;            // ... and buffer sets allocated
     unsigned cont_bounce = 2, cont_lanes = 48, cont_refill = 16, cont_waves = 2048;
-    unsigned cont_walk = 0;   // (PT_CONT_WALK) pt_cont's schedule: 0 per wave-bounce, T > 0 per lane (TraceArgs::cont_walk)
     // auto mode: compaction pays on the heavy 4K frames (sky + dragon +19 %, dragon stand-in +10 %) and
     // costs elsewhere (bunny 4K -22 %, helmet -9 %, rank-sized frames -29 %: profiles/r05i_*), which
     // the draw's arguments do not tell apart. So the draws of one target / program / partition time it:
@@ -574,7 +573,6 @@ void cont_args(Dev* c, int p, pt::TraceArgs& a)
     a.cont_bounce = std::max(2u, c->cont_bounce);   // the G-buffer's normal / colour / id are final from bounce 2
     a.cont_lanes = c->cont_lanes;
     a.cont_refill = c->cont_refill;
-    a.cont_walk = c->cont_walk;
 }
 
 // auto mode of late-bounce compaction (Dev::ContTune): whether this draw compacts
@@ -1232,7 +1230,6 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_CONT_BOUNCE")) c->cont_bounce = (unsigned)std::max(2, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_LANES")) c->cont_lanes = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_REFILL")) c->cont_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
-    if (const char* v = std::getenv("PT_CONT_WALK")) c->cont_walk = (unsigned)std::min(64, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_WAVES")) c->cont_waves = (unsigned)std::max(1, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_AUTO_PIXELS")) c->cont_auto_pixels = (size_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_SPLIT_NEAR")) c->split_near = std::max(1, std::min(128, std::atoi(v)));

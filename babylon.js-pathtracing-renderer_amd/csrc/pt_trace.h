@@ -537,170 +537,6 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_cont(TraceArg
     }
 }
 
-// ------------------------------------------------------------------------------ pt_cont at walk granularity
-// The child-pair walk's loop body (bvhWalkPairs, pt_device.h: the same operations in the same order) as one
-// step of a per-lane state machine, so that a lane can leave the walk loop and come back to it.
-struct PairWalk {
-    uint32_t code;
-    int sp, pop;
-    float hT, tID, tU, tV;
-};
-template <class Stk>
-PT_D bool pairWalkStep(const TraceArgs& a, const PairBufs& b, f3 O, f3 D, f3 inv, bool dbl, bool fast, Stk& st,
-                       PairWalk& w, bool anyHit)
-{
-    int pop = w.pop;
-    asm volatile("" : "+v"(pop));
-    const int sp2 = w.sp - pop;
-    if (sp2 < 0) return false;   // the stack is empty: the walk is over
-    w.sp = sp2;
-    const float2 e = stackPop(st, pop ? sp2 : 0, make_float2(kINF, 0.0f));
-    const bool live = !pop || e.x < w.hT;
-    w.code = pop ? __float_as_uint(e.y) : w.code;
-    w.pop = 1;
-    if (!live) return true;
-    const uint32_t off = w.code & ~kLeafBit;
-    const float4 r0 = ldRec4(b.rec, off), r1 = ldRec4(b.rec, off + 16u), r2 = ldRec4(b.rec, off + 32u);
-    const float2 r3 = ldRec2(b.rec, off + 48u);
-    if (!(w.code & kLeafBit)) {
-        float tA, tB;
-        pairBoxes(r0, r1, r2, O, inv, fast, tA, tB);
-        const bool sw = tB < tA;
-        const float tN = sw ? tB : tA, tF = sw ? tA : tB;
-        const bool hitN = tN < w.hT, hitF = tF < w.hT;
-        const float cN = sw ? r3.y : r3.x, cF = sw ? r3.x : r3.y;
-        if (hitN && hitF) {
-            unsigned ovf = 0;
-            stackPush(a, st, w.sp, make_float2(tF, cF), ovf);
-            w.sp++;
-        }
-        w.code = __float_as_uint(hitN ? cN : hitF ? cF : __uint_as_float(w.code));
-        w.pop = (hitN || hitF) ? 0 : 1;
-    } else {
-        float tu, tv;
-        const float d = bvhTriangleE(mk(r0.x, r0.y, r0.z), mk(r0.w, r1.x, r1.y), mk(r1.z, r1.w, r2.x), O, D, tu, tv, dbl);
-        if (d < w.hT) {
-            w.hT = d; w.tID = 8.0f * r2.y; w.tU = tu; w.tV = tv;
-            if (anyHit) w.sp = 0;
-        }
-        asm volatile("" ::"v"(r3.x));
-    }
-    return true;
-}
-
-// pt_cont with the paths stepped per lane instead of per wave-bounce (cont_walk = T > 0; child-pair walk). A
-// lane is in one of four phases: no path, a segment to begin (SceneIntersect up to the walk: the analytic
-// objects, the model-space ray, the root box), walking, or walk done (the hit's attributes and the shading
-// step; then the next segment, or the pixel's radiance and no path). Each iteration refills the lanes without
-// a path from the queue (as pt_cont), begins their segments and those of the lanes that continue, then walks
-// - until at most T lanes are still walking while others wait (a walk that ended, or room for a refill) -
-// and shades the lanes whose walk ended. A lane's walk state (stack in its LDS / slab slot, registers) waits
-// across the iterations, so no lane waits for the wave's longest walk of a bounce. The path's state between
-// two segments stays in its record (contStore / contLoad): the walk loop holds only the walk's registers.
-// Every lane runs exactly its path's operations: the bits are the uncompacted kernel's.
-template <int PROG>
-__global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_cont_walk(TraceArgs a)
-{
-    static_assert(kPairs<PROG> && !kTrail<PROG> && kHasMesh<PROG>, "the child-pair stack walk");
-    __shared__ float2 lds_stack[kWalkSlotsOf<PROG> * kTraceBlock];
-    const unsigned lane = threadIdx.x;
-    const unsigned n = a.cont_count[0];
-    unsigned* const head = a.cont_count + 1;
-    bool more = true;
-    const unsigned deep = blockIdx.x * kTraceBlock + lane;
-    const unsigned long long below = (1ull << lane) - 1ull;
-    MegaStack<kTraceBlock, kStackLdsOf<PROG>, kScratchOf<PROG>> st{ (lds_float2*)lds_stack, lane, (glb_float2*)a.spill,
-                                                                    deep, a.spill_stride };
-    const PairBufs b = pairBufs(a);
-    const bool dbl = (!a.uses_albedo && a.model_mat == TRANSPARENT);
-    const bool lastOk = !kHasTex<PROG> && !a.uses_albedo &&
-                        (a.model_mat == DIFFUSE || a.model_mat == METAL || a.model_mat == TRANSPARENT);
-    const unsigned T = a.cont_walk;
-    Cnt cnt = { 0, 0, 0, 0, 0, 0, 0 };
-    Path p;
-    p.bn = 0u;
-    PState s;
-    Hit h;
-    f3 sn = mk(0, 0, 0), O = mk(0, 0, 0), D = mk(0, 0, 0), inv = mk(0, 0, 0);
-    PairWalk w = { 0u, 0, 1, 0.0f, -1.0f, 0.0f, 0.0f };
-    bool fast = false, anyHit = false;
-    unsigned slot = 0;
-    // NEW: a record just taken (its ray still in memory); NEXT: the lane's path continues (ray in registers)
-    enum { NONE = 0, NEW = 1, NEXT = 2, WALK = 3, SHADE = 4 };
-    int phase = NONE;
-    for (;;) {
-        const unsigned long long dead = __ballot(phase == NONE);
-        const unsigned ndead = (unsigned)__popcll(dead);
-        if (more && (ndead >= a.cont_refill || ndead == 64u)) {   // (wave-uniform: every lane is here)
-            unsigned base = 0;
-            if (lane == 0) base = atomicAdd(head, ndead);
-            base = __shfl(base, 0, 64);
-            if (base + ndead >= n) more = false;
-            if (phase == NONE) {
-                const unsigned q = base + (unsigned)__popcll(dead & below);
-                if (q < n) {
-                    slot = q;
-                    phase = NEW;
-                }
-            }
-        }
-        if (phase == NEW) {   // the ray and the flags of the record
-            const float4* r = a.cont_rec + 4ull * slot;
-            const float4 r0 = r[0], r1 = r[1];
-            const unsigned bits = __float_as_uint(r[3].y);
-            p.ro = mk(r0.x, r0.y, r0.z); p.rd = mk(r0.w, r1.x, r1.y);
-            s.bounce = (int)((bits >> 16) & 0xffu); s.sampleLight = (bits >> 26) & 1u;
-            phase = NEXT;
-        }
-        if (phase == NEXT) {   // SceneIntersect up to the walk (pt_trace.h sceneIntersect, bounceStep)
-            analyticNearest<PROG>(a, p.ro, p.rd, h, sn);
-            O = mul(a.model, p.ro, 1.0f);
-            D = mul(a.model, p.rd, 0.0f);
-            inv = mk(grcp(D.x), grcp(D.y), grcp(D.z));
-            fast = pairWalkFast(O, inv);
-            anyHit = s.sampleLight || (s.bounce == 5 && lastOk);
-            const float* rb = a.bvh_root_box;
-            const float rootT = box(mk(rb[0], rb[1], rb[2]), mk(rb[3], rb[4], rb[5]), O, inv);
-            w.code = a.bvh_root_code; w.hT = h.t; w.sp = 0; w.pop = rootT < h.t ? 0 : 1;
-            w.tID = -1.0f; w.tU = 0.0f; w.tV = 0.0f;
-            phase = WALK;
-        }
-        const unsigned long long alive = __ballot(phase != NONE);
-        if (alive == 0ull) {
-            if (!more) break;
-            continue;
-        }
-        const unsigned nalive = (unsigned)__popcll(alive);
-        const bool room = more && 64u - nalive >= a.cont_refill;
-        for (;;) {
-            const unsigned nw = (unsigned)__popcll(__ballot(phase == WALK));
-            if (nw == 0u || (nw <= T && (nw < nalive || room))) break;
-            if (phase == WALK && !pairWalkStep(a, b, O, D, inv, dbl, fast, st, w, anyHit)) phase = SHADE;
-        }
-        if (phase == SHADE) {   // the rest of SceneIntersect and the shading step
-            contLoad(a, slot, p, s);
-            GBits g{ &p.bn };
-            h.t = w.hT;
-            if (w.tID >= 0.0f && anyHit) {   // the mesh occludes: what shadeStep reads of a mesh hit, no lookup
-                h.normal = mk(0.0f, 0.0f, 1.0f);
-                h.type = a.uses_albedo ? PBR_MATERIAL : a.model_mat;
-                h.color = mk(1.0f, 1.0f, 1.0f);
-                h.id = meshObjectId<PROG>(a);
-            } else if (w.tID >= 0.0f) meshHit<PROG, false>(a, w.tID, w.tU, w.tV, h, cnt);
-            else analyticAttributes<PROG>(a, h, sn);
-            f3 accum = mk(0, 0, 0);   // (CalculateRadiance assigns it only where the path ends)
-            if (shadeStep<PROG, false, GBits>(a, p, s, g, accum, h, cnt)) {
-                contStore(a, slot, p, s);
-                phase = NEXT;
-            } else {
-                const unsigned aux = a.cont_aux[slot];
-                radianceOut(a, (long long)(aux & 0x7fffffffu), max3s(accum, 0.0f), g.sharp(), (aux >> 31) != 0u);
-                phase = NONE;
-            }
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------ persistent paths
 // pt_persist<PROG,COUNT>: the same per-pixel program with path regeneration. A wave owns a list
 // of `per_wave` 8x8 wave tiles (the static kernel's lane order) and keeps its 64 lanes busy: when

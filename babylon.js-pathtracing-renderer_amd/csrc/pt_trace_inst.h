@@ -22,11 +22,6 @@ template <int P>
 hipError_t launchCont(const TraceArgs* a, dim3 grid, hipStream_t s)
 {
     if constexpr (kHasMesh<P>) {
-        if constexpr (kPairs<P> && !kTrail<P>)
-            if (a->cont_walk) {
-                hipLaunchKernelGGL((pt_cont_walk<P>), grid, dim3(kTraceBlock), 0, s, *a);
-                return hipGetLastError();
-            }
         hipLaunchKernelGGL((pt_cont<P>), grid, dim3(kTraceBlock), 0, s, *a);
         return hipGetLastError();
     }

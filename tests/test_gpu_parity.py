@@ -328,17 +328,14 @@ def test_overlapped_frames_observed_between_draws(engine, size):
         assert _bits_equal(want, got), "%s, frame %d: %s" % (what, i, _diff_report(want, got))
 
 
-@pytest.mark.parametrize("layout,walk", [("pairs", "0"), ("trail", "0"), ("pairs", "1"), ("pairs", "24"), ("pairs", "64")])
-def test_late_bounce_compaction_1080p_bitexact(monkeypatch, layout, walk):
+@pytest.mark.parametrize("layout", ["pairs", "trail"])
+def test_late_bounce_compaction_1080p_bitexact(monkeypatch, layout):
     """Late-bounce compaction forced on (PT_CONT=1, from bounce 2 for waves with <= 48 live paths, the
     default PT_CONT_LANES: the
     pt_trace<P,false,true> variant stores them, pt_cont runs them packed on the draw's side stream):
-    the dragon stand-in's four recorded 1920x1080 frames, accumulation and canvas bit-exact - with pt_cont
-    stepping its paths per wave-bounce and, on the child-pair walk, per lane (pt_cont_walk, yielding the walk
-    loop at 1, 24 or 64 walking lanes)."""
+    the dragon stand-in's four recorded 1920x1080 frames, accumulation and canvas bit-exact."""
     import babylon_pt as bp
     monkeypatch.setenv("PT_CONT", "1")
-    monkeypatch.setenv("PT_CONT_WALK", walk)   # pt_cont's schedule: per wave-bounce (0), per lane (pt_cont_walk)
     e = bp.Engine(0)
     try:
         e.set_bvh_layout(layout)

@@ -29,12 +29,15 @@ def main():
     W, Hh = (int(v) for v in args.size.lower().split("x"))
     engine = bp.Engine(0)
     try:
-        v, ms, rows = bench.rank_share_run(engine, args.workload, W, Hh, args.world, args.rank, args.warmup, args.steps)
+        v, ms, rows, _, _, lat = bench.rank_share_run(engine, args.workload, W, Hh, args.world, args.rank, args.warmup,
+                                                      args.steps)
         q = engine.queue_stats()
+        bench.end_partition(engine)
         print(json.dumps({"workload": args.workload, "size": [W, Hh], "world": args.world, "rank": args.rank,
                           "rows": rows, "mpaths_per_s": round(v, 2), "ms_per_frame": round(ms, 4),
                           "late_bounce_compaction": q["late_bounce_compaction"],
-                          "frames_in_flight": q["frames_in_flight"], "env": {k: v for k, v in os.environ.items()
+                          "frames_in_flight": q["frames_in_flight"],
+                          "frame_latency_ms": bench.latency_summary(lat, ms), "env": {k: v for k, v in os.environ.items()
                                                                              if k.startswith("PT_")}}))
     finally:
         engine.dispose()
