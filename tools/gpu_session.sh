@@ -11,11 +11,13 @@
 #   bench:W[:ARGS]             bench.py --workload W (ARGS: extra bench flags, commas for spaces)
 #   envmx:ROUNDS:WLS:ENVS      path-tracing kernel ms per workload under environment settings, alternating
 #                              rounds (WLS comma-separated; ENVS '|'-separated, each space-free K=V[,K=V] or -)
+#   fshort:ROUNDS:WLS:ENVS     frames with the driver's short run (--steps 20 --warmup 5)
 #   frames:ROUNDS:WLS:ENVS     the same for whole frames (bench.py --no-pmc --cpu-budget 0 per setting);
 #                              a workload W@WxH runs at that frame size
 #   wavetime:LIB:WLS           wave timeline + CU occupancy of a -DPT_SECPROF build (tools/wavetime.py)
 #   prof                       rocprofv3 --kernel-trace --stats of the exact command's workload (20 steps + 5 warmup)
 #   pmc[:W]                    the five PMC passes over tools/prof_frames.py (default workload dragon)
+#   rankpx:ROUNDS:WORLD:ENVS   tools/rank_proxy.py (rank 0's share of the 4K dragon frame at N = WORLD) per setting
 #   ktrace:K                   rocprofv3 --kernel-trace --stats over the GPU tests matching -k K
 set -o pipefail   # a step's status is its GPU command's, not that of a `| tail` after it
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -42,7 +44,7 @@ for step in "$@"; do
       else run 900 "$LOG" env $envs python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread; fi ;;
     exact) run 300 "$LOG" python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     bench) run 400 "$LOG" python3 bench.py --workload "$a1" ${a2//,/ } ;;
-    envmx|frames)
+    envmx|frames|fshort)
       : > "$LOG"; rc=0
       for r in $(seq "$a1"); do
         IFS='|' read -ra ENVS <<< "$a3"
@@ -53,11 +55,24 @@ for step in "$@"; do
             if [ $kind = envmx ]; then
               res=$(set -o pipefail; env $envs timeout -k 10 120 python tools/exp_timing.py --workload "$wl" --frames 30 --backends megakernel --layouts pairs --no-mesh-variant 2>&1 | tail -1); rc=$?
             else
-              res=$(set -o pipefail; env $envs timeout -k 10 200 python3 bench.py --workload "$wl" $sz --no-pmc --cpu-budget 0 --no-check --no-anchors 2>&1 | tail -1); rc=$?
+              short=""; [ $kind = fshort ] && short="--steps 20 --warmup 5"
+              res=$(set -o pipefail; env $envs timeout -k 10 200 python3 bench.py --workload "$wl" $sz $short --no-pmc --cpu-budget 0 --no-check --no-anchors 2>&1 | tail -1); rc=$?
             fi
             echo "r$r [$cfg] $w $res" >> "$LOG"
             [ $rc -ne 0 ] && break 3
           done
+        done
+      done
+      (exit $rc) ;;
+    rankpx)   # rankpx:ROUNDS:WORLD:ENVS - tools/rank_proxy.py (rank 0's share of the 4K dragon frame) per setting
+      : > "$LOG"; rc=0
+      for r in $(seq "$a1"); do
+        IFS='|' read -ra ENVS <<< "$a3"
+        for cfg in "${ENVS[@]}"; do
+          envs=""; [ "$cfg" != "-" ] && envs="${cfg//,/ }"
+          res=$(set -o pipefail; env $envs timeout -k 10 200 python3 tools/rank_proxy.py --world "$a2" 2>&1 | tail -1); rc=$?
+          echo "r$r [$cfg] n$a2 $res" >> "$LOG"
+          [ $rc -ne 0 ] && break 2
         done
       done
       (exit $rc) ;;
