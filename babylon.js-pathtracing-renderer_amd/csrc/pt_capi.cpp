@@ -208,6 +208,7 @@ struct Dev {
     // path-tracing draw, reused when the next draw has the same grid, target and program
     bool lpt = true;
     bool lpt_zig = false;     // PT_LPT=2: the order taken from both ends alternately (TraceArgs::order_zig)
+    bool xcd_blocked = false; // (experiment, PT_XCD_BLOCKED) without an order: a contiguous eighth of the tiles per XCD
     unsigned prio_tiles = 0;   // longest-first: the first prio_tiles 16x16 tiles run at raised wave priority
     unsigned split_tiles = 32; // longest-first: at most this many of the slowest tiles shaded by 16-lane waves
                                // (pt_trace, pt_order_build; PT_SPLIT_TILES)
@@ -1021,6 +1022,7 @@ int render_trace(DevFx* fx, DevTex* target)
         a.split = (a.order && split) ? c->lpt_split(par) : nullptr;
     }
     a.ntiles = (unsigned)n;
+    if (!a.order && c->xcd_blocked) a.order_zig = 2u;
     if (int rc = begin_draw(c, fx->prog, ts)) return rc;
     HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, ts));
     if (cont) {   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
@@ -1213,6 +1215,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_PERSIST_TILES")) c->persist_tiles = (unsigned)std::max(1, std::atoi(v));
     if (const char* v = std::getenv("PT_DRAW_EVENTS")) c->draw_events = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_LPT")) { c->lpt = std::atoi(v) != 0; c->lpt_zig = std::atoi(v) == 2; }
+    if (const char* v = std::getenv("PT_XCD_BLOCKED")) c->xcd_blocked = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_PRIO_TILES")) c->prio_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;

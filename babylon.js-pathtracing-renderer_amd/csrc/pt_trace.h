@@ -338,11 +338,14 @@ PT_D bool tracePlace(const TraceArgs& a, int lane, TracePlace& pl)
         wave = (int)(r / T);
     }
     unsigned rank = slot;   // the slot's place in the longest-first order
-    if (a.order_zig && slot >= K) {   // runs of 8 (one tile per XCD): from the top and the bottom in turn
+    if (a.order_zig == 1u && slot >= K) {   // runs of 8 (one tile per XCD): from the top and the bottom in turn
         const unsigned j = slot - K, m = ntiles - K, g = j >> 3, t = (g >> 1) * 8u + (j & 7u);
         rank = K + ((g & 1u) ? m - 1u - t : t);
     }
-    const unsigned tile = a.order ? a.order[rank] : slot;
+    // (experiment, PT_XCD_BLOCKED with PT_LPT=0: XCD j = slot % 8 takes the j-th eighth of the frame's tiles in
+    // row-major order - each L2 sees one contiguous strip of the frame, whatever its cost)
+    const unsigned tile = a.order ? a.order[rank]
+                                  : (a.order_zig == 2u && (ntiles & 7u) == 0u) ? (slot & 7u) * (ntiles >> 3) + (slot >> 3) : slot;
     if (rank < a.prio_tiles) __builtin_amdgcn_s_setprio(3);   // the critical path: issue first
     const int tx = (int)(tile % tiles_x);
     const unsigned bY = tile / tiles_x;
