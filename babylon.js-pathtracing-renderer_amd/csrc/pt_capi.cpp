@@ -213,6 +213,7 @@ struct Dev {
     unsigned split_tiles = 32; // longest-first: at most this many of the slowest tiles shaded by 16-lane waves
                                // (pt_trace, pt_order_build; PT_SPLIT_TILES)
     int split_near = 3;             // ... those within this many cost buckets of the slowest (1/8 octave each; PT_SPLIT_NEAR)
+    int lpt_flat = -1;              // (PT_LPT_FLAT) buckets more than this below the slowest dealt as one (orderBuild)
     unsigned split_dominance = 8;   // ... when the slowest wave costs this many times the mean (PT_SPLIT_ALWAYS=1: 0)
     // the order build of the last megakernel draw, deferred to run as an extra block of the next
     // screenOutput pass (pt_output) instead of a kernel of its own; any other draw, stream switch or
@@ -1043,7 +1044,8 @@ int render_trace(DevFx* fx, DevTex* target)
     HIPCHK(c, pt_launch_blend(&b, gy, c->stream, n <= pt::kOrderHeld * 64u ? c->main_waves : 0));
     if (a.cost) {   // this draw's costs order draw k + 2: the build rides along with the next screenOutput
         c->pending_order = { true, (unsigned)n, a.cost, c->lpt_order(par), c->lpt_split(par),
-                             (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance, c->split_near };
+                             (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance,
+                             c->split_near | ((c->lpt_flat + 1) << 8) };
         if (!c->fuse_order) { if (int rc = flush_order(c)) return rc; }
         c->lpt_key[par] = { true, n, target, fx->prog, c->part, c->num_parts };
     }
@@ -1235,6 +1237,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_CONT_REFILL")) c->cont_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_WAVES")) c->cont_waves = (unsigned)std::max(1, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_AUTO_PIXELS")) c->cont_auto_pixels = (size_t)std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("PT_LPT_FLAT")) c->lpt_flat = std::max(-1, std::min(127, std::atoi(v)));
     if (const char* v = std::getenv("PT_SPLIT_NEAR")) c->split_near = std::max(1, std::min(128, std::atoi(v)));
     if (const char* v = std::getenv("PT_SPLIT_ALWAYS")) c->split_dominance = std::atoi(v) ? 0u : 8u;
     if (const char* v = std::getenv("PT_BVH_LAYOUT"))   // reference | pairs | trail: the context's initial walk

@@ -50,12 +50,18 @@ PT_D int costBucket(unsigned dur)
 // bucket by bucket, slowest bucket first; within a bucket the order is whatever the LDS atomics
 // give - any permutation renders the same bits, only the schedule changes.
 // (one block of 1024 threads as its own kernel, or of 256 as the extra block of pt_output)
+// near_arg: near_buckets (bits 0-7) | (flat + 1) << 8 (bits 8-15, 0 = no flattening): with flat >= 0, every
+// bucket more than `flat` below the slowest tile's is dealt as one bucket, in (about) row-major order - the
+// slowest tiles still start first, the bulk of the frame sweeps down the screen, so the tiles in flight at
+// once lie in one band (their BVH working set shared in each XCD's L2)
 PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split, unsigned split_cap,
-                     unsigned dominance, int near_buckets)
+                     unsigned dominance, int near_arg)
 {
     __shared__ unsigned cnt[kCostBuckets];
     __shared__ unsigned long long total;
     __shared__ unsigned slowest;
+    __shared__ unsigned floorB;
+    const int near_buckets = near_arg & 255, flat = (near_arg >> 8) - 1;
     for (int b = threadIdx.x; b < kCostBuckets; b += blockDim.x) cnt[b] = 0;
     if (threadIdx.x == 0) { total = 0; slowest = 0; }
     __syncthreads();
@@ -124,35 +130,44 @@ PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, uns
         }
         unsigned near = (2 * l <= top && 2 * l > top - near_buckets ? c0 : 0u) +
                         (2 * l + 1 <= top && 2 * l + 1 > top - near_buckets ? c1 : 0u);
-        unsigned suf = c0 + c1;   // inclusive suffix sum over lanes l..63 (descending bucket order)
-        for (int o = 1; o < 64; o <<= 1) {
-            near += (unsigned)__shfl_xor((int)near, o, 64);
-            const unsigned t = (unsigned)__shfl_down((int)suf, o, 64);
-            if (l + o < 64) suf += t;
-        }
+        for (int o = 1; o < 64; o <<= 1) near += (unsigned)__shfl_xor((int)near, o, 64);
         if (l == 0) {
             const unsigned k = (near + 7u) & ~7u;   // split_cap: a multiple of 8, <= ntiles
             const bool dominated = (unsigned long long)slowest * 4ull * ntiles >= dominance * total && total > 0;
             *split = dominated ? min(k, split_cap) : 0u;
         }
-        const unsigned excl = suf - c0 - c1;   // tiles in buckets above 2l + 1
+        // flattening: the buckets below fl dealt as bucket fl (their counts folded into it)
+        const int fl = flat >= 0 ? max(0, top - flat) : 0;
+        unsigned below = (2 * l < fl ? c0 : 0u) + (2 * l + 1 < fl ? c1 : 0u);
+        for (int o = 32; o > 0; o >>= 1) below += (unsigned)__shfl_xor((int)below, o, 64);
+        unsigned f0 = 2 * l < fl ? 0u : c0, f1 = 2 * l + 1 < fl ? 0u : c1;
+        if (2 * l == fl) f0 += below;
+        if (2 * l + 1 == fl) f1 += below;
+        unsigned suf = f0 + f1;   // inclusive suffix sum over lanes l..63 (descending bucket order)
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned t = (unsigned)__shfl_down((int)suf, o, 64);
+            if (l + o < 64) suf += t;
+        }
+        const unsigned excl = suf - f0 - f1;   // tiles in buckets above 2l + 1
         cnt[2 * l + 1] = excl;
-        cnt[2 * l] = excl + c1;
+        cnt[2 * l] = excl + f1;
+        if (l == 0) floorB = (unsigned)fl;
     }
     __syncthreads();
+    const unsigned fb = floorB;
     if (held) {
 #pragma unroll
         for (int j = 0; j < (int)kOrderHeld; j++) {
             const unsigned t = threadIdx.x + j * blockDim.x;
             if (t < ntiles) {
-                const unsigned pos = atomicAdd(&cnt[(bk[j >> 2] >> (8 * (j & 3))) & 255u], 1u);
+                const unsigned pos = atomicAdd(&cnt[max((bk[j >> 2] >> (8 * (j & 3))) & 255u, fb)], 1u);
                 if (pos < ntiles) order[pos] = t;
             }
         }
         return;
     }
     for (unsigned t = threadIdx.x; t < ntiles; t += blockDim.x) {
-        const unsigned pos = atomicAdd(&cnt[tileBucket(t)], 1u);
+        const unsigned pos = atomicAdd(&cnt[max((unsigned)tileBucket(t), fb)], 1u);
         if (pos < ntiles) order[pos] = t;
     }
 }
