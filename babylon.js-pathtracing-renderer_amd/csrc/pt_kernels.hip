@@ -131,13 +131,14 @@ PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, uns
         unsigned near = (2 * l <= top && 2 * l > top - near_buckets ? c0 : 0u) +
                         (2 * l + 1 <= top && 2 * l + 1 > top - near_buckets ? c1 : 0u);
         for (int o = 1; o < 64; o <<= 1) near += (unsigned)__shfl_xor((int)near, o, 64);
+        const bool dominated = (unsigned long long)slowest * 4ull * ntiles >= dominance * total && total > 0;
         if (l == 0) {
             const unsigned k = (near + 7u) & ~7u;   // split_cap: a multiple of 8, <= ntiles
-            const bool dominated = (unsigned long long)slowest * 4ull * ntiles >= dominance * total && total > 0;
             *split = dominated ? min(k, split_cap) : 0u;
         }
-        // flattening: the buckets below fl dealt as bucket fl (their counts folded into it)
-        const int fl = flat >= 0 ? max(0, top - flat) : 0;
+        // flattening: the buckets below fl dealt as bucket fl (their counts folded into it) - not where a
+        // few tiles dominate (the helmet: there the whole order matters, flattened it lost 1.4 %)
+        const int fl = flat >= 0 && !dominated ? max(0, top - flat) : 0;
         unsigned below = (2 * l < fl ? c0 : 0u) + (2 * l + 1 < fl ? c1 : 0u);
         for (int o = 32; o > 0; o >>= 1) below += (unsigned)__shfl_xor((int)below, o, 64);
         unsigned f0 = 2 * l < fl ? 0u : c0, f1 = 2 * l + 1 < fl ? 0u : c1;
