@@ -213,7 +213,11 @@ struct Dev {
     unsigned split_tiles = 32; // longest-first: at most this many of the slowest tiles shaded by 16-lane waves
                                // (pt_trace, pt_order_build; PT_SPLIT_TILES)
     int split_near = 3;             // ... those within this many cost buckets of the slowest (1/8 octave each; PT_SPLIT_NEAR)
-    int lpt_flat = -1;              // (PT_LPT_FLAT) buckets more than this below the slowest dealt as one (orderBuild)
+    // (PT_LPT_FLAT, -1 = off) frames of more than 8192 tiles: the tiles more than this many buckets (1/8 octave
+    // each) below the slowest are dealt as one bucket, in about row-major order, so that the tiles in flight lie
+    // in one band of the frame (orderBuild). 6: dragon stand-in 4K +1.6-2.2 %, helmet 4K +8 %, sky + dragon 4K
+    // +0.9 %, bunny 4K ±0 (profiles/r06g_frames_lpt_flat_4k.log); 1080p frames keep the whole order
+    int lpt_flat = 6;
     unsigned split_dominance = 8;   // ... when the slowest wave costs this many times the mean (PT_SPLIT_ALWAYS=1: 0)
     // the order build of the last megakernel draw, deferred to run as an extra block of the next
     // screenOutput pass (pt_output) instead of a kernel of its own; any other draw, stream switch or
