@@ -161,14 +161,6 @@ struct Dev {
     size_t lag_pixels = 800000;   // (PT_OVERLAP_LAG_PIXELS)
     hipStream_t ts[kDepthMax] = {};
     hipEvent_t ev_mark[kSetsMax] = {}, ev_traced[kDepthMax] = {};
-    // (PT_STAGGER) a draw that finds the pipeline drained (the previous overlapped draw's path tracing done
-    // when it is submitted) starts a chain: the next depth - 1 draws each wait for the path-tracing kernel of
-    // the draw before them (ev_trace_end), so that the frames of a restarted pipeline start one after the
-    // other, as in the steady state, instead of all at once
-    bool stagger = false;
-    hipEvent_t ev_trace_end[kDepthMax] = {};
-    unsigned chain_start = 0;
-    int last_str = -1;            // the stream of the last overlapped draw (-1: none since the last serial draw)
     unsigned mk_seq = 0;          // megakernel draws so far (buffer set mk_seq % (depth + lag), stream mk_seq % depth)
     bool need_fresh = true;       // the next megakernel draw must wait for everything before it (a fresh mark)
     unsigned mark_floor = 0;      // no draw waits for a mark older than draw mark_floor's
@@ -691,7 +683,6 @@ int overlap_init(Dev* c)
             HIPCHK(c, hipStreamCreateWithFlags(&c->ts[p], hipStreamNonBlocking));
         }
         HIPCHK(c, hipEventCreateWithFlags(&c->ev_traced[p], hipEventDisableTiming));
-        HIPCHK(c, hipEventCreateWithFlags(&c->ev_trace_end[p], hipEventDisableTiming));
     }
     return PT_OK;
 }
@@ -1024,15 +1015,8 @@ int render_trace(DevFx* fx, DevTex* target)
         // this stream is ordered by the stream
         const unsigned w = k + 1 >= D ? std::max(k + 1 - D, c->mark_floor) : c->mark_floor;
         HIPCHK(c, hipStreamWaitEvent(ts, c->ev_mark[w % D], 0));
-        if (c->stagger) {
-            const bool drained = c->last_str < 0 || hipEventQuery(c->ev_traced[c->last_str]) == hipSuccess;
-            if (drained || c->mark_floor == k) c->chain_start = k;
-            const unsigned pos = k - c->chain_start;
-            if (pos >= 1 && pos < (unsigned)depth) HIPCHK(c, hipStreamWaitEvent(ts, c->ev_trace_end[c->last_str], 0));
-        }
     } else {
         c->need_fresh = true;
-        c->last_str = -1;
     }
     if (lpt) {
         if (!same) HIPCHK(c, hipMemsetAsync(c->lpt_cost(par), 0, 4 * n * sizeof(unsigned), ts));   // costs start afresh
@@ -1046,8 +1030,6 @@ int render_trace(DevFx* fx, DevTex* target)
     if (!a.order && c->xcd_blocked) a.order_zig = 2u;
     if (int rc = begin_draw(c, fx->prog, ts)) return rc;
     HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, ts));
-    if (overlap && c->stagger && c->mk_seq - c->chain_start + 1 < (unsigned)depth)
-        HIPCHK(c, hipEventRecord(c->ev_trace_end[str], ts));
     if (cont) {   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
         HIPCHK(c, pt_launch_cont(fx->prog, &a, (int)std::min<size_t>(c->cont_waves, (size_t)gx * gy * 4), ts));
         c->cont_draws++;
@@ -1058,7 +1040,6 @@ int render_trace(DevFx* fx, DevTex* target)
     if (overlap) {
         HIPCHK(c, hipEventRecord(c->ev_traced[str], ts));
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_traced[str], 0));
-        c->last_str = str;
     }
     // the history half of main() on the main stream, where the copy / output draws that read the
     // accumulation follow
@@ -1246,7 +1227,6 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_MAIN_WAVES")) c->main_waves = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
-    if (const char* v = std::getenv("PT_STAGGER")) c->stagger = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_MOVING_SERIAL")) c->moving_serial = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP_DEPTH")) {
         c->depth = std::min(Dev::kDepthMax, std::max(2, std::atoi(v)));
@@ -1312,7 +1292,6 @@ void dev_ctx_destroy(Dev* c)
     for (int p = 0; p < Dev::kDepthMax; p++) {   // (every side-stream draw was waited for by a blend on the main stream)
         if (c->ts[p]) { hipStreamSynchronize(c->ts[p]); hipStreamDestroy(c->ts[p]); }
         if (c->ev_traced[p]) hipEventDestroy(c->ev_traced[p]);
-        if (c->ev_trace_end[p]) hipEventDestroy(c->ev_trace_end[p]);
     }
     if (c->gb_mem) hipFree(c->gb_mem);
     if (c->d_err) hipFree(c->d_err);
