@@ -368,6 +368,21 @@ def latency_summary(lat, ms_per_step):
                           "complete, main stream); every event_every-th frame of the timed region"}
 
 
+def timing_fields(kernel_ms, launches, lat, ms_per_step, event_every):
+    """The line's kernel-timing fields: the sampled HIP-event spans per draw kind, the frame latency and the
+    spans' sum against the step (event windows add their own stream time around the bracketed draws: a sum
+    above the step time flags sampled spans inflated by them - or, with frames overlapping, spans that share
+    the GPU)."""
+    ksum = sum(kernel_ms.values())
+    return {"kernel_timing": ("HIP events around the draws of every %d-th timed frame (%d launches); pathtrace = the "
+                              "span of a frame's path tracing on its side stream (pt_trace, then pt_cont when the "
+                              "draw compacts), which overlaps the neighbouring frames' spans" % (event_every, launches)),
+            "kernel_ms": kernel_ms,
+            "frame_latency_ms": latency_summary(lat, ms_per_step),
+            "kernel_sum_ms": round(ksum, 4),
+            "kernel_sum_exceeds_step": bool(ksum > ms_per_step)}
+
+
 def timed_region(engine, step, first, count, event_every, barrier_sync, program):
     """`count` steps from frame index `first`, bracketed by barrier_sync, with HIP-event windows around
     every event_every-th draw of each kind. Returns (elapsed s, kernel_ms dict, bracketed launches,
@@ -934,7 +949,6 @@ def main():
                                "%s (+ pt_cont<...> when the draws compact) of one frame" % kernel, note)
     roofline["kernel"] = kernel
     roofline["bvh_walk"] = layout
-    ksum = sum(kernel_ms.values())
     line = {
         "metric": baseline_metric() if args.workload == "dragon" else METRICS[args.workload],
         "value": round(value, 2),
@@ -954,15 +968,7 @@ def main():
                               "of own bands, async RCCL gather of RGBA8 bands to rank 0 overlapping the next "
                               "frame") if world > 1 else None},
         "pathtrace_span_mpaths_per_s": round(W * Hh / (avg_span_ms * 1e-3) / 1e6 * world, 2),
-        "kernel_timing": ("HIP events around the draws of every %d-th timed frame (%d launches); pathtrace = the "
-                          "span of a frame's path tracing on its side stream (pt_trace, then pt_cont when the draw "
-                          "compacts), which overlaps the neighbouring frames' spans" % (event_every, pt_n)),
-        "kernel_ms": kernel_ms,
-        "frame_latency_ms": latency_summary(lat, ms_per_step),
-        # event windows add their own stream time around the bracketed draws: a sum above the step
-        # time flags sampled kernel times inflated by them
-        "kernel_sum_ms": round(ksum, 4),
-        "kernel_sum_exceeds_step": bool(ksum > ms_per_step),
+        **timing_fields(kernel_ms, pt_n, lat, ms_per_step, event_every),
         "late_bounce_compaction": comp,
         "roofline": roofline,
     }

@@ -180,3 +180,33 @@ def test_frame_latency_summary():
     assert (s["p50"], s["max"], s["frames"], s["p50_per_step"]) == (2.75, 9.0, 4, 2.75)
     assert bench.latency_summary([1.5, 0.5, 1.0], 0.5)["p50"] == 1.0
     assert bench.latency_summary([], 1.0) is None
+
+
+class _FakeEngine:
+    """timing_begin / timing_end / timing_latency as libpt's window reports them (no GPU)."""
+    def __init__(self):
+        self.began = False
+
+    def timing_begin(self):
+        self.began = True
+
+    def timing_end(self, kind):
+        return {"gltf": (10.0, 5), "screenCopy": (0.0, 0), "screenOutput": (0.5, 5)}[kind]
+
+    def timing_latency(self, kind):
+        return [2.0, 2.5, 2.25, 3.0, 2.1]
+
+
+def test_every_line_carries_frame_latency():
+    """The timed region returns the window's per-frame latencies, and the line's timing fields (bench.py
+    timing_fields, shared by the headline) carry frame_latency_ms {p50, max} next to the kernel spans."""
+    sys.path.insert(0, ROOT)
+    import bench
+    e = _FakeEngine()
+    steps = []
+    el, km, n, lat = bench.timed_region(e, steps.append, 5, 4, 1, lambda: None, "gltf")
+    assert e.began and steps == [5, 6, 7, 8] and n == 5 and km["pathtrace"] == 2.0 and len(lat) == 5
+    f = bench.timing_fields(km, n, lat, 0.8, 1)
+    assert f["frame_latency_ms"]["p50"] == 2.25 and f["frame_latency_ms"]["max"] == 3.0
+    assert f["frame_latency_ms"]["p50_per_step"] == round(2.25 / 0.8, 3)
+    assert f["kernel_sum_exceeds_step"] is True and f["kernel_ms"] is km
