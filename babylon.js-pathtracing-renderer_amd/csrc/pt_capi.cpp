@@ -218,6 +218,7 @@ struct Dev {
     // in one band of the frame (orderBuild). 6: dragon stand-in 4K +1.6-2.2 %, helmet 4K +8 %, sky + dragon 4K
     // +0.9 %, bunny 4K ±0 (profiles/r06g_frames_lpt_flat_4k.log); 1080p frames keep the whole order
     int lpt_flat = 6;
+    unsigned lpt_flat_tiles = 8192;   // (PT_LPT_FLAT_TILES) ... for frames of more than this many tiles
     unsigned split_dominance = 8;   // ... when the slowest wave costs this many times the mean (PT_SPLIT_ALWAYS=1: 0)
     // the order build of the last megakernel draw, deferred to run as an extra block of the next
     // screenOutput pass (pt_output) instead of a kernel of its own; any other draw, stream switch or
@@ -1049,7 +1050,7 @@ int render_trace(DevFx* fx, DevTex* target)
     if (a.cost) {   // this draw's costs order draw k + 2: the build rides along with the next screenOutput
         c->pending_order = { true, (unsigned)n, a.cost, c->lpt_order(par), c->lpt_split(par),
                              (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance,
-                             c->split_near | ((c->lpt_flat + 1) << 8) };
+                             c->split_near | ((c->lpt_flat + 1) << 8) | (int)((c->lpt_flat_tiles / 64u) << 16) };
         if (!c->fuse_order) { if (int rc = flush_order(c)) return rc; }
         c->lpt_key[par] = { true, n, target, fx->prog, c->part, c->num_parts };
     }
@@ -1242,6 +1243,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_CONT_WAVES")) c->cont_waves = (unsigned)std::max(1, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_AUTO_PIXELS")) c->cont_auto_pixels = (size_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_LPT_FLAT")) c->lpt_flat = std::max(-1, std::min(127, std::atoi(v)));
+    if (const char* v = std::getenv("PT_LPT_FLAT_TILES")) c->lpt_flat_tiles = (unsigned)std::max(0, std::min(1 << 21, std::atoi(v)));
     if (const char* v = std::getenv("PT_SPLIT_NEAR")) c->split_near = std::max(1, std::min(128, std::atoi(v)));
     if (const char* v = std::getenv("PT_SPLIT_ALWAYS")) c->split_dominance = std::atoi(v) ? 0u : 8u;
     if (const char* v = std::getenv("PT_BVH_LAYOUT"))   // reference | pairs | trail: the context's initial walk

@@ -50,7 +50,8 @@ PT_D int costBucket(unsigned dur)
 // bucket by bucket, slowest bucket first; within a bucket the order is whatever the LDS atomics
 // give - any permutation renders the same bits, only the schedule changes.
 // (one block of 1024 threads as its own kernel, or of 256 as the extra block of pt_output)
-// near_arg: near_buckets (bits 0-7) | (flat + 1) << 8 (bits 8-15, 0 = no flattening): with flat >= 0, every
+// near_arg: near_buckets (bits 0-7) | (flat + 1) << 8 (bits 8-15, 0 = no flattening) | the least tiles / 64 of a
+// flattened frame << 16: with flat >= 0, every
 // bucket more than `flat` below the slowest tile's is dealt as one bucket, in (about) row-major order - the
 // slowest tiles still start first, the bulk of the frame sweeps down the screen, so the tiles in flight at
 // once lie in one band (their BVH working set shared in each XCD's L2)
@@ -61,7 +62,8 @@ PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, uns
     __shared__ unsigned long long total;
     __shared__ unsigned slowest;
     __shared__ unsigned floorB;
-    const int near_buckets = near_arg & 255, flat = (near_arg >> 8) - 1;
+    const int near_buckets = near_arg & 255, flat = ((near_arg >> 8) & 255) - 1;
+    const unsigned flat_min = (unsigned)(near_arg >> 16) * 64u;   // flattening from this many tiles up
     for (int b = threadIdx.x; b < kCostBuckets; b += blockDim.x) cnt[b] = 0;
     if (threadIdx.x == 0) { total = 0; slowest = 0; }
     __syncthreads();
@@ -138,7 +140,7 @@ PT_D void orderBuild(unsigned ntiles, const unsigned* cost, unsigned* order, uns
         }
         // flattening: the buckets below fl dealt as bucket fl (their counts folded into it) - for frames of more
         // than 8192 tiles (4K); at 1080p it lost on the helmet and StanfordBunny (-1.4 %, -2.5 %)
-        const int fl = flat >= 0 && ntiles > kOrderHeld * 64u ? max(0, top - flat) : 0;
+        const int fl = flat >= 0 && ntiles > flat_min ? max(0, top - flat) : 0;
         unsigned below = (2 * l < fl ? c0 : 0u) + (2 * l + 1 < fl ? c1 : 0u);
         for (int o = 32; o > 0; o >>= 1) below += (unsigned)__shfl_xor((int)below, o, 64);
         unsigned f0 = 2 * l < fl ? 0u : c0, f1 = 2 * l + 1 < fl ? 0u : c1;
