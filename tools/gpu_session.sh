@@ -18,7 +18,7 @@
 #   prof                       rocprofv3 --kernel-trace --stats of the exact command's workload (20 steps + 5 warmup)
 #   pmc[:W]                    the five PMC passes over tools/prof_frames.py (default workload dragon)
 #   rankpx:ROUNDS:WORLD:ENVS   tools/rank_proxy.py (rank 0's share of the 4K dragon frame at N = WORLD) per setting
-#   profw:W                    rocprofv3 kernel trace + stats of bench.py --workload W (50 frames after 100)
+#   profw:W[:WxH]              rocprofv3 kernel trace + stats of bench.py --workload W (50 frames after 100)
 #   ktrace:K                   rocprofv3 --kernel-trace --stats over the GPU tests matching -k K
 set -o pipefail   # a step's status is its GPU command's, not that of a `| tail` after it
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -82,8 +82,9 @@ for step in "$@"; do
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$R/gpurun_out/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 --cpu-budget 0 --no-pmc --no-anchors) > "$LOG" 2>&1 ;;
     profw)    # profw:W - rocprofv3 kernel trace + stats of bench.py --workload W (50 frames after 100)
+      sz=""; [ -n "$a2" ] && sz="--size $a2"
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$R/gpurun_out/prof_${TAG}_$a1" -o run -- python3 "$R/bench.py" --workload "$a1" --steps 50 --warmup 100 \
+        -d "$R/gpurun_out/prof_${TAG}_$a1" -o run -- python3 "$R/bench.py" --workload "$a1" $sz --steps 50 --warmup 100 \
         --cpu-budget 0 --no-pmc --no-anchors) > "$LOG" 2>&1 ;;
     ktrace)   # rocprofv3 --kernel-trace --stats over the GPU tests matching -k a1
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
