@@ -231,6 +231,7 @@ struct Dev {
     // for four on one CU (r05bi: dragon stand-in 1080p +2 %, helmet +3 %; at 4K -4 %, so only up to 8192
     // tiles)
     int main_waves = 16384;
+    size_t blend_1w_tiles = pt::kOrderHeld * 64u;   // (PT_BLEND_1W_TILES) pt_blend in one-wave form up to this many tiles
     unsigned* lpt_mem = nullptr;            // cost[kSetsMax][4 * cap] | order[kSetsMax][cap] | split[kSetsMax]
     size_t lpt_cap = 0;
     struct LptKey { bool valid; size_t n; const void* target; int prog, part, parts; };
@@ -1046,7 +1047,7 @@ int render_trace(DevFx* fx, DevTex* target)
     // accumulation follow
     pt::BlendArgs b{ a.width, a.height, a.num_parts, a.part, a.frame, a.moving, a.rad, a.prev, a.out, a.cont_count };
     // (one-wave workgroups up to 8192 tiles, as the output pass below)
-    HIPCHK(c, pt_launch_blend(&b, gy, c->stream, n <= pt::kOrderHeld * 64u ? c->main_waves : 0));
+    HIPCHK(c, pt_launch_blend(&b, gy, c->stream, n <= c->blend_1w_tiles ? c->main_waves : 0));
     if (a.cost) {   // this draw's costs order draw k + 2: the build rides along with the next screenOutput
         c->pending_order = { true, (unsigned)n, a.cost, c->lpt_order(par), c->lpt_split(par),
                              (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance,
@@ -1227,6 +1228,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_SPLIT_TILES")) c->split_tiles = (unsigned)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_MAIN_WAVES")) c->main_waves = std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("PT_BLEND_1W_TILES")) c->blend_1w_tiles = (size_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_MOVING_SERIAL")) c->moving_serial = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP_DEPTH")) {
