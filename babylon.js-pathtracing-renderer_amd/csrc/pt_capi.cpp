@@ -232,6 +232,11 @@ struct Dev {
     // tiles)
     int main_waves = 16384;
     size_t blend_1w_tiles = pt::kOrderHeld * 64u;   // (PT_BLEND_1W_TILES) pt_blend in one-wave form up to this many tiles
+    size_t out_1w_tiles = pt::kOrderHeld * 64u;     // (PT_OUT_1W_TILES) pt_output likewise, when no order build rides along
+    // (PT_ORDER_SIDE_TILES) frames of more tiles than this, drawn without lag, build their longest-first order
+    // as a one-wave block on their own side stream after the traced event, instead of riding along with the
+    // next screenOutput (which then needs no 4-wave block)
+    size_t order_side_tiles = ~(size_t)0;
     unsigned* lpt_mem = nullptr;            // cost[kSetsMax][4 * cap] | order[kSetsMax][cap] | split[kSetsMax]
     size_t lpt_cap = 0;
     struct LptKey { bool valid; size_t n; const void* target; int prog, part, parts; };
@@ -992,7 +997,13 @@ int render_trace(DevFx* fx, DevTex* target)
         cont_args(c, par, a);
     }
     if (lpt && c->lpt_cap < n) {
-        if (c->lpt_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->lpt_mem)); c->lpt_mem = nullptr; }
+        if (c->lpt_mem) {   // (side-stream order builds write it after their traced event: every stream first)
+            HIPCHK(c, hipStreamSynchronize(c->stream));
+            for (int p = 0; p < Dev::kDepthMax; p++)
+                if (c->ts[p]) HIPCHK(c, hipStreamSynchronize(c->ts[p]));
+            HIPCHK(c, hipFree(c->lpt_mem));
+            c->lpt_mem = nullptr;
+        }
         HIPCHK(c, hipMalloc(&c->lpt_mem, (5 * n + 1) * Dev::kSetsMax * sizeof(unsigned)));   // cost | order | split
         c->lpt_cap = n;
         c->need_fresh = true;
@@ -1039,9 +1050,17 @@ int render_trace(DevFx* fx, DevTex* target)
     // the draw's timing events bracket all of its path tracing on the side stream: pt_trace and, when the
     // draw compacts, pt_cont (the blend below is the main stream's)
     if (int rc = end_draw(c, fx->prog, ts)) return rc;
+    const int near_arg = c->split_near | ((c->lpt_flat + 1) << 8) | (int)((c->lpt_flat_tiles / 64u) << 16);
+    const unsigned split_cap = (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u;
+    bool side_order = false;
     if (overlap) {
         HIPCHK(c, hipEventRecord(c->ev_traced[str], ts));
         HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_traced[str], 0));
+        // the set's next draw runs on this stream (no lag), so the order it reads is built by then
+        side_order = a.cost && lag == 0 && n > c->order_side_tiles;
+        if (side_order)
+            HIPCHK(c, pt_launch_order_build((unsigned)n, a.cost, c->lpt_order(par), c->lpt_split(par), split_cap,
+                                            c->split_dominance, near_arg, ts, 64));
     }
     // the history half of main() on the main stream, where the copy / output draws that read the
     // accumulation follow
@@ -1049,10 +1068,11 @@ int render_trace(DevFx* fx, DevTex* target)
     // (one-wave workgroups up to 8192 tiles, as the output pass below)
     HIPCHK(c, pt_launch_blend(&b, gy, c->stream, n <= c->blend_1w_tiles ? c->main_waves : 0));
     if (a.cost) {   // this draw's costs order draw k + 2: the build rides along with the next screenOutput
-        c->pending_order = { true, (unsigned)n, a.cost, c->lpt_order(par), c->lpt_split(par),
-                             (unsigned)std::min<size_t>(c->split_tiles, n) & ~7u, c->split_dominance,
-                             c->split_near | ((c->lpt_flat + 1) << 8) | (int)((c->lpt_flat_tiles / 64u) << 16) };
-        if (!c->fuse_order) { if (int rc = flush_order(c)) return rc; }
+        if (!side_order) {
+            c->pending_order = { true, (unsigned)n, a.cost, c->lpt_order(par), c->lpt_split(par), split_cap,
+                                 c->split_dominance, near_arg };
+            if (!c->fuse_order) { if (int rc = flush_order(c)) return rc; }
+        }
         c->lpt_key[par] = { true, n, target, fx->prog, c->part, c->num_parts };
     }
     c->mk_seq++;
@@ -1148,7 +1168,8 @@ int render_output(DevFx* fx, DevTex* target)
         // ~2 MP, and a rank's share of 4K), else the 4-wave blocks with a 256-thread order build
         const int nb = (a.height + 15) / 16, ob = a.part < nb ? (nb - a.part + a.num_parts - 1) / a.num_parts : 0;
         const unsigned tiles = (unsigned)((a.width + 15) / 16) * (unsigned)ob;   // (as pt_launch_output's grid)
-        const bool one = tiles <= pt::kOrderHeld * 64u && (!a.ob_cost || a.ob_ntiles <= pt::kOrderHeld * 64u);
+        const bool one = a.ob_cost ? tiles <= pt::kOrderHeld * 64u && a.ob_ntiles <= pt::kOrderHeld * 64u
+                                   : tiles <= c->out_1w_tiles;
         HIPCHK(c, pt_launch_output(&a, c->stream, one ? c->main_waves : 0));
     }
     return end_draw(c, fx->prog);
@@ -1229,6 +1250,8 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_FUSE_ORDER")) c->fuse_order = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_MAIN_WAVES")) c->main_waves = std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_BLEND_1W_TILES")) c->blend_1w_tiles = (size_t)std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("PT_OUT_1W_TILES")) c->out_1w_tiles = (size_t)std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("PT_ORDER_SIDE_TILES")) c->order_side_tiles = (size_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_OVERLAP")) c->overlap = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_MOVING_SERIAL")) c->moving_serial = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_OVERLAP_DEPTH")) {
@@ -1275,6 +1298,8 @@ void dev_ctx_destroy(Dev* c)
     c->pending_copy.on = false;   // nothing can observe its target any more
     c->pending_order.on = false;  // ... nor a next draw the order
     if (c->stream) hipStreamSynchronize(c->stream);
+    for (int p = 0; p < Dev::kDepthMax; p++)   // (side-stream order builds may still write the order arrays)
+        if (c->ts[p]) hipStreamSynchronize(c->ts[p]);
     std::vector<DevFx*> fx(c->effects.begin(), c->effects.end());
     for (auto* f : fx) dev_effect_destroy(f);
     std::vector<DevTex*> tx(c->textures.begin(), c->textures.end());
@@ -1684,6 +1709,8 @@ int dev_queue_stats(Dev* c, uint32_t out[16])
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = flush_order(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int q = 0; q < Dev::kDepthMax; q++)   // (a side-stream order build may still write the split count)
+        if (c->ts[q]) HIPCHK(c, hipStreamSynchronize(c->ts[q]));
     const int p = (int)(c->mk_seq % (unsigned)(c->depth_run + c->lag_run));   // the tiles the next megakernel draw of the same grid splits
     if (c->lpt_mem && c->lpt_key[p].valid)
         HIPCHK(c, hipMemcpy(&out[7], c->lpt_split(p), sizeof(uint32_t), hipMemcpyDeviceToHost));
