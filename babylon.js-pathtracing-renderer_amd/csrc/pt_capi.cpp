@@ -1276,7 +1276,16 @@ Dev* dev_ctx_create(int device, int* err)
                                                                                   : PT_BVH_PAIRS;
     if (const char* v = std::getenv("PT_PERSIST_REFILL")) c->persist_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    if (e == hipSuccess) {
+        // (experiment, PT_MAIN_PRIO=1) the context's stream - blend, copy, output - at the device's highest
+        // priority, so that its small kernels take freed CU slots before the side streams' path tracing
+        const char* mp = std::getenv("PT_MAIN_PRIO");
+        int least = 0, greatest = 0;
+        if (mp && std::atoi(mp) != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+            e = hipStreamCreateWithPriority(&c->own_stream, hipStreamNonBlocking, greatest);
+        else
+            e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+    }
     c->stream = c->own_stream;
     if (e == hipSuccess) e = hipMalloc(&c->d_err, 256);
     if (e == hipSuccess) e = hipMalloc(&c->d_counters, pt::C_NUM * sizeof(unsigned long long));
