@@ -133,6 +133,13 @@ struct TraceArgs {
     unsigned* cont_aux;     // per record: the pixel (py * width + px) | the 2x2 edge flag << 31
     unsigned* cont_count;   // [0] records stored by this draw, [1] pt_cont's queue head (both zeroed by the draw's pt_blend)
     unsigned cont_bounce, cont_lanes, cont_refill;
+    // (PT_CONT_SORT) pt_cont takes the records ordered by a ray key (pt_trace.h contRank): per record its key and
+    // its rank among the key's records (pt_trace), the keys' totals (NULL: no sort), the order (pt_cont_scatter)
+    unsigned short* cont_key;
+    unsigned* cont_rank;
+    unsigned* cont_bins;
+    const unsigned* cont_perm;
+    float cont_cell[3];          // the key's origin cells: (o - model box min) * cont_cell, 0..3 per axis
     Tex8 bluenoise;
     const float4* aabb;
     long long aabb_texels;
@@ -236,6 +243,18 @@ struct BlendArgs {
     const float4* prev;
     float4* out;
     unsigned* cont_count;   // late-bounce compaction: the draw's record counter, zeroed here (NULL: none)
+    unsigned* cont_bins;    // (PT_CONT_SORT) the record sort's kSortBins totals, zeroed here (NULL: none)
+};
+
+// (PT_CONT_SORT) pt_cont's records ordered by a ray key (pt_kernels.hip pt_cont_hist / pt_cont_scatter)
+constexpr int kSortBins = 1024;
+struct SortArgs {
+    const unsigned* count;        // [0] records stored by the draw
+    const unsigned short* key;    // per record (pt_trace)
+    const unsigned* rank;         // per record: its place among its key's records (pt_trace)
+    const unsigned* bins;         // the keys' totals
+    unsigned* perm;
+    unsigned chunk;               // pt_cont_scatter: records per workgroup
 };
 
 struct CopyArgs {

@@ -34,6 +34,7 @@ hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned
                                  unsigned split_cap, unsigned dominance, int near_buckets, hipStream_t s, int threads);
 hipError_t pt_launch_copy(const pt::CopyArgs* a, int grid_x, int grid_y, hipStream_t s);
 hipError_t pt_launch_blend(const pt::BlendArgs* a, int bands, hipStream_t s, int waves);
+hipError_t pt_launch_cont_sort(const pt::SortArgs* a, size_t cap, hipStream_t s);
 hipError_t pt_launch_cont(int prog, const pt::TraceArgs* a, int waves, hipStream_t s);
 hipError_t pt_launch_output(const pt::OutputArgs* a, hipStream_t s, int waves);
 hipError_t pt_launch_math_probe(int op, const float* x, const float* y, float* out, int n, hipStream_t s);
@@ -175,6 +176,7 @@ struct Dev {
     size_t cont_cap = 0;          // records per buffer set ...
     int cont_sets = 0;            // ... and buffer sets allocated
     unsigned cont_bounce = 2, cont_lanes = 48, cont_refill = 16, cont_waves = 2048;
+    int cont_sort = 1;            // (PT_CONT_SORT) pt_cont takes its records ordered by a ray key (0: as stored)
     // auto mode: compaction pays on the heavy 4K frames (sky + dragon +19 %, dragon stand-in +10 %) and
     // costs elsewhere (bunny 4K -22 %, helmet -9 %, rank-sized frames -29 %: profiles/r05i_*), which
     // the draw's arguments do not tell apart. So the draws of one target / program / partition time it:
@@ -557,6 +559,15 @@ size_t traced_pixels(const Dev* c, const DevTex* target)
 // buffer sets: per set records [cap x 64 B] | pixels [cap x 4 B] | counter; the counters start at zero here,
 // afterwards each draw's pt_blend zeroes its own. (Sized by the partition's pixels and the sets its draws
 // cycle through, not the whole target times every set: a 4K frame's records are 0.53 GB per set.)
+// bytes of one buffer set for `paths` records: records [paths x 64 B] | pixels [x 4 B] | (PT_CONT_SORT: order
+// [x 4 B] | ranks [x 4 B] | keys [x 2 B] | the keys' totals) | counter
+size_t cont_bytes(const Dev* c, size_t paths)
+{
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    size_t per = paths * 64 + al(paths * 4) + 256;
+    if (c->cont_sort) per += 2 * al(paths * 4) + al(paths * 2) + pt::kSortBins * 4;
+    return per;
+}
 int cont_reserve(Dev* c, size_t paths, int sets)
 {
     if (paths <= c->cont_cap && sets <= c->cont_sets) return PT_OK;
@@ -565,7 +576,7 @@ int cont_reserve(Dev* c, size_t paths, int sets)
     if (c->cont_mem) { HIPCHK(c, hipStreamSynchronize(c->stream)); HIPCHK(c, hipFree(c->cont_mem)); c->cont_mem = nullptr; }
     c->cont_cap = 0;
     c->cont_sets = 0;
-    const size_t per = paths * 64 + ((paths * 4 + 255) & ~(size_t)255) + 256;
+    const size_t per = cont_bytes(c, paths);
     HIPCHK(c, hipMalloc(&c->cont_mem, (size_t)sets * per));
     // on the main stream (hipMemset would go to the null stream, which the non-blocking side streams do
     // not wait for: the next draw's atomics raced with it); the next draw's path tracing waits for a mark
@@ -578,11 +589,15 @@ int cont_reserve(Dev* c, size_t paths, int sets)
 }
 void cont_args(Dev* c, int p, pt::TraceArgs& a)
 {
-    const size_t per = c->cont_cap * 64 + ((c->cont_cap * 4 + 255) & ~(size_t)255) + 256;
+    const size_t per = cont_bytes(c, c->cont_cap);
     char* m = (char*)c->cont_mem + (size_t)p * per;
     a.cont_rec = (float4*)m;
     a.cont_aux = (unsigned*)(m + c->cont_cap * 64);
     a.cont_count = (unsigned*)(m + per - 256);
+    a.cont_perm = nullptr;
+    a.cont_rank = nullptr;
+    a.cont_key = nullptr;
+    a.cont_bins = nullptr;
     a.cont_bounce = std::max(2u, c->cont_bounce);   // the G-buffer's normal / colour / id are final from bounce 2
     a.cont_lanes = c->cont_lanes;
     a.cont_refill = c->cont_refill;
@@ -1042,7 +1057,31 @@ int render_trace(DevFx* fx, DevTex* target)
     a.ntiles = (unsigned)n;
     if (!a.order && c->xcd_blocked) a.order_zig = 2u;
     if (int rc = begin_draw(c, fx->prog, ts)) return rc;
+    if (cont && c->cont_sort && a.bvh_walk != pt::WALK_REF) {   // (the model's root box: child-pair walks only)
+        const size_t cap = c->cont_cap;
+        auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        char* m = (char*)a.cont_rec + cap * 64 + al(cap * 4);
+        a.cont_perm = (unsigned*)m;
+        a.cont_rank = (unsigned*)(m + al(cap * 4));
+        a.cont_key = (unsigned short*)(m + 2 * al(cap * 4));
+        a.cont_bins = (unsigned*)(m + 2 * al(cap * 4) + al(cap * 2));
+        for (int k = 0; k < 3; k++) {
+            const float ext = a.bvh_root_box[3 + k] - a.bvh_root_box[k];
+            a.cont_cell[k] = ext > 0.0f ? 4.0f / ext : 0.0f;
+        }
+    }
     HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, ts));
+    if (a.cont_bins) {   // (PT_CONT_SORT) the records' order, from the keys' totals and ranks pt_trace took
+        pt::SortArgs so;
+        std::memset(&so, 0, sizeof(so));
+        so.count = a.cont_count;
+        so.key = a.cont_key;
+        so.rank = a.cont_rank;
+        so.bins = a.cont_bins;
+        so.perm = (unsigned*)a.cont_perm;
+        so.chunk = 2048;
+        HIPCHK(c, pt_launch_cont_sort(&so, c->cont_cap, ts));
+    }
     if (cont) {   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
         HIPCHK(c, pt_launch_cont(fx->prog, &a, (int)std::min<size_t>(c->cont_waves, (size_t)gx * gy * 4), ts));
         c->cont_draws++;
@@ -1064,7 +1103,7 @@ int render_trace(DevFx* fx, DevTex* target)
     }
     // the history half of main() on the main stream, where the copy / output draws that read the
     // accumulation follow
-    pt::BlendArgs b{ a.width, a.height, a.num_parts, a.part, a.frame, a.moving, a.rad, a.prev, a.out, a.cont_count };
+    pt::BlendArgs b{ a.width, a.height, a.num_parts, a.part, a.frame, a.moving, a.rad, a.prev, a.out, a.cont_count, a.cont_bins };
     // (one-wave workgroups up to 8192 tiles, as the output pass below)
     HIPCHK(c, pt_launch_blend(&b, gy, c->stream, n <= c->blend_1w_tiles ? c->main_waves : 0));
     if (a.cost) {   // this draw's costs order draw k + 2: the build rides along with the next screenOutput
@@ -1265,6 +1304,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_CONT_BOUNCE")) c->cont_bounce = (unsigned)std::max(2, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_LANES")) c->cont_lanes = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_REFILL")) c->cont_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
+    if (const char* v = std::getenv("PT_CONT_SORT")) c->cont_sort = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_CONT_WAVES")) c->cont_waves = (unsigned)std::max(1, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_AUTO_PIXELS")) c->cont_auto_pixels = (size_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_LPT_FLAT")) c->lpt_flat = std::max(-1, std::min(127, std::atoi(v)));

@@ -238,6 +238,8 @@ __global__ __launch_bounds__(256) void pt_blend(BlendArgs a)
     const int x = blockIdx.x * 64 + (threadIdx.x & 63);
     const int r0 = band * kTile + (threadIdx.x >> 6);
     if (a.cont_count && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 2) a.cont_count[threadIdx.x] = 0u;   // counter, queue head (pt_cont is done)
+    if (a.cont_bins && blockIdx.x == 0 && blockIdx.y == 0)
+        for (int i = threadIdx.x; i < kSortBins; i += 256) a.cont_bins[i] = 0u;
     if (x >= a.width) return;
     blendRows(a, x, r0);
 }
@@ -247,6 +249,8 @@ __global__ __launch_bounds__(256) void pt_blend(BlendArgs a)
 __global__ __launch_bounds__(64) void pt_blend_w(BlendArgs a, int units_x, int units)
 {
     if (a.cont_count && blockIdx.x == 0 && threadIdx.x < 2) a.cont_count[threadIdx.x] = 0u;
+    if (a.cont_bins && blockIdx.x == 0)
+        for (int i = threadIdx.x; i < kSortBins; i += 64) a.cont_bins[i] = 0u;
     for (int u = blockIdx.x; u < units; u += gridDim.x) {
         const int cx = u % units_x, rest = u / units_x;
         const int band = (rest >> 2) * a.num_parts + a.part;
@@ -638,6 +642,35 @@ __global__ void pt_math_probe_kernel(int op, const float* x, const float* y, flo
     out[i] = r;
 }
 
+// ------------------------------------------------------------------------------ pt_cont's record order
+// (experiment, PT_CONT_SORT) between pt_trace and pt_cont on the draw's side stream: the records in the order
+// of their ray keys (pt_trace.h contRank) - a counting sort whose counts and ranks pt_trace took as it stored
+// the records, so this pass only places them: perm[first place of the key + rank] = record. One-wave
+// workgroups of `chunk` records each; every workgroup forms the keys' first places from the totals.
+__global__ __launch_bounds__(64) void pt_cont_scatter(SortArgs s)
+{
+    __shared__ unsigned off[kSortBins];
+    const unsigned lane = threadIdx.x;
+    const unsigned n = *s.count;
+    const unsigned begin = blockIdx.x * s.chunk, end = min(n, begin + s.chunk);
+    if (begin >= end) return;
+    constexpr int kPer = kSortBins / 64;   // consecutive keys per lane
+    unsigned v[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) { v[k] = s.bins[kPer * lane + k]; sum += v[k]; }
+    unsigned inc = sum;   // inclusive scan over the lanes
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned o = __shfl_up(inc, d, 64);
+        if (lane >= (unsigned)d) inc += o;
+    }
+    unsigned run = inc - sum;
+#pragma unroll
+    for (int k = 0; k < kPer; k++) { off[kPer * lane + k] = run; run += v[k]; }
+    __syncthreads();
+    for (unsigned i = begin + lane; i < end; i += 64u) s.perm[off[s.key[i]] + s.rank[i]] = i;
+}
+
 } // namespace pt
 
 // ------------------------------------------------------------------------------ launchers
@@ -680,6 +713,14 @@ hipError_t pt_launch_cont(int prog, const pt::TraceArgs* a, int waves, hipStream
     case pt::WALK_TRAIL: return pt_launch_cont_trail(prog, a, grid, s);
     default: return hipErrorInvalidValue;
     }
+}
+
+// (PT_CONT_SORT) the record order of a draw's pt_cont: up to `cap` records
+hipError_t pt_launch_cont_sort(const pt::SortArgs* a, size_t cap, hipStream_t s)
+{
+    const unsigned blocks = (unsigned)((cap + a->chunk - 1) / a->chunk);
+    hipLaunchKernelGGL(pt::pt_cont_scatter, dim3(blocks ? blocks : 1), dim3(64), 0, s, *a);
+    return hipGetLastError();
 }
 
 hipError_t pt_launch_order_build(unsigned ntiles, const unsigned* cost, unsigned* order, unsigned* split,

@@ -240,6 +240,42 @@ struct GBits {
     }
 };
 
+// (experiment, PT_CONT_SORT) a stored record's ray key - whether the ray samples the light (the any-hit
+// walk), the origin's cell in a 4x4x4 grid over the model's box (Morton order), the direction's octant -
+// and its rank among the key's records: the lanes of one key found by a ballot per distinct key, then one
+// atomic per key (all in one instruction) on the key's total. pt_cont_scatter places the records by them.
+PT_D void contRank(const TraceArgs& a, int slot, const Path& p, const PState& s, bool inside)
+{
+    unsigned key = 0u;
+    if (inside) {
+        const float* rb = a.bvh_root_box;
+        const f3 o = mul(a.model, p.ro, 1.0f);
+        const unsigned cx = (unsigned)min(3, max(0, (int)((o.x - rb[0]) * a.cont_cell[0])));
+        const unsigned cy = (unsigned)min(3, max(0, (int)((o.y - rb[1]) * a.cont_cell[1])));
+        const unsigned cz = (unsigned)min(3, max(0, (int)((o.z - rb[2]) * a.cont_cell[2])));
+        auto spread = [](unsigned v) { return (v & 1u) | ((v & 2u) << 2); };
+        const unsigned oct = (p.rd.x < 0.0f ? 1u : 0u) | (p.rd.y < 0.0f ? 2u : 0u) | (p.rd.z < 0.0f ? 4u : 0u);
+        key = (s.sampleLight ? 512u : 0u) | ((spread(cx) | (spread(cy) << 1) | (spread(cz) << 2)) << 3) | oct;
+    }
+    unsigned long long todo = __ballot(inside), peers = 0ull;
+    while (todo) {   // (wave-uniform)
+        const int lead = __ffsll((long long)todo) - 1;
+        const unsigned k = __shfl(key, lead, 64);
+        const bool mine = inside && key == k;
+        const unsigned long long m = __ballot(mine);
+        if (mine) peers = m;
+        todo &= ~m;
+    }
+    const int leader = inside ? __ffsll((long long)peers) - 1 : (int)__lane_id();
+    unsigned base = 0u;
+    if (inside && (int)__lane_id() == leader) base = atomicAdd(&a.cont_bins[key], (unsigned)__popcll(peers));
+    base = __shfl(base, leader, 64);
+    if (inside) {
+        a.cont_key[slot] = (unsigned short)key;
+        a.cont_rank[slot] = base + (unsigned)__popcll(peers & ((1ull << __lane_id()) - 1ull));
+    }
+}
+
 // CalculateRadiance's loop. With late-bounce compaction (a.cont_rec): after a bounce >= cont_bounce, when
 // at most cont_lanes of the wave's lanes are still looping (all at the same bounce: a ballot, wave-uniform),
 // they leave the loop together and store their paths for pt_cont; `slot` is then the record's index (-1:
@@ -267,6 +303,7 @@ PT_D f3 radiance(const TraceArgs& a, Path& p, G& g, float2* lds, unsigned lane_s
                 slot = (int)(base + (unsigned)__popcll(st & ((1ull << __lane_id()) - 1ull)));
                 contStore(a, (unsigned)slot, p, s);
             }
+            if (a.cont_bins) contRank(a, slot, p, s, inside);
             break;
         }
     }
@@ -521,8 +558,8 @@ __global__ __launch_bounds__(kTraceBlock, kMinWaves<PROG>) void pt_cont(TraceArg
             if (!alive) {
                 const unsigned q = base + (unsigned)__popcll(dead & below);
                 if (q < n) {
-                    slot = q;
-                    contLoad(a, q, p, s);
+                    slot = a.cont_perm ? a.cont_perm[q] : q;
+                    contLoad(a, slot, p, s);
                     accum = mk(0, 0, 0);
                     alive = true;
                 }
