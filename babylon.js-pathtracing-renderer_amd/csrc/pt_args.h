@@ -139,7 +139,8 @@ struct TraceArgs {
     unsigned* cont_rank;
     unsigned* cont_bins;
     const unsigned* cont_perm;
-    float cont_cell[3];          // the key's origin cells: (o - model box min) * cont_cell, 0..3 per axis
+    float cont_cell[3];          // the key's origin cells: (o - model box min) * cont_cell, 0..2^cont_grid_bits - 1 per axis
+    unsigned cont_grid_bits, cont_key_mode;
     Tex8 bluenoise;
     const float4* aabb;
     long long aabb_texels;
@@ -247,7 +248,7 @@ struct BlendArgs {
 };
 
 // (PT_CONT_SORT) pt_cont's records ordered by a ray key (pt_kernels.hip pt_cont_hist / pt_cont_scatter)
-constexpr int kSortBins = 1024;
+constexpr int kSortBins = 8192;   // at most: light flag x 8 octants x 8^3 cells
 struct SortArgs {
     const unsigned* count;        // [0] records stored by the draw
     const unsigned short* key;    // per record (pt_trace)
@@ -255,6 +256,7 @@ struct SortArgs {
     const unsigned* bins;         // the keys' totals
     unsigned* perm;
     unsigned chunk;               // pt_cont_scatter: records per workgroup
+    unsigned nbins;               // keys in use (a multiple of 64, <= kSortBins)
 };
 
 struct CopyArgs {

@@ -177,6 +177,7 @@ struct Dev {
     int cont_sets = 0;            // ... and buffer sets allocated
     unsigned cont_bounce = 2, cont_lanes = 48, cont_refill = 16, cont_waves = 2048;
     int cont_sort = 1;            // (PT_CONT_SORT) pt_cont takes its records ordered by a ray key (0: as stored)
+    unsigned cont_grid_bits = 2, cont_key_mode = 0;   // (PT_CONT_SORT_GRID, PT_CONT_SORT_KEY) the key's cells, field order
     // auto mode: compaction pays on the heavy 4K frames (sky + dragon +19 %, dragon stand-in +10 %) and
     // costs elsewhere (bunny 4K -22 %, helmet -9 %, rank-sized frames -29 %: profiles/r05i_*), which
     // the draw's arguments do not tell apart. So the draws of one target / program / partition time it:
@@ -1067,8 +1068,10 @@ int render_trace(DevFx* fx, DevTex* target)
         a.cont_bins = (unsigned*)(m + 2 * al(cap * 4) + al(cap * 2));
         for (int k = 0; k < 3; k++) {
             const float ext = a.bvh_root_box[3 + k] - a.bvh_root_box[k];
-            a.cont_cell[k] = ext > 0.0f ? 4.0f / ext : 0.0f;
+            a.cont_cell[k] = ext > 0.0f ? (float)(1u << c->cont_grid_bits) / ext : 0.0f;
         }
+        a.cont_grid_bits = c->cont_grid_bits;
+        a.cont_key_mode = c->cont_key_mode;
     }
     HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, ts));
     if (a.cont_bins) {   // (PT_CONT_SORT) the records' order, from the keys' totals and ranks pt_trace took
@@ -1080,6 +1083,7 @@ int render_trace(DevFx* fx, DevTex* target)
         so.bins = a.cont_bins;
         so.perm = (unsigned*)a.cont_perm;
         so.chunk = 2048;
+        so.nbins = 16u << (3u * c->cont_grid_bits);
         HIPCHK(c, pt_launch_cont_sort(&so, c->cont_cap, ts));
     }
     if (cont) {   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
@@ -1305,6 +1309,8 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_CONT_LANES")) c->cont_lanes = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_REFILL")) c->cont_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_SORT")) c->cont_sort = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PT_CONT_SORT_GRID")) c->cont_grid_bits = (unsigned)std::min(3, std::max(1, std::atoi(v)));
+    if (const char* v = std::getenv("PT_CONT_SORT_KEY")) c->cont_key_mode = (unsigned)std::min(2, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_WAVES")) c->cont_waves = (unsigned)std::max(1, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_AUTO_PIXELS")) c->cont_auto_pixels = (size_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_LPT_FLAT")) c->lpt_flat = std::max(-1, std::min(127, std::atoi(v)));

@@ -643,21 +643,17 @@ __global__ void pt_math_probe_kernel(int op, const float* x, const float* y, flo
 }
 
 // ------------------------------------------------------------------------------ pt_cont's record order
-// (experiment, PT_CONT_SORT) between pt_trace and pt_cont on the draw's side stream: the records in the order
-// of their ray keys (pt_trace.h contRank) - a counting sort whose counts and ranks pt_trace took as it stored
-// the records, so this pass only places them: perm[first place of the key + rank] = record. One-wave
-// workgroups of `chunk` records each; every workgroup forms the keys' first places from the totals.
-__global__ __launch_bounds__(64) void pt_cont_scatter(SortArgs s)
+// (PT_CONT_SORT) between pt_trace and pt_cont on the draw's side stream: the records in the order of their
+// ray keys (pt_trace.h contRank) - a counting sort whose counts and ranks pt_trace took as it stored the
+// records, so what is left is the keys' first places (one wave: an exclusive scan of the totals, in place)
+// and placing the records: perm[first place of the key + rank] = record. No LDS in either kernel: beside the
+// path-tracing waves, which fill every CU's LDS, a workgroup that needs some waits for a wave to end.
+__global__ __launch_bounds__(64) void pt_cont_offsets(SortArgs s)
 {
-    __shared__ unsigned off[kSortBins];
-    const unsigned lane = threadIdx.x;
-    const unsigned n = *s.count;
-    const unsigned begin = blockIdx.x * s.chunk, end = min(n, begin + s.chunk);
-    if (begin >= end) return;
-    constexpr int kPer = kSortBins / 64;   // consecutive keys per lane
-    unsigned v[kPer], sum = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; k++) { v[k] = s.bins[kPer * lane + k]; sum += v[k]; }
+    const unsigned lane = threadIdx.x, per = s.nbins / 64u;   // consecutive keys per lane
+    unsigned* const bins = (unsigned*)s.bins;
+    unsigned sum = 0;
+    for (unsigned k = 0; k < per; k++) sum += bins[per * lane + k];
     unsigned inc = sum;   // inclusive scan over the lanes
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -665,10 +661,17 @@ __global__ __launch_bounds__(64) void pt_cont_scatter(SortArgs s)
         if (lane >= (unsigned)d) inc += o;
     }
     unsigned run = inc - sum;
-#pragma unroll
-    for (int k = 0; k < kPer; k++) { off[kPer * lane + k] = run; run += v[k]; }
-    __syncthreads();
-    for (unsigned i = begin + lane; i < end; i += 64u) s.perm[off[s.key[i]] + s.rank[i]] = i;
+    for (unsigned k = 0; k < per; k++) {
+        const unsigned v = bins[per * lane + k];
+        bins[per * lane + k] = run;
+        run += v;
+    }
+}
+__global__ __launch_bounds__(64) void pt_cont_scatter(SortArgs s)
+{
+    const unsigned n = *s.count;
+    const unsigned begin = blockIdx.x * s.chunk, end = min(n, begin + s.chunk);
+    for (unsigned i = begin + threadIdx.x; i < end; i += 64u) s.perm[s.bins[s.key[i]] + s.rank[i]] = i;
 }
 
 } // namespace pt
@@ -719,6 +722,7 @@ hipError_t pt_launch_cont(int prog, const pt::TraceArgs* a, int waves, hipStream
 hipError_t pt_launch_cont_sort(const pt::SortArgs* a, size_t cap, hipStream_t s)
 {
     const unsigned blocks = (unsigned)((cap + a->chunk - 1) / a->chunk);
+    hipLaunchKernelGGL(pt::pt_cont_offsets, dim3(1), dim3(64), 0, s, *a);
     hipLaunchKernelGGL(pt::pt_cont_scatter, dim3(blocks ? blocks : 1), dim3(64), 0, s, *a);
     return hipGetLastError();
 }

@@ -250,12 +250,18 @@ PT_D void contRank(const TraceArgs& a, int slot, const Path& p, const PState& s,
     if (inside) {
         const float* rb = a.bvh_root_box;
         const f3 o = mul(a.model, p.ro, 1.0f);
-        const unsigned cx = (unsigned)min(3, max(0, (int)((o.x - rb[0]) * a.cont_cell[0])));
-        const unsigned cy = (unsigned)min(3, max(0, (int)((o.y - rb[1]) * a.cont_cell[1])));
-        const unsigned cz = (unsigned)min(3, max(0, (int)((o.z - rb[2]) * a.cont_cell[2])));
-        auto spread = [](unsigned v) { return (v & 1u) | ((v & 2u) << 2); };
+        const unsigned gb = a.cont_grid_bits;
+        const int top = (1 << gb) - 1;
+        const unsigned cx = (unsigned)min(top, max(0, (int)((o.x - rb[0]) * a.cont_cell[0])));
+        const unsigned cy = (unsigned)min(top, max(0, (int)((o.y - rb[1]) * a.cont_cell[1])));
+        const unsigned cz = (unsigned)min(top, max(0, (int)((o.z - rb[2]) * a.cont_cell[2])));
+        auto spread = [](unsigned v) { return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4); };   // bits 0-2 -> 0, 3, 6
+        const unsigned cell = spread(cx) | (spread(cy) << 1) | (spread(cz) << 2);
         const unsigned oct = (p.rd.x < 0.0f ? 1u : 0u) | (p.rd.y < 0.0f ? 2u : 0u) | (p.rd.z < 0.0f ? 4u : 0u);
-        key = (s.sampleLight ? 512u : 0u) | ((spread(cx) | (spread(cy) << 1) | (spread(cz) << 2)) << 3) | oct;
+        const unsigned lt = s.sampleLight ? 1u : 0u;
+        key = a.cont_key_mode == 1u ? (lt << (3u + 3u * gb)) | (oct << (3u * gb)) | cell   // octant-major
+            : a.cont_key_mode == 2u ? (cell << 3) | oct                                   // no light flag
+            : (lt << (3u + 3u * gb)) | (cell << 3) | oct;
     }
     unsigned long long todo = __ballot(inside), peers = 0ull;
     while (todo) {   // (wave-uniform)
