@@ -976,6 +976,10 @@ int render_trace(DevFx* fx, DevTex* target)
     bool cont = false;
     int depth = c->depth;
     if (int rc = cont_decide(c, target, fx->prog, mesh && !c->counting && !PT_SECPROF_BUILD, &cont, &depth)) return rc;
+    // a moving-camera draw that runs alone (PT_MOVING_SERIAL) does not compact: with no next frame beside it,
+    // pt_cont's tail (a wave waits for its longest chain of walks) is the frame's (dragon stand-in 1080p
+    // 1.19 -> 1.09 ms per frame, profiles/r06af_movpx.log); its slowest tiles are split instead
+    if (a.moving && c->moving_serial) cont = false;
     const size_t traced = (size_t)target->w * target->h / (size_t)std::max(1, c->num_parts);   // (about)
     const int lag = draw_lag(c, traced);
     if (depth != c->depth_run || lag != c->lag_run) {   // another buffer-set cycle: the draw waits for everything before it

@@ -77,6 +77,18 @@ for step in "$@"; do
         done
       done
       (exit $rc) ;;
+    movpx)    # movpx:ROUNDS:ENVS - tools/moving_proxy.py (the moving-camera anchor) per setting
+      : > "$LOG"; rc=0
+      for r in $(seq "$a1"); do
+        IFS='|' read -ra ENVS <<< "$a2"
+        for cfg in "${ENVS[@]}"; do
+          envs=""; [ "$cfg" != "-" ] && envs="${cfg//,/ }"
+          res=$(set -o pipefail; env $envs timeout -k 10 200 python3 tools/moving_proxy.py 2>&1 | tail -1); rc=$?
+          echo "r$r [$cfg] $res" >> "$LOG"
+          [ $rc -ne 0 ] && break 2
+        done
+      done
+      (exit $rc) ;;
     wavetime) mkdir -p "gpurun_out/wt_$TAG"; PT_LIBPT=$a1 run 300 "$LOG" python3 tools/wavetime.py "gpurun_out/wt_$TAG" ${a2//,/ } ;;
     prof)
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
