@@ -178,6 +178,7 @@ struct Dev {
     unsigned cont_bounce = 2, cont_lanes = 48, cont_refill = 16, cont_waves = 2048;
     int cont_sort = 1;            // (PT_CONT_SORT) pt_cont takes its records ordered by a ray key (0: as stored)
     unsigned cont_grid_bits = 2, cont_key_mode = 0;   // (PT_CONT_SORT_GRID, PT_CONT_SORT_KEY) the key's cells, field order
+    unsigned sort_chunk = 512;    // (PT_CONT_SORT_CHUNK) records per pt_cont_scatter workgroup (2048: ±0, 8192: -1 to -5 %)
     // auto mode: compaction pays on the heavy 4K frames (sky + dragon +19 %, dragon stand-in +10 %) and
     // costs elsewhere (bunny 4K -22 %, helmet -9 %, rank-sized frames -29 %: profiles/r05i_*), which
     // the draw's arguments do not tell apart. So the draws of one target / program / partition time it:
@@ -1086,7 +1087,7 @@ int render_trace(DevFx* fx, DevTex* target)
         so.rank = a.cont_rank;
         so.bins = a.cont_bins;
         so.perm = (unsigned*)a.cont_perm;
-        so.chunk = 2048;
+        so.chunk = c->sort_chunk;
         so.nbins = 16u << (3u * c->cont_grid_bits);
         HIPCHK(c, pt_launch_cont_sort(&so, c->cont_cap, ts));
     }
@@ -1313,6 +1314,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_CONT_LANES")) c->cont_lanes = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_REFILL")) c->cont_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_SORT")) c->cont_sort = std::atoi(v) != 0;
+    if (const char* v = std::getenv("PT_CONT_SORT_CHUNK")) c->sort_chunk = (unsigned)std::max(64, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_SORT_GRID")) c->cont_grid_bits = (unsigned)std::min(3, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_SORT_KEY")) c->cont_key_mode = (unsigned)std::min(2, std::max(0, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_WAVES")) c->cont_waves = (unsigned)std::max(1, std::atoi(v));

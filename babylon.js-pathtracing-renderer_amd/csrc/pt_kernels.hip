@@ -653,6 +653,7 @@ __global__ __launch_bounds__(64) void pt_cont_offsets(SortArgs s)
     const unsigned lane = threadIdx.x, per = s.nbins / 64u;   // consecutive keys per lane
     unsigned* const bins = (unsigned*)s.bins;
     unsigned sum = 0;
+#pragma unroll 16
     for (unsigned k = 0; k < per; k++) sum += bins[per * lane + k];
     unsigned inc = sum;   // inclusive scan over the lanes
 #pragma unroll
@@ -671,7 +672,24 @@ __global__ __launch_bounds__(64) void pt_cont_scatter(SortArgs s)
 {
     const unsigned n = *s.count;
     const unsigned begin = blockIdx.x * s.chunk, end = min(n, begin + s.chunk);
-    for (unsigned i = begin + threadIdx.x; i < end; i += 64u) s.perm[s.bins[s.key[i]] + s.rank[i]] = i;
+    // eight records per lane at a time, their loads issued together (each record is a chain of three:
+    // key -> the key's first place -> the store)
+    for (unsigned i0 = begin + threadIdx.x; i0 < end; i0 += 8u * 64u) {
+        unsigned key[8], rank[8], at[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const unsigned i = i0 + 64u * k;
+            key[k] = i < end ? (unsigned)s.key[i] : 0u;
+            rank[k] = i < end ? s.rank[i] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) at[k] = s.bins[key[k]];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const unsigned i = i0 + 64u * k;
+            if (i < end) s.perm[at[k] + rank[k]] = i;
+        }
+    }
 }
 
 } // namespace pt
