@@ -259,6 +259,14 @@ PT_D void contRank(const TraceArgs& a, int slot, const Path& p, const PState& s,
         const unsigned cell = spread(cx) | (spread(cy) << 1) | (spread(cz) << 2);
         const unsigned oct = (p.rd.x < 0.0f ? 1u : 0u) | (p.rd.y < 0.0f ? 2u : 0u) | (p.rd.z < 0.0f ? 4u : 0u);
         const unsigned lt = s.sampleLight ? 1u : 0u;
+        if (a.cont_key_mode == 3u) {   // 24 directions: the major axis and its sign (cube face), the quadrant
+            const float ax = fabsf(p.rd.x), ay = fabsf(p.rd.y), az = fabsf(p.rd.z);
+            const unsigned face = ax >= ay && ax >= az ? 0u : ay >= az ? 1u : 2u;
+            const float m = face == 0u ? p.rd.x : face == 1u ? p.rd.y : p.rd.z;
+            const float u = face == 0u ? p.rd.y : p.rd.x, v = face == 2u ? p.rd.y : p.rd.z;
+            const unsigned dir = ((face * 2u + (m < 0.0f ? 1u : 0u)) << 2) | (u < 0.0f ? 1u : 0u) | (v < 0.0f ? 2u : 0u);
+            key = (lt << (5u + 3u * gb)) | (cell << 5) | dir;
+        } else
         key = a.cont_key_mode == 1u ? (lt << (3u + 3u * gb)) | (oct << (3u * gb)) | cell   // octant-major
             : a.cont_key_mode == 2u ? (cell << 3) | oct                                   // no light flag
             : (lt << (3u + 3u * gb)) | (cell << 3) | oct;

@@ -328,14 +328,22 @@ def test_overlapped_frames_observed_between_draws(engine, size):
         assert _bits_equal(want, got), "%s, frame %d: %s" % (what, i, _diff_report(want, got))
 
 
-@pytest.mark.parametrize("layout", ["pairs", "trail"])
-def test_late_bounce_compaction_1080p_bitexact(monkeypatch, layout):
+@pytest.mark.parametrize("layout,order", [("pairs", "keys"), ("trail", "keys"), ("pairs", "stored"),
+                                          ("pairs", "octant-major 8x8x8")])
+def test_late_bounce_compaction_1080p_bitexact(monkeypatch, layout, order):
     """Late-bounce compaction forced on (PT_CONT=1, from bounce 2 for waves with <= 48 live paths, the
     default PT_CONT_LANES: the
     pt_trace<P,false,true> variant stores them, pt_cont runs them packed on the draw's side stream):
-    the dragon stand-in's four recorded 1920x1080 frames, accumulation and canvas bit-exact."""
+    the dragon stand-in's four recorded 1920x1080 frames, accumulation and canvas bit-exact - with pt_cont
+    taking the records in ray-key order (the default: 4x4x4 cells, light flag first), in store order
+    (PT_CONT_SORT=0), and in the 8192-key octant-major order (PT_CONT_SORT_GRID=3, PT_CONT_SORT_KEY=1)."""
     import babylon_pt as bp
     monkeypatch.setenv("PT_CONT", "1")
+    if order == "stored":
+        monkeypatch.setenv("PT_CONT_SORT", "0")
+    elif order != "keys":
+        monkeypatch.setenv("PT_CONT_SORT_GRID", "3")
+        monkeypatch.setenv("PT_CONT_SORT_KEY", "1")
     e = bp.Engine(0)
     try:
         e.set_bvh_layout(layout)
