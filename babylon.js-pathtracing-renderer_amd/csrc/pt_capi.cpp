@@ -1088,7 +1088,7 @@ int render_trace(DevFx* fx, DevTex* target)
         so.bins = a.cont_bins;
         so.perm = (unsigned*)a.cont_perm;
         so.chunk = c->sort_chunk;
-        so.nbins = (c->cont_key_mode == 3u ? 64u : 16u) << (3u * c->cont_grid_bits);
+        so.nbins = (c->cont_key_mode == 3u ? 64u : c->cont_key_mode == 4u ? 32u : 16u) << (3u * c->cont_grid_bits);
         HIPCHK(c, pt_launch_cont_sort(&so, c->cont_cap, ts));
     }
     if (cont) {   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
@@ -1316,8 +1316,8 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_CONT_SORT")) c->cont_sort = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_CONT_SORT_CHUNK")) c->sort_chunk = (unsigned)std::max(64, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_SORT_GRID")) c->cont_grid_bits = (unsigned)std::min(3, std::max(1, std::atoi(v)));
-    if (const char* v = std::getenv("PT_CONT_SORT_KEY")) c->cont_key_mode = (unsigned)std::min(3, std::max(0, std::atoi(v)));
-    if (c->cont_key_mode == 3u) c->cont_grid_bits = std::min(2u, c->cont_grid_bits);   // (at most kSortBins keys)
+    if (const char* v = std::getenv("PT_CONT_SORT_KEY")) c->cont_key_mode = (unsigned)std::min(4, std::max(0, std::atoi(v)));
+    if (c->cont_key_mode >= 3u) c->cont_grid_bits = std::min(2u, c->cont_grid_bits);   // (at most kSortBins keys)
     if (const char* v = std::getenv("PT_CONT_WAVES")) c->cont_waves = (unsigned)std::max(1, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_AUTO_PIXELS")) c->cont_auto_pixels = (size_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_LPT_FLAT")) c->lpt_flat = std::max(-1, std::min(127, std::atoi(v)));

@@ -269,6 +269,8 @@ PT_D void contRank(const TraceArgs& a, int slot, const Path& p, const PState& s,
         } else
         key = a.cont_key_mode == 1u ? (lt << (3u + 3u * gb)) | (oct << (3u * gb)) | cell   // octant-major
             : a.cont_key_mode == 2u ? (cell << 3) | oct                                   // no light flag
+            : a.cont_key_mode == 4u   // the paths with more bounces left first (longest first), then as mode 0
+                ? (lt << (4u + 3u * gb)) | (((unsigned)s.bounce > a.cont_bounce ? 1u : 0u) << (3u + 3u * gb)) | (cell << 3) | oct
             : (lt << (3u + 3u * gb)) | (cell << 3) | oct;
     }
     unsigned long long todo = __ballot(inside), peers = 0ull;
