@@ -104,11 +104,12 @@ for step in "$@"; do
         --timeout 300 --timeout-method thread -k "$a1") > "$LOG" 2>&1 ;;
     pmc)
       W=${a1:-dragon}; OUT="$R/gpurun_out/pmc_$TAG"; mkdir -p "$OUT"; i=0; rc=0
+      SZ=""; [ -n "$a2" ] && SZ="--width ${a2%x*} --height ${a2#*x}"   # pmc:W[:WxH]
       for C in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES" \
                "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE" "SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_ANY SQ_INSTS_BRANCH"; do
         i=$((i + 1))
         (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $C --output-format csv -d "$OUT/p$i" -o run \
-          -- python3 "$R/tools/prof_frames.py" --workload "$W" --frames 10) > "$OUT/p$i.log" 2>&1 || { rc=$?; break; }
+          -- python3 "$R/tools/prof_frames.py" --workload "$W" $SZ --frames 10) > "$OUT/p$i.log" 2>&1 || { rc=$?; break; }
       done
       (exit $rc) ;;
     *) echo "unknown step $step" >> "$SLOG"; exit 2 ;;
