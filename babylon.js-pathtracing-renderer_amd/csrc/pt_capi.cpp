@@ -176,6 +176,13 @@ struct Dev {
     size_t cont_cap = 0;          // records per buffer set ...
     int cont_sets = 0;            // ... and buffer sets allocated
     unsigned cont_bounce = 2, cont_lanes = 48, cont_refill = 16, cont_waves = 2048;
+    // pt_cont's waves for draws that trace at least cont_big_pixels (PT_CONT_WAVES_BIG, PT_CONT_BIG_PIXELS): beside
+    // a 4K frame's path tracing fewer of them leave more wave slots to the next frames (dragon stand-in 4K
+    // +3.2 to +3.9 %, helmet 4K +0.9 %, a rank's half of the 4K frame +1.5 %, 2560x1440 +1.1 %; 1080p keeps
+    // 2048: 1536 there -1.8 %; profiles/r06bc_*, r06bd_*, r06be_*)
+    unsigned cont_waves_big = 1024;
+    size_t cont_big_pixels = 3000000;
+    bool cont_waves_env = false;
     int cont_sort = 1;            // (PT_CONT_SORT) pt_cont takes its records ordered by a ray key (0: as stored)
     unsigned cont_grid_bits = 2, cont_key_mode = 0;   // (PT_CONT_SORT_GRID, PT_CONT_SORT_KEY) the key's cells, field order
     unsigned sort_chunk = 512;    // (PT_CONT_SORT_CHUNK) records per pt_cont_scatter workgroup (2048: ±0, 8192: -1 to -5 %)
@@ -1092,7 +1099,9 @@ int render_trace(DevFx* fx, DevTex* target)
         HIPCHK(c, pt_launch_cont_sort(&so, c->cont_cap, ts));
     }
     if (cont) {   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
-        HIPCHK(c, pt_launch_cont(fx->prog, &a, (int)std::min<size_t>(c->cont_waves, (size_t)gx * gy * 4), ts));
+        // (the sky composite keeps 2048: its sky pixels store few records, and 1024 waves cost it 0.5 %)
+        const bool big = !c->cont_waves_env && traced >= c->cont_big_pixels && fx->prog != PT_PROG_SKY_MESH;
+        HIPCHK(c, pt_launch_cont(fx->prog, &a, (int)std::min<size_t>(big ? c->cont_waves_big : c->cont_waves, (size_t)gx * gy * 4), ts));
         c->cont_draws++;
     }
     // the draw's timing events bracket all of its path tracing on the side stream: pt_trace and, when the
@@ -1318,7 +1327,9 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_CONT_SORT_GRID")) c->cont_grid_bits = (unsigned)std::min(3, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_SORT_KEY")) c->cont_key_mode = (unsigned)std::min(4, std::max(0, std::atoi(v)));
     if (c->cont_key_mode >= 3u) c->cont_grid_bits = std::min(2u, c->cont_grid_bits);   // (at most kSortBins keys)
-    if (const char* v = std::getenv("PT_CONT_WAVES")) c->cont_waves = (unsigned)std::max(1, std::atoi(v));
+    if (const char* v = std::getenv("PT_CONT_WAVES")) { c->cont_waves = (unsigned)std::max(1, std::atoi(v)); c->cont_waves_env = true; }
+    if (const char* v = std::getenv("PT_CONT_WAVES_BIG")) c->cont_waves_big = (unsigned)std::max(1, std::atoi(v));
+    if (const char* v = std::getenv("PT_CONT_BIG_PIXELS")) c->cont_big_pixels = (size_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_CONT_AUTO_PIXELS")) c->cont_auto_pixels = (size_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("PT_LPT_FLAT")) c->lpt_flat = std::max(-1, std::min(127, std::atoi(v)));
     if (const char* v = std::getenv("PT_LPT_FLAT_TILES")) c->lpt_flat_tiles = (unsigned)std::max(0, std::min(1 << 21, std::atoi(v)));
