@@ -16,7 +16,8 @@
 #                              a workload W@WxH runs at that frame size
 #   wavetime:LIB:WLS           wave timeline + CU occupancy of a -DPT_SECPROF build (tools/wavetime.py)
 #   prof                       rocprofv3 --kernel-trace --stats of the exact command's workload (20 steps + 5 warmup)
-#   pmc[:W]                    the five PMC passes over tools/prof_frames.py (default workload dragon)
+#   pmc[:W[:WxH]]              the five PMC passes over tools/prof_frames.py (default workload dragon), at a frame size
+#   movpx:ROUNDS:ENVS          tools/moving_proxy.py (the moving-camera anchor) per setting
 #   rankpx:ROUNDS:WORLD:ENVS   tools/rank_proxy.py (rank 0's share of the 4K dragon frame at N = WORLD) per setting
 #   profw:W[:WxH]              rocprofv3 kernel trace + stats of bench.py --workload W (50 frames after 100)
 #   ktrace:K                   rocprofv3 --kernel-trace --stats over the GPU tests matching -k K
