@@ -185,6 +185,7 @@ struct Dev {
     bool cont_waves_env = false;
     int cont_sort = 1;            // (PT_CONT_SORT) pt_cont takes its records ordered by a ray key (0: as stored)
     unsigned cont_grid_bits = 2, cont_key_mode = 0;   // (PT_CONT_SORT_GRID, PT_CONT_SORT_KEY) the key's cells, field order
+    bool cont_grid_env = false;
     unsigned sort_chunk = 512;    // (PT_CONT_SORT_CHUNK) records per pt_cont_scatter workgroup (2048: ±0, 8192: -1 to -5 %)
     // auto mode: compaction pays on the heavy 4K frames (sky + dragon +19 %, dragon stand-in +10 %) and
     // costs elsewhere (bunny 4K -22 %, helmet -9 %, rank-sized frames -29 %: profiles/r05i_*), which
@@ -1078,11 +1079,14 @@ int render_trace(DevFx* fx, DevTex* target)
         a.cont_rank = (unsigned*)(m + al(cap * 4));
         a.cont_key = (unsigned short*)(m + 2 * al(cap * 4));
         a.cont_bins = (unsigned*)(m + 2 * al(cap * 4) + al(cap * 2));
+        // 8x8x8 cells for draws that trace 3 Mpx or more (4K: dragon stand-in +0.4 %, helmet +1.1 %, sky +
+        // dragon +0.6 %, three rounds, profiles/r06bj_*; at 1080p the helmet lost 5.5 % with them, r06ao_*)
+        const unsigned gb = c->cont_grid_env || c->cont_key_mode >= 3u || traced < c->cont_big_pixels ? c->cont_grid_bits : 3u;
         for (int k = 0; k < 3; k++) {
             const float ext = a.bvh_root_box[3 + k] - a.bvh_root_box[k];
-            a.cont_cell[k] = ext > 0.0f ? (float)(1u << c->cont_grid_bits) / ext : 0.0f;
+            a.cont_cell[k] = ext > 0.0f ? (float)(1u << gb) / ext : 0.0f;
         }
-        a.cont_grid_bits = c->cont_grid_bits;
+        a.cont_grid_bits = gb;
         a.cont_key_mode = c->cont_key_mode;
     }
     HIPCHK(c, pt_launch_trace(fx->prog, c->counting ? 1 : 0, &a, gx, a.split ? gy_grid : gy, ts));
@@ -1095,7 +1099,7 @@ int render_trace(DevFx* fx, DevTex* target)
         so.bins = a.cont_bins;
         so.perm = (unsigned*)a.cont_perm;
         so.chunk = c->sort_chunk;
-        so.nbins = (c->cont_key_mode == 3u ? 64u : c->cont_key_mode == 4u ? 32u : 16u) << (3u * c->cont_grid_bits);
+        so.nbins = (c->cont_key_mode == 3u ? 64u : c->cont_key_mode == 4u ? 32u : 16u) << (3u * a.cont_grid_bits);
         HIPCHK(c, pt_launch_cont_sort(&so, c->cont_cap, ts));
     }
     if (cont) {   // (its one-wave workgroups index the spill slab below the trace grid's lanes)
@@ -1324,7 +1328,7 @@ Dev* dev_ctx_create(int device, int* err)
     if (const char* v = std::getenv("PT_CONT_REFILL")) c->cont_refill = (unsigned)std::min(64, std::max(1, std::atoi(v)));
     if (const char* v = std::getenv("PT_CONT_SORT")) c->cont_sort = std::atoi(v) != 0;
     if (const char* v = std::getenv("PT_CONT_SORT_CHUNK")) c->sort_chunk = (unsigned)std::max(64, std::atoi(v));
-    if (const char* v = std::getenv("PT_CONT_SORT_GRID")) c->cont_grid_bits = (unsigned)std::min(3, std::max(1, std::atoi(v)));
+    if (const char* v = std::getenv("PT_CONT_SORT_GRID")) { c->cont_grid_bits = (unsigned)std::min(3, std::max(1, std::atoi(v))); c->cont_grid_env = true; }
     if (const char* v = std::getenv("PT_CONT_SORT_KEY")) c->cont_key_mode = (unsigned)std::min(4, std::max(0, std::atoi(v)));
     if (c->cont_key_mode >= 3u) c->cont_grid_bits = std::min(2u, c->cont_grid_bits);   // (at most kSortBins keys)
     if (const char* v = std::getenv("PT_CONT_WAVES")) { c->cont_waves = (unsigned)std::max(1, std::atoi(v)); c->cont_waves_env = true; }
